@@ -1,0 +1,269 @@
+/*
+ * pcs.h — C ABI of the MI355X (gfx950) HIP library behind pcs_amd.PointNetSegmentation.
+ *
+ * The reference (seokjuchung/point-cloud-cnn-segmentation, point_cloud_segmentation.py,
+ * cited P:<line>) has no native code: its hot path is PyTorch ATen ops called from
+ * PointNetSegmentation.forward (P:98-133), CrossEntropyLoss (P:216,251), autograd
+ * (P:254) and Adam (P:217,255).  Each entry point below replaces a group of those ATen
+ * calls; the comment on each cites the reference lines whose semantics it implements.
+ *
+ * Contract (all entry points):
+ *  - plain device pointers and sizes; no torch types.  The CALLER owns every buffer
+ *    (torch caching allocator); the library never allocates, frees or retains pointers.
+ *  - all work is enqueued on the given stream; no device synchronisation inside; no
+ *    global mutable state (safe from several host threads / processes).
+ *  - return 0 on success, a negative code on error (-hipError_t, or PCS_EINVAL);
+ *    pcs_last_error() returns a thread-local message.  No exceptions cross the ABI.
+ *  - activations are points-major [M, C] row-major (M = B*N rows, one per point,
+ *    scene-major), stored as fp32 (PCS_F32: parity path, exact-f32 MFMA) or bf16
+ *    (PCS_BF16: bench path, bf16 MFMA with fp32 accumulation and fp32 BN statistics).
+ *    Weights arrive as fp32 in the state-dict layout (Cout, Cin, 1) == [Cout, Cin].
+ */
+#ifndef PCS_H
+#define PCS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *pcs_stream_t; /* == hipStream_t */
+
+enum { PCS_F32 = 0, PCS_BF16 = 1 };
+enum { PCS_OK = 0, PCS_EINVAL = -1000 };
+
+/* prologue applied to an operand element A[m,k] as it is staged into LDS */
+enum {
+  PCS_PRO_RAW = 0,      /* a = A                                                        */
+  PCS_PRO_BNRELU = 1,   /* a = max(A*s[k] + t[k], 0) [* keep(m,k) * keep_scale]  P:106-127 */
+  PCS_PRO_BWD = 2,      /* a = alpha[k]*dZ[m,k] + beta[k] + gamma[k]*Y[m,k]   BN backward */
+  PCS_PRO_BWD_POOL = 3  /* a = beta[k] + gamma[k]*Y[m,k] + (m==am[b,k] ? sp[b,k] : 0)
+                           BN backward of bn_global fed by the max-pool (P:113-114)      */
+};
+
+/* epilogue of the points-major GEMM */
+enum {
+  PCS_EPI_FWD = 0,   /* y = acc + bias; store y; per-chunk BN statistics (mean, M2);
+                        optional per-chunk max/min + arg for the global max-pool          */
+  PCS_EPI_DGRAD = 1, /* v = acc (+addend) (*keep*keep_scale); dz = (Yp*s+t > 0) ? v : 0;
+                        store dz; per-chunk S1 = sum dz, S2 = sum dz*xhat                 */
+  PCS_EPI_RAW = 2    /* store acc                                                        */
+};
+
+/*
+ * Points-major GEMM  C[m, n] = sum_k pro(A)[m, k] * W[n, k]  (+ epilogue).
+ * Used for every 1x1 Conv1d forward (P:106-128) and every input-gradient (dgrad) of the
+ * backward (P:254).  Rows are processed in scene-aligned chunks (a chunk never straddles
+ * two clouds), so BN statistics, per-scene sums and the max-pool come out per scene.
+ */
+typedef struct {
+  int64_t num_scenes;   /* B */
+  int64_t scene_rows;   /* N: padded points per scene; M = B*N */
+  int32_t K;            /* reduction length (input channels) */
+  int32_t Ncols;        /* output channels */
+  int32_t dtype;        /* PCS_F32 | PCS_BF16 */
+  int32_t prologue;     /* PCS_PRO_* */
+  int32_t epilogue;     /* PCS_EPI_* */
+  int32_t chunks_per_scene; /* 0 = auto; pcs_gemm_geometry() reports the value used */
+  const void *A;        /* [M,K] dtype: Y_{l-1} (fwd) | dZ_l (PRO_BWD) | Y_l (PRO_BWD_POOL) */
+  const void *A2;       /* [M,K] dtype: Y_l (PRO_BWD) */
+  const float *pa;      /* [K] s (BNRELU) | alpha (BWD) */
+  const float *pb;      /* [K] t (BNRELU) | beta (BWD, BWD_POOL) */
+  const float *pc;      /* [K] gamma (BWD, BWD_POOL) */
+  const uint8_t *a_mask;/* [M, K/8] dropout keep bits (BNRELU) or NULL */
+  float a_keep_scale;   /* 1/(1-p) */
+  const int32_t *pool_idx; /* [B,K] argmax row (global index) (BWD_POOL) */
+  const float *pool_coef;  /* [B,K] alpha*dz at the argmax row (BWD_POOL) */
+  const void *W;        /* [Ncols, K] dtype */
+  void *C;              /* [M, Ncols] dtype output */
+  const float *bias;    /* [Ncols] (FWD) or NULL */
+  const float *scene_bias; /* [B, Ncols] per-scene bias (FWD; seg_conv1 global half) */
+  const void *addend;   /* [M, Ncols] dtype added before the mask (DGRAD) or NULL */
+  const uint8_t *c_mask;/* [M, Ncols/8] keep bits of the dropout after BN_{l-1} (DGRAD) */
+  float c_keep_scale;
+  const void *Yp;       /* [M, Ncols] dtype: Y_{l-1} (DGRAD) */
+  const float *es, *et; /* [Ncols] BN_{l-1} scale/shift (DGRAD ReLU mask) */
+  const float *emean, *erstd; /* [Ncols] BN_{l-1} batch mean / rstd (DGRAD S2) */
+  float *stats;         /* [B*chunks_per_scene, Ncols, 2] partials (FWD, DGRAD) or NULL */
+  float *pool;          /* [B*chunks_per_scene, Ncols, 4] (maxv, argmax, minv, argmin) or NULL */
+} pcs_gemm_args;
+
+/* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error. */
+int64_t pcs_gemm_geometry(pcs_gemm_args *args);
+/* Launch the GEMM. */
+int pcs_gemm(const pcs_gemm_args *args, pcs_stream_t stream);
+/* conv1 (Cin = input_dim = 4, P:70, P:106) forward: A = points f32 [M,4] (RAW), W f32
+ * [64,4]; epilogue PCS_EPI_FWD semantics (C in dtype, stats).  Same geometry rules. */
+int pcs_conv1_fwd(const pcs_gemm_args *args, pcs_stream_t stream);
+
+/*
+ * Weight gradient  dW[n, k] = sum_m dy[m, n] * x[m, k]   (autograd of P:106-128, P:254)
+ * dy = pro_dy(dZ, Y) (PCS_PRO_BWD or PCS_PRO_BWD_POOL), x = pro_x(X) (PCS_PRO_BNRELU or
+ * PCS_PRO_RAW).  The reduction over M is split into scene-aligned slices whose fp32
+ * partials are summed in a fixed order (deterministic).
+ */
+typedef struct {
+  int64_t num_scenes, scene_rows;
+  int32_t Cout, Cin;    /* dW is [Cout, Cin] */
+  int32_t dtype;
+  int32_t splits_per_scene; /* 0 = auto */
+  int32_t dy_mode;      /* PCS_PRO_BWD | PCS_PRO_BWD_POOL */
+  const void *dZ;       /* [M, Cout] */
+  const void *Y;        /* [M, Cout] */
+  const float *alpha, *beta, *gamma; /* [Cout] */
+  const int32_t *pool_idx; const float *pool_coef; /* [B, Cout] (BWD_POOL) */
+  int32_t x_mode;       /* PCS_PRO_BNRELU | PCS_PRO_RAW */
+  const void *X;        /* [M, Cin] dtype (f32 for conv1) */
+  const float *s, *t;   /* [Cin] */
+  const uint8_t *x_mask; float x_keep_scale;
+  float *partial;       /* workspace: pcs_wgrad_workspace() bytes */
+  float *dW;            /* [Cout, Cin] f32 output, row stride ldw */
+  int64_t ldw;          /* 0 = Cin */
+} pcs_wgrad_args;
+
+int64_t pcs_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_per_scene */
+int pcs_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream);
+int pcs_conv1_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream); /* X = points f32 */
+
+/*
+ * BatchNorm1d train-mode statistics (P:86-94 semantics used at P:106-127): merge the
+ * per-chunk (mean, M2) partials (Chan, fp64) into the batch mean / biased variance over
+ * all B*N rows (pads included), derive the fused affine y*scale+shift, and update the
+ * running buffers (momentum, unbiased variance) when update_running != 0.
+ * scene_sum[B, C] receives the per-scene sum of y (may be NULL).
+ */
+int pcs_bn_fwd_finalize(const float *stats, int64_t num_scenes, int64_t scene_rows,
+                        int32_t C, int32_t chunks_per_scene, int64_t rows_per_chunk,
+                        const float *gamma, const float *beta, float *running_mean,
+                        float *running_var, float momentum, float eps, int32_t update_running,
+                        float *mean, float *rstd, float *scale, float *shift,
+                        float *scene_sum, pcs_stream_t stream);
+/* eval-mode BatchNorm: scale/shift from the running buffers (P:432 eval path) */
+int pcs_bn_eval_coefs(const float *gamma, const float *beta, const float *running_mean,
+                      const float *running_var, float eps, int32_t C, float *scale,
+                      float *shift, pcs_stream_t stream);
+/*
+ * BatchNorm1d backward from per-chunk (S1 = sum dz, S2 = sum dz*xhat) partials:
+ * dy = alpha*dz + beta_c + gamma_c*y, dgamma = S2, dbeta = S1, and the conv-bias
+ * gradient sum_m dy.  scene_s1[B,C] (sum dz per scene) may be NULL.
+ */
+int pcs_bn_bwd_finalize(const float *stats, int64_t num_scenes, int64_t scene_rows, int32_t C,
+                        int32_t chunks_per_scene, const float *mean, const float *rstd,
+                        const float *gamma, const float *scene_sum, float *alpha,
+                        float *beta_c, float *gamma_c, float *dgamma, float *dbeta,
+                        float *dbias, float *scene_s1, pcs_stream_t stream);
+
+/*
+ * Global max-pool (P:114) from per-chunk max/min partials of the global_feat conv output:
+ * g[b,c] = max_n relu(y*s+t) taken at argmax (s>0) / argmin (s<0) of y; am = that row.
+ */
+int pcs_pool_finalize(const float *pool, int64_t num_scenes, int64_t scene_rows, int32_t C,
+                      int32_t chunks_per_scene, const float *s, const float *t, float *g,
+                      int32_t *am, float *ysel, pcs_stream_t stream);
+
+/* out[b, n] = bias[n] + sum_k W[n, col_off + k] * g[b, k]   (seg_conv1 global half, P:117-123) */
+int pcs_scene_gemv(const float *g, int64_t num_scenes, int32_t Kg, const float *W, int64_t ldw,
+                   int32_t col_off, const float *bias, int32_t Nout, float *out,
+                   pcs_stream_t stream);
+
+/*
+ * Backward through repeat+cat (P:117-120), the max-pool (P:114) and bn_global (P:113):
+ * from bn_seg1's backward coefficients builds csum[b,n] = sum_{rows of b} dy_seg1[:, n],
+ * dW_seg1[:, 64:] = sum_b csum_b (x) g_b, dg = W_seg1[:, 64:]^T csum_b, dz_g = dg*(g>0),
+ * then bn_global's (alpha, beta, gamma, dgamma, dbeta, dbias) and the sparse coefficient
+ * sp[b,c] = alpha_c*dz_g[b,c] consumed by PCS_PRO_BWD_POOL.
+ */
+typedef struct {
+  int64_t num_scenes, scene_rows;
+  int32_t Cs;           /* 512: seg_conv1 outputs */
+  int32_t Cg;           /* 1024: global channels */
+  int32_t col_off;      /* 64: first global column of W_seg1 */
+  const float *s1_alpha, *s1_beta, *s1_gamma;  /* [Cs] bn_seg1 backward coefficients */
+  const float *s1_scene_s1;   /* [B, Cs] sum dz per scene */
+  const float *s1_scene_sum;  /* [B, Cs] sum y per scene (forward) */
+  const float *W_s1;    /* [Cs, ldw] f32 */
+  int64_t ldw;
+  const float *g;       /* [B, Cg] pooled features */
+  const float *ysel;    /* [B, Cg] global conv output at the argmax row */
+  const float *g_mean, *g_rstd, *g_gamma; /* [Cg] bn_global */
+  const float *g_scene_sum; /* [B, Cg] sum y_global per scene */
+  float *dW_s1_global;  /* [Cs, ldw] f32: columns col_off.. written */
+  float *csum;          /* [B, Cs] workspace */
+  float *alpha, *beta_c, *gamma_c; /* [Cg] out */
+  float *dgamma, *dbeta, *dbias;    /* [Cg] out */
+  float *sp;            /* [B, Cg] out */
+} pcs_pool_bwd_args;
+int pcs_pool_bwd(const pcs_pool_bwd_args *args, pcs_stream_t stream);
+
+/*
+ * Segmentation head: seg_conv4 (P:128, no BN) on relu(bn_seg3(y)) and, by mode,
+ *  PCS_HEAD_FWD: logits only;
+ *  PCS_HEAD_CE : logits, weighted CE with ignore_index=-1 (P:216, P:251) and its gradient,
+ *                then the seg_conv4 backward: dz_s3 = relu'(z)*(dlogits W), S1/S2 partials,
+ *                dW_s4 / db_s4 partials;
+ *  PCS_HEAD_BWD: the same backward from caller-supplied dlogits (autograd drop-in path).
+ */
+enum { PCS_HEAD_FWD = 0, PCS_HEAD_CE = 1, PCS_HEAD_BWD = 2 };
+typedef struct {
+  int64_t num_scenes, scene_rows;
+  int32_t Cin;          /* 128 */
+  int32_t num_classes;  /* C <= 16 */
+  int32_t dtype, mode;
+  int32_t chunks_per_scene; /* 0 = auto */
+  const void *Y;        /* [M, Cin] y_seg3 */
+  const float *s, *t;   /* bn_seg3 scale/shift */
+  const float *W, *bias;/* seg_conv4 f32 [C, Cin], [C] */
+  float *logits;        /* [M, C] f32 out or NULL */
+  const int64_t *labels;/* [M] (CE) */
+  const float *class_weight; /* [C] (CE) */
+  const float *wsum;    /* device scalar D: CE gradient is divided by D (the global
+                           sum of class weights over valid points, P:216); NULL = 1 */
+  const float *dlogits; /* (BWD) */
+  int64_t dl_stride_row, dl_stride_col; /* element strides of dlogits viewed as [M, C] */
+  void *dZ;             /* [M, Cin] dz_seg3 (CE, BWD) */
+  const float *mean, *rstd; /* bn_seg3 batch stats (S2) */
+  float *stats;         /* [chunks, Cin, 2] */
+  float *wpartial;      /* [chunks, C*Cin + C]: dW_s4 (row-major) then db_s4 partials */
+  float *loss_partial;  /* [chunks]: sum w*nll (CE) */
+} pcs_head_args;
+int64_t pcs_head_geometry(pcs_head_args *args); /* fills chunks_per_scene; rows per chunk */
+int pcs_head(const pcs_head_args *args, pcs_stream_t stream);
+
+/* sum of class_weight[label] over labels != -1 (the CE denominator, P:216) -> out[0] (f32),
+ * count of valid labels -> out[1], 1/out[0] -> out[2].  Exact: integer class counts (counts_ws[C], int64
+ * workspace) times the weights, summed in fp64. */
+int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weight,
+                      int32_t C, int64_t *counts_ws, float *out, pcs_stream_t stream);
+
+/* Dropout(p) keep bits (P:96, P:124, P:126): Philox4x32-10(seed, offset + element),
+ * keep = u >= p, 8 bits per byte along the channel dimension; bits[M, C/8]. */
+int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                     uint8_t *bits, pcs_stream_t stream);
+
+/* out[i] = scale * sum_s partial[s*len + i]  (fixed order) */
+int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale,
+                        float *out, int64_t out_stride_rows, int64_t row_len,
+                        pcs_stream_t stream);
+
+/* fp32 [rows, cols] (row stride ldw) -> dtype copies W ([rows, cols] contiguous) and W^T
+ * ([cols, rows]); either output may be NULL */
+int pcs_cast_weight(const float *W, int64_t rows, int64_t cols, int64_t ldw, int32_t dtype,
+                    void *Wc, void *WcT, pcs_stream_t stream);
+
+/*
+ * torch.optim.Adam step with L2 (coupled) weight decay, amsgrad=False (P:217, P:255) on
+ * flat fp32 buffers.  g_eff = g * (*grad_scale if non-NULL) + wd * p.
+ */
+int pcs_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+             const float *grad_scale, float lr, float beta1, float beta2, float eps,
+             float weight_decay, int64_t step, pcs_stream_t stream);
+
+/* Build-time identification and error string. */
+int pcs_abi_version(void);
+const char *pcs_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCS_H */

@@ -1,0 +1,115 @@
+// Shared device helpers for the pcs HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pcs.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short bf16_t;  // storage type of one bf16 element
+
+#define PCS_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------------------
+// element traits: T = float (parity path, f32 MFMA) or bf16_t (bench path, bf16 MFMA)
+// EPC = elements per 16-byte chunk
+// ---------------------------------------------------------------------------------------
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static constexpr int EPC = 4;
+  static constexpr int SIZE = 4;
+};
+template <> struct Elem<bf16_t> {
+  static constexpr int EPC = 8;
+  static constexpr int SIZE = 2;
+};
+
+PCS_DEV float bf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+PCS_DEV uint32_t pack2bf(float a, float b) {
+  f32x2 v = {a, b};
+  bf16x2 h = __builtin_convertvector(v, bf16x2);
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+// 16-byte chunk <-> float[EPC]
+PCS_DEV void unpack_chunk(const uint4 &c, float (&v)[4]) {
+  v[0] = __uint_as_float(c.x); v[1] = __uint_as_float(c.y);
+  v[2] = __uint_as_float(c.z); v[3] = __uint_as_float(c.w);
+}
+PCS_DEV void unpack_chunk(const uint4 &c, float (&v)[8]) {
+  v[0] = bf2f(c.x & 0xffffu); v[1] = bf2f(c.x >> 16);
+  v[2] = bf2f(c.y & 0xffffu); v[3] = bf2f(c.y >> 16);
+  v[4] = bf2f(c.z & 0xffffu); v[5] = bf2f(c.z >> 16);
+  v[6] = bf2f(c.w & 0xffffu); v[7] = bf2f(c.w >> 16);
+}
+PCS_DEV uint4 pack_chunk(const float (&v)[4]) {
+  return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                    __float_as_uint(v[3]));
+}
+PCS_DEV uint4 pack_chunk(const float (&v)[8]) {
+  return make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
+                    pack2bf(v[6], v[7]));
+}
+
+PCS_DEV float load_elem(const float *p, int64_t i) { return p[i]; }
+PCS_DEV float load_elem(const bf16_t *p, int64_t i) { return bf2f(p[i]); }
+
+// load EPC floats of a small per-channel coefficient vector (L1/L2 resident)
+template <int EPC>
+PCS_DEV void load_vec(const float *__restrict__ p, int k, float (&v)[EPC]) {
+#pragma unroll
+  for (int e = 0; e < EPC; e += 4) {
+    const float4 q = *reinterpret_cast<const float4 *>(p + k + e);
+    v[e] = q.x; v[e + 1] = q.y; v[e + 2] = q.z; v[e + 3] = q.w;
+  }
+}
+
+// dropout keep bit of element (row, k): bits packed 8 per byte along k.
+PCS_DEV uint32_t mask_bits(const uint8_t *__restrict__ bits, int64_t row, int K, int k, int n) {
+  // returns n (4 or 8) consecutive keep bits starting at k (k % n == 0)
+  const uint32_t byte = bits[row * (K >> 3) + (k >> 3)];
+  return n == 8 ? byte : ((byte >> (k & 7)) & 0xFu);
+}
+
+// wave-level helpers (wave64)
+PCS_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Chan's parallel merge of (n, mean, M2) triples.
+PCS_DEV void chan_merge(float &n, float &mean, float &m2, float nb, float meanb, float m2b) {
+  const float nn = n + nb;
+  if (nb == 0.f) return;
+  if (n == 0.f) { n = nb; mean = meanb; m2 = m2b; return; }
+  const float d = meanb - mean;
+  const float f = nb / nn;
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
+  n = nn;
+}
+
+// row-tile geometry of one scene-aware chunk (rows never straddle scenes)
+struct ChunkGeo {
+  int64_t scene_rows;   // N: rows per scene (padded cloud length)
+  int tiles_per_scene;  // ceil(N / BM)
+  int tiles_per_chunk;
+  int chunks_per_scene;
+};
+
+PCS_DEV int64_t pcs_min64(int64_t a, int64_t b) { return a < b ? a : b; }
+
+#define PCS_CHECK_LAUNCH()                                     \
+  do {                                                         \
+    hipError_t _e = hipGetLastError();                         \
+    if (_e != hipSuccess) return pcs_set_error(_e, __func__);  \
+  } while (0)
+
+int pcs_set_error(hipError_t e, const char *where);
+int pcs_set_einval(const char *where, const char *msg);

@@ -1,0 +1,461 @@
+// Points-major fused GEMM for the 1x1 Conv1d chain of PointNetSegmentation.
+//
+//   C[m, n] = sum_k pro(A)[m, k] * W[n, k]        (forward: P:106-128; dgrad: P:254)
+//
+// * pro(): BN-apply + ReLU (+ dropout keep bits) of the previous layer, or the BatchNorm
+//   backward affine dy = alpha*dz + beta + gamma*y, applied while the tile is staged
+//   global -> registers -> LDS, so activations are read once per tile and never written
+//   back in transformed form.
+// * epilogue: bias / per-scene bias, store, and per-chunk BatchNorm statistics (Welford
+//   per thread, Chan merge across threads) plus max/min+arg for the global max-pool; or,
+//   for dgrad, the ReLU/dropout mask of the previous layer and its BN-backward sums.
+// * MFMA: v_mfma_f32_16x16x32_bf16 (bf16 path) or v_mfma_f32_16x16x4_f32 (fp32 parity
+//   path: exact f32 products, one rounding per FMA).  Operands are swapped (W as the
+//   MFMA A operand) so each lane owns 4 consecutive output channels of one point.
+// * LDS operand tiles are 64 B per row (one k-step) with a 16-B-slot XOR swizzle that
+//   makes the ds_read_b128 fragment reads bank-conflict free.
+// * A workgroup walks a scene-aligned chunk of row tiles for one column block; blocks
+//   that share a chunk are mapped onto one XCD (round-robin dispatch, speed only).
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 256;
+constexpr int ROWB = 64;  // bytes per LDS operand row (one k-step)
+
+PCS_DEV int swz(int row, int slot) { return slot ^ ((-(row >> 2)) & 3); }
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16_t> {
+  static constexpr int KSTEP = 32;  // elements per k-step (64 B)
+  static constexpr int KK = 1;      // MFMA k-iterations per k-step
+  typedef bf16x8 frag;
+  static PCS_DEV frag load(const char *tile, int row, int lane, int kk) {
+    (void)kk;
+    return *reinterpret_cast<const frag *>(tile + row * ROWB + swz(row, lane >> 4) * 16);
+  }
+  static PCS_DEV f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<float> {
+  static constexpr int KSTEP = 16;
+  static constexpr int KK = 4;
+  typedef float frag;
+  static PCS_DEV frag load(const char *tile, int row, int lane, int kk) {
+    return *reinterpret_cast<const float *>(tile + row * ROWB + swz(row, kk) * 16 +
+                                            (lane >> 4) * 4);
+  }
+  static PCS_DEV f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+};
+
+// bijective XCD-grouping remap of the linear block id (cdna_hip_programming.md §5)
+PCS_DEV int xcd_remap(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+template <typename T, int BM, int BN, int PRO, int EPI, bool POOL>
+__global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int tiles_per_scene,
+                                                          int tiles_per_chunk, int ncb) {
+  constexpr int EPC = Elem<T>::EPC;
+  constexpr int SZ = Elem<T>::SIZE;
+  constexpr int KSTEP = Mfma<T>::KSTEP;
+  constexpr int WTM = BM / 2, WTN = BN / 2;  // 2x2 waves
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int ACH = BM / 64, BCH = BN / 64;  // 16-B chunks per thread per k-step
+  constexpr int STAGE_BYTES = 2 * (BM + BN) * ROWB;
+  constexpr int CROW = BN * SZ + 16;           // epilogue tile row stride (bytes)
+  constexpr int CTILE_BYTES = BM * CROW;
+  constexpr int CPR = BN * SZ / 16;            // chunks per output row
+  constexpr int RPP = THREADS / CPR;           // rows per epilogue pass
+  constexpr int RED_BYTES = RPP * BN * 16;
+  constexpr int LDS_BYTES = STAGE_BYTES > CTILE_BYTES
+                                ? (STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES)
+                                : (CTILE_BYTES > RED_BYTES ? CTILE_BYTES : RED_BYTES);
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = L / ncb, cb = L % ncb;
+  const int cps = a.chunks_per_scene;
+  const int scene = chunk / cps, cis = chunk % cps;
+  const int n0 = cb * BN;
+  const int K = a.K, Ncols = a.Ncols;
+  const int64_t N = a.scene_rows;
+  const int t_begin = cis * tiles_per_chunk;
+  const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
+  const int nks = K / KSTEP;
+
+  const T *__restrict__ Ag = reinterpret_cast<const T *>(a.A);
+  const T *__restrict__ A2g = reinterpret_cast<const T *>(a.A2);
+  const T *__restrict__ Wg = reinterpret_cast<const T *>(a.W);
+  T *__restrict__ Cg = reinterpret_cast<T *>(a.C);
+
+  const int slot = tid & 3;           // staging: fixed k-slot per thread
+  const int srow = tid >> 2;          // staging: row (+64*i)
+
+  // epilogue thread mapping (fixed columns per thread)
+  const int ecc = tid % CPR, er0 = tid / CPR;
+  const int ecol = n0 + ecc * EPC;
+
+  // per-thread epilogue accumulators
+  float st_mean[EPC], st_m2[EPC], st_cnt = 0.f;
+  float pmax[EPC], pmin[EPC];
+  int pmaxi[EPC], pmini[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    st_mean[e] = 0.f; st_m2[e] = 0.f;
+    pmax[e] = -__builtin_huge_valf(); pmin[e] = __builtin_huge_valf();
+    pmaxi[e] = 0x7fffffff; pmini[e] = 0x7fffffff;
+  }
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int64_t row_base = scene * N + (int64_t)tile * BM;
+    const int valid = (int)pcs_min64(BM, N - (int64_t)tile * BM);
+
+    uint4 ra[ACH], ra2[ACH], rb[BCH];
+    auto load_stage = [&](int ks) {
+      const int k0 = ks * KSTEP + slot * EPC;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int r = srow + 64 * i;
+        if (r < valid) {
+          const int64_t off = (row_base + r) * K + k0;
+          ra[i] = *reinterpret_cast<const uint4 *>(Ag + off);
+          if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const uint4 *>(A2g + off);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int r = srow + 64 * i;
+        rb[i] = *reinterpret_cast<const uint4 *>(Wg + (int64_t)(n0 + r) * K + k0);
+      }
+    };
+    auto store_stage = [&](int ks, int buf) {
+      char *tA = lds + buf * (BM + BN) * ROWB;
+      char *tB = tA + BM * ROWB;
+      const int k0 = ks * KSTEP + slot * EPC;
+      float c0[EPC], c1[EPC], c2[EPC];
+      if constexpr (PRO == PCS_PRO_BNRELU) {
+        load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1);
+      } else if constexpr (PRO == PCS_PRO_BWD) {
+        load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
+      } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+        load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
+        load_vec<EPC>(a.pool_coef + scene * K, k0, c0);
+      }
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int r = srow + 64 * i;
+        uint4 out = make_uint4(0, 0, 0, 0);
+        if (r < valid) {
+          float v[EPC];
+          unpack_chunk(ra[i], v);
+          if constexpr (PRO == PCS_PRO_BNRELU) {
+            uint32_t bits = 0xffu;
+            if (a.a_mask) bits = mask_bits(a.a_mask, row_base + r, K, k0, EPC);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+              float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+              if (a.a_mask) x *= ((bits >> e) & 1u) ? a.a_keep_scale : 0.f;
+              v[e] = x;
+            }
+          } else if constexpr (PRO == PCS_PRO_BWD) {
+            float y[EPC];
+            unpack_chunk(ra2[i], y);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) v[e] = fmaf(c0[e], v[e], fmaf(c2[e], y[e], c1[e]));
+          } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+            // A holds Y_l here; the sparse dz lives at the argmax rows
+            const int grow = (int)(row_base + r);
+            const int *am = a.pool_idx + scene * K + k0;
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+              float x = fmaf(c2[e], v[e], c1[e]);
+              if (am[e] == grow) x += c0[e];
+              v[e] = x;
+            }
+          }
+          out = pack_chunk(v);
+        }
+        *reinterpret_cast<uint4 *>(tA + r * ROWB + swz(r, slot) * 16) = out;
+      }
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int r = srow + 64 * i;
+        *reinterpret_cast<uint4 *>(tB + r * ROWB + swz(r, slot) * 16) = rb[i];
+      }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    load_stage(0);
+    store_stage(0, 0);
+    __syncthreads();
+    for (int ks = 0; ks < nks; ++ks) {
+      const int buf = ks & 1;
+      if (ks + 1 < nks) load_stage(ks + 1);
+      const char *tA = lds + buf * (BM + BN) * ROWB;
+      const char *tB = tA + BM * ROWB;
+#pragma unroll
+      for (int kk = 0; kk < Mfma<T>::KK; ++kk) {
+        typename Mfma<T>::frag af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = Mfma<T>::load(tA, wm * WTM + i * 16 + (lane & 15), lane, kk);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = Mfma<T>::load(tB, wn * WTN + j * 16 + (lane & 15), lane, kk);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::mma(bf[j], af[i], acc[i][j]);
+      }
+      if (ks + 1 < nks) store_stage(ks + 1, buf ^ 1);
+      __syncthreads();
+    }
+
+    // ---- epilogue phase 1: accumulators (+bias) -> LDS tile [BM][BN] in T ----
+    {
+      const float *bias = nullptr;
+      if constexpr (EPI == PCS_EPI_FWD) bias = a.scene_bias ? a.scene_bias + scene * Ncols : a.bias;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = wm * WTM + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = wn * WTN + j * 16 + 4 * (lane >> 4);
+          float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+          if (bias) {
+            const float4 bb = *reinterpret_cast<const float4 *>(bias + n0 + n);
+            v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
+          }
+          char *dst = lds + m * CROW + n * SZ;
+          if constexpr (SZ == 4) {
+            *reinterpret_cast<float4 *>(dst) = make_float4(v0, v1, v2, v3);
+          } else {
+            *reinterpret_cast<uint2 *>(dst) = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- epilogue phase 2: coalesced row chunks ----
+    {
+      float es[EPC], et[EPC], em[EPC], er[EPC];
+      if constexpr (EPI == PCS_EPI_DGRAD) {
+        load_vec<EPC>(a.es, ecol, es); load_vec<EPC>(a.et, ecol, et);
+        load_vec<EPC>(a.emean, ecol, em); load_vec<EPC>(a.erstd, ecol, er);
+      }
+      const T *Ypg = reinterpret_cast<const T *>(a.Yp);
+      const T *Addg = reinterpret_cast<const T *>(a.addend);
+#pragma unroll 2
+      for (int rr = er0; rr < BM; rr += RPP) {
+        if (rr >= valid) break;
+        const int64_t grow = row_base + rr;
+        const int64_t goff = grow * Ncols + ecol;
+        float v[EPC];
+        unpack_chunk(*reinterpret_cast<const uint4 *>(lds + rr * CROW + ecc * 16), v);
+        if constexpr (EPI == PCS_EPI_FWD) {
+          if (Cg) *reinterpret_cast<uint4 *>(Cg + goff) =
+              *reinterpret_cast<const uint4 *>(lds + rr * CROW + ecc * 16);
+          if (a.stats) {
+            st_cnt += 1.f;
+            const float rn = 1.f / st_cnt;
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+              const float d = v[e] - st_mean[e];
+              st_mean[e] = fmaf(d, rn, st_mean[e]);
+              st_m2[e] = fmaf(d, v[e] - st_mean[e], st_m2[e]);
+            }
+          }
+          if constexpr (POOL) {
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+              if (v[e] > pmax[e]) { pmax[e] = v[e]; pmaxi[e] = (int)grow; }
+              if (v[e] < pmin[e]) { pmin[e] = v[e]; pmini[e] = (int)grow; }
+            }
+          }
+        } else if constexpr (EPI == PCS_EPI_DGRAD) {
+          if (Addg) {
+            float ad[EPC];
+            unpack_chunk(*reinterpret_cast<const uint4 *>(Addg + goff), ad);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) v[e] += ad[e];
+          }
+          if (a.c_mask) {
+            const uint32_t bits = mask_bits(a.c_mask, grow, Ncols, ecol, EPC);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) v[e] *= ((bits >> e) & 1u) ? a.c_keep_scale : 0.f;
+          }
+          float y[EPC];
+          unpack_chunk(*reinterpret_cast<const uint4 *>(Ypg + goff), y);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? v[e] : 0.f;
+            v[e] = dz;
+            st_mean[e] += dz;                                   // S1
+            st_m2[e] = fmaf(dz, (y[e] - em[e]) * er[e], st_m2[e]);  // S2
+          }
+          *reinterpret_cast<uint4 *>(Cg + goff) = pack_chunk(v);
+        } else {  // RAW
+          *reinterpret_cast<uint4 *>(Cg + goff) =
+              *reinterpret_cast<const uint4 *>(lds + rr * CROW + ecc * 16);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- chunk end: cross-thread reduction of the per-thread partials ----
+  if (t_begin >= t_end) return;  // uniform across the block
+  const int64_t chunk_id = (int64_t)scene * cps + cis;
+  if constexpr (EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD) {
+    if (a.stats) {
+      float4 *red = reinterpret_cast<float4 *>(lds);  // [RPP][BN]
+#pragma unroll
+      for (int e = 0; e < EPC; ++e)
+        red[er0 * BN + ecc * EPC + e] = make_float4(st_cnt, st_mean[e], st_m2[e], 0.f);
+      __syncthreads();
+      for (int c = tid; c < BN; c += THREADS) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int j = 0; j < RPP; ++j) {
+          const float4 q = red[j * BN + c];
+          if constexpr (EPI == PCS_EPI_FWD) {
+            chan_merge(n, mean, m2, q.x, q.y, q.z);
+          } else {
+            mean += q.y; m2 += q.z;
+          }
+        }
+        *reinterpret_cast<float2 *>(a.stats + (chunk_id * Ncols + n0 + c) * 2) = make_float2(mean, m2);
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (POOL) {
+    float4 *red = reinterpret_cast<float4 *>(lds);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e)
+      red[er0 * BN + ecc * EPC + e] =
+          make_float4(pmax[e], __int_as_float(pmaxi[e]), pmin[e], __int_as_float(pmini[e]));
+    __syncthreads();
+    for (int c = tid; c < BN; c += THREADS) {
+      float mx = -__builtin_huge_valf(), mn = __builtin_huge_valf();
+      int mxi = 0x7fffffff, mni = 0x7fffffff;
+      for (int j = 0; j < RPP; ++j) {
+        const float4 q = red[j * BN + c];
+        const int qi = __float_as_int(q.y), qj = __float_as_int(q.w);
+        if (q.x > mx || (q.x == mx && qi < mxi)) { mx = q.x; mxi = qi; }
+        if (q.z < mn || (q.z == mn && qj < mni)) { mn = q.z; mni = qj; }
+      }
+      *reinterpret_cast<float4 *>(a.pool + (chunk_id * Ncols + n0 + c) * 4) =
+          make_float4(mx, __int_as_float(mxi), mn, __int_as_float(mni));
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int PRO, int EPI, bool POOL>
+int launch_t(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
+  const int ncb = a.Ncols / BN;
+  const int nb = ncb * (int)(a.num_scenes * a.chunks_per_scene);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL>), dim3(nb), dim3(THREADS), 0, s,
+                     a, tps, tpc, ncb);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T, int BN>
+int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
+  constexpr int BM = 128;
+  const bool pool = a.pool != nullptr;
+  switch (a.epilogue) {
+    case PCS_EPI_FWD:
+      switch (a.prologue) {
+        case PCS_PRO_BNRELU:
+          return pool ? launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_FWD, true>(a, tps, tpc, s)
+                      : launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_FWD, false>(a, tps, tpc, s);
+        case PCS_PRO_RAW:
+          return launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_FWD, false>(a, tps, tpc, s);
+        default: break;
+      }
+      break;
+    case PCS_EPI_DGRAD:
+      switch (a.prologue) {
+        case PCS_PRO_BWD: return launch_t<T, BM, BN, PCS_PRO_BWD, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
+        case PCS_PRO_BWD_POOL:
+          return launch_t<T, BM, BN, PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
+        default: break;
+      }
+      break;
+    case PCS_EPI_RAW:
+      switch (a.prologue) {
+        case PCS_PRO_BWD: return launch_t<T, BM, BN, PCS_PRO_BWD, PCS_EPI_RAW, false>(a, tps, tpc, s);
+        case PCS_PRO_BNRELU:
+          return launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_RAW, false>(a, tps, tpc, s);
+        default: break;
+      }
+      break;
+  }
+  return pcs_set_einval("pcs_gemm", "unsupported prologue/epilogue combination");
+}
+
+}  // namespace
+
+static constexpr int GEMM_BM = 128;
+
+extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
+  if (!a || a->num_scenes <= 0 || a->scene_rows <= 0)
+    return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
+  const int64_t tps = (a->scene_rows + GEMM_BM - 1) / GEMM_BM;
+  int64_t cps = a->chunks_per_scene;
+  if (cps <= 0) {
+    const int ncb = a->Ncols >= 128 ? a->Ncols / 128 : 1;
+    const int64_t target = 2048;  // ~8 workgroups per CU
+    cps = (target + a->num_scenes * ncb - 1) / (a->num_scenes * ncb);
+  }
+  if (cps > tps) cps = tps;
+  if (cps < 1) cps = 1;
+  const int64_t tpc = (tps + cps - 1) / cps;
+  cps = (tps + tpc - 1) / tpc;  // no empty chunks
+  a->chunks_per_scene = (int32_t)cps;
+  return tpc * GEMM_BM;
+}
+
+extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
+  if (!ap) return pcs_set_einval("pcs_gemm", "null args");
+  pcs_gemm_args a = *ap;
+  if (a.K <= 0 || a.Ncols <= 0) return pcs_set_einval("pcs_gemm", "K/Ncols must be positive");
+  if (a.Ncols % 64 != 0) return pcs_set_einval("pcs_gemm", "Ncols must be a multiple of 64");
+  const int kstep = a.dtype == PCS_BF16 ? 32 : 16;
+  if (a.K % kstep != 0) return pcs_set_einval("pcs_gemm", "K must be a multiple of the k-step");
+  if (!a.A || !a.W) return pcs_set_einval("pcs_gemm", "A and W are required");
+  if (a.prologue == PCS_PRO_BWD && (!a.A2 || !a.pa || !a.pb || !a.pc))
+    return pcs_set_einval("pcs_gemm", "PRO_BWD needs A2 (=Y_l), alpha, beta, gamma");
+  if (a.prologue == PCS_PRO_BWD_POOL && (!a.pb || !a.pc || !a.pool_idx || !a.pool_coef))
+    return pcs_set_einval("pcs_gemm", "PRO_BWD_POOL needs beta, gamma, pool_idx, pool_coef");
+  if (a.prologue == PCS_PRO_BNRELU && (!a.pa || !a.pb))
+    return pcs_set_einval("pcs_gemm", "PRO_BNRELU needs s and t");
+  if (a.epilogue == PCS_EPI_DGRAD && (!a.Yp || !a.es || !a.et || !a.emean || !a.erstd || !a.C))
+    return pcs_set_einval("pcs_gemm", "EPI_DGRAD needs Yp, es, et, emean, erstd and C");
+  if (a.pool && a.epilogue != PCS_EPI_FWD) return pcs_set_einval("pcs_gemm", "pool needs EPI_FWD");
+  if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31)
+    return pcs_set_einval("pcs_gemm", "M must be < 2^31 rows");
+  const int64_t rpc = pcs_gemm_geometry(&a);
+  if (rpc < 0) return (int)rpc;
+  const int tps = (int)((a.scene_rows + GEMM_BM - 1) / GEMM_BM);
+  const int tpc = (int)(rpc / GEMM_BM);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool bn128 = a.Ncols % 128 == 0;
+  if (a.dtype == PCS_BF16)
+    return bn128 ? dispatch_pro_epi<bf16_t, 128>(a, tps, tpc, s) : dispatch_pro_epi<bf16_t, 64>(a, tps, tpc, s);
+  if (a.dtype == PCS_F32)
+    return bn128 ? dispatch_pro_epi<float, 128>(a, tps, tpc, s) : dispatch_pro_epi<float, 64>(a, tps, tpc, s);
+  return pcs_set_einval("pcs_gemm", "bad dtype");
+}

@@ -1,0 +1,856 @@
+// Small / bandwidth-light kernels of the PointNetSegmentation training step:
+// conv1 (Cin = 4) forward and weight gradient, BatchNorm statistic finalisation (forward
+// and backward), the global max-pool finalisation and its backward, the per-scene GEMV of
+// seg_conv1's global half, dropout keep bits (Philox4x32-10), the CE weight sum, fp32
+// partial reduction, weight casting and the fused Adam step.
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 256;
+constexpr int C1_BM = 128;  // conv1 row tile (same chunk geometry rules as pcs_gemm)
+
+// ---------------------------------------------------------------------------------------
+// conv1 forward: y[m, c] = b[c] + sum_k W[c,k] x[m,k]  (P:70, P:106), K = 4, fp32 math
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int tiles_per_scene,
+                                                            int tiles_per_chunk) {
+  constexpr int EPC = Elem<T>::EPC;
+  constexpr int COLS = 64;
+  constexpr int CPR = COLS / EPC;
+  constexpr int RPP = THREADS / CPR;
+  __shared__ float4 red[RPP * COLS];
+  const int tid = threadIdx.x;
+  const int cps = a.chunks_per_scene;
+  const int scene = blockIdx.x / cps, cis = blockIdx.x % cps;
+  const int64_t N = a.scene_rows;
+  const int cc = tid % CPR, r0 = tid / CPR, c0 = cc * EPC;
+  const float *X = reinterpret_cast<const float *>(a.A);
+  const float *W = reinterpret_cast<const float *>(a.W);
+  T *Cg = reinterpret_cast<T *>(a.C);
+  float w[EPC][4], bias[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    bias[e] = a.bias ? a.bias[c0 + e] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[e][k] = W[(c0 + e) * 4 + k];
+  }
+  float mean[EPC], m2[EPC], cnt = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
+  const int64_t r_begin = (int64_t)cis * tiles_per_chunk * C1_BM;
+  const int64_t r_end = pcs_min64(r_begin + (int64_t)tiles_per_chunk * C1_BM, N);
+  for (int64_t r = r_begin + r0; r < r_end; r += RPP) {
+    const int64_t grow = scene * N + r;
+    const float4 x = *reinterpret_cast<const float4 *>(X + grow * 4);
+    float v[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      float acc = bias[e];
+      acc = fmaf(w[e][0], x.x, acc);
+      acc = fmaf(w[e][1], x.y, acc);
+      acc = fmaf(w[e][2], x.z, acc);
+      acc = fmaf(w[e][3], x.w, acc);
+      v[e] = acc;
+    }
+    const uint4 packed = pack_chunk(v);
+    *reinterpret_cast<uint4 *>(Cg + grow * COLS + c0) = packed;
+    unpack_chunk(packed, v);  // statistics of the stored (rounded) values
+    cnt += 1.f;
+    const float rn = 1.f / cnt;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const float d = v[e] - mean[e];
+      mean[e] = fmaf(d, rn, mean[e]);
+      m2[e] = fmaf(d, v[e] - mean[e], m2[e]);
+    }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) red[r0 * COLS + c0 + e] = make_float4(cnt, mean[e], m2[e], 0.f);
+  __syncthreads();
+  if (tid < COLS) {
+    float n = 0.f, mu = 0.f, q = 0.f;
+    for (int j = 0; j < RPP; ++j) {
+      const float4 p = red[j * COLS + tid];
+      chan_merge(n, mu, q, p.x, p.y, p.z);
+    }
+    *reinterpret_cast<float2 *>(a.stats + ((int64_t)blockIdx.x * COLS + tid) * 2) = make_float2(mu, q);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// conv1 weight gradient: dW[c,k] = sum_m dy[m,c] x[m,k]; dy = alpha dz + beta + gamma y
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(THREADS) void conv1_wgrad_kernel(pcs_wgrad_args a, int64_t rows_per_split) {
+  constexpr int EPC = Elem<T>::EPC;
+  constexpr int COLS = 64;
+  constexpr int CPR = COLS / EPC;
+  constexpr int RPP = THREADS / CPR;
+  __shared__ float red[RPP][COLS * 4];
+  const int tid = threadIdx.x;
+  const int sps = a.splits_per_scene;
+  const int scene = blockIdx.x / sps, sis = blockIdx.x % sps;
+  const int64_t N = a.scene_rows;
+  const int cc = tid % CPR, r0 = tid / CPR, c0 = cc * EPC;
+  const T *dZ = reinterpret_cast<const T *>(a.dZ);
+  const T *Y = reinterpret_cast<const T *>(a.Y);
+  const float *X = reinterpret_cast<const float *>(a.X);
+  float ca[EPC], cb[EPC], cg[EPC];
+  load_vec<EPC>(a.alpha, c0, ca); load_vec<EPC>(a.beta, c0, cb); load_vec<EPC>(a.gamma, c0, cg);
+  float acc[EPC][4];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[e][k] = 0.f;
+  const int64_t lo = (int64_t)sis * rows_per_split, hi = pcs_min64(lo + rows_per_split, N);
+  for (int64_t r = lo + r0; r < hi; r += RPP) {
+    const int64_t grow = scene * N + r;
+    float dz[EPC], y[EPC];
+    unpack_chunk(*reinterpret_cast<const uint4 *>(dZ + grow * COLS + c0), dz);
+    unpack_chunk(*reinterpret_cast<const uint4 *>(Y + grow * COLS + c0), y);
+    const float4 x = *reinterpret_cast<const float4 *>(X + grow * 4);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const float dy = fmaf(ca[e], dz[e], fmaf(cg[e], y[e], cb[e]));
+      acc[e][0] = fmaf(dy, x.x, acc[e][0]);
+      acc[e][1] = fmaf(dy, x.y, acc[e][1]);
+      acc[e][2] = fmaf(dy, x.z, acc[e][2]);
+      acc[e][3] = fmaf(dy, x.w, acc[e][3]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[r0][(c0 + e) * 4 + k] = acc[e][k];
+  __syncthreads();
+  for (int i = tid; i < COLS * 4; i += THREADS) {
+    float s = 0.f;
+    for (int j = 0; j < RPP; ++j) s += red[j][i];
+    a.partial[(int64_t)blockIdx.x * COLS * 4 + i] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// BatchNorm statistics
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(THREADS) void bn_fwd_finalize_kernel(
+    const float *stats, int64_t B, int64_t N, int C, int cps, int64_t rpc, const float *gamma,
+    const float *beta, float *rmean, float *rvar, float momentum, float eps, int update,
+    float *mean_o, float *rstd_o, float *scale_o, float *shift_o, float *scene_sum) {
+  __shared__ double sh[THREADS][3];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double gn = 0, gmean = 0, gm2 = 0;
+  for (int64_t b = 0; b < B; ++b) {
+    double n = 0, mu = 0, q = 0;
+    for (int j = tid; j < cps; j += THREADS) {
+      const double nb = (double)pcs_min64(rpc, N - (int64_t)j * rpc);
+      const float2 p = *reinterpret_cast<const float2 *>(stats + ((b * cps + j) * C + c) * 2);
+      const double nn = n + nb, d = (double)p.x - mu;
+      mu += d * nb / nn;
+      q += (double)p.y + d * d * n * nb / nn;
+      n = nn;
+    }
+    sh[tid][0] = n; sh[tid][1] = mu; sh[tid][2] = q;
+    __syncthreads();
+    for (int s = THREADS / 2; s > 0; s >>= 1) {
+      if (tid < s) {
+        const double na = sh[tid][0], nb = sh[tid + s][0];
+        if (nb > 0) {
+          const double nn = na + nb, d = sh[tid + s][1] - sh[tid][1];
+          sh[tid][1] += d * nb / nn;
+          sh[tid][2] += sh[tid + s][2] + d * d * na * nb / nn;
+          sh[tid][0] = nn;
+        }
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const double nb = sh[0][0], mb = sh[0][1], qb = sh[0][2];
+      if (scene_sum) scene_sum[b * C + c] = (float)(nb * mb);
+      const double nn = gn + nb, d = mb - gmean;
+      gmean += d * nb / nn;
+      gm2 += qb + d * d * gn * nb / nn;
+      gn = nn;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double var = gm2 / gn;  // biased (normalisation)
+    const double rstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * rstd;
+    mean_o[c] = (float)gmean;
+    rstd_o[c] = (float)rstd;
+    scale_o[c] = (float)sc;
+    shift_o[c] = (float)((double)beta[c] - gmean * sc);
+    if (update) {
+      const double unb = gn > 1 ? gm2 / (gn - 1) : gm2;
+      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * gmean);
+      rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+    }
+  }
+}
+
+__global__ void bn_eval_kernel(const float *gamma, const float *beta, const float *rm,
+                               const float *rv, float eps, int C, float *scale, float *shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sc = (double)gamma[c] / sqrt((double)rv[c] + (double)eps);
+  scale[c] = (float)sc;
+  shift[c] = (float)((double)beta[c] - (double)rm[c] * sc);
+}
+
+__global__ __launch_bounds__(THREADS) void bn_bwd_finalize_kernel(
+    const float *stats, int64_t B, int64_t N, int C, int cps, const float *mean, const float *rstd,
+    const float *gamma, const float *scene_sum, float *alpha, float *beta_c, float *gamma_c,
+    float *dgamma, float *dbeta, float *dbias, float *scene_s1) {
+  __shared__ double sh[THREADS][2];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double S1 = 0, S2 = 0, Sy = 0;
+  for (int64_t b = 0; b < B; ++b) {
+    double s1 = 0, s2 = 0;
+    for (int j = tid; j < cps; j += THREADS) {
+      const float2 p = *reinterpret_cast<const float2 *>(stats + ((b * cps + j) * C + c) * 2);
+      s1 += p.x; s2 += p.y;
+    }
+    sh[tid][0] = s1; sh[tid][1] = s2;
+    __syncthreads();
+    for (int s = THREADS / 2; s > 0; s >>= 1) {
+      if (tid < s) { sh[tid][0] += sh[tid + s][0]; sh[tid][1] += sh[tid + s][1]; }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      if (scene_s1) scene_s1[b * C + c] = (float)sh[0][0];
+      S1 += sh[0][0]; S2 += sh[0][1];
+      if (scene_sum) Sy += scene_sum[b * C + c];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double M = (double)(B * N);
+    const double r = rstd[c], g = gamma[c], mu = mean[c];
+    const double al = g * r;
+    const double ga = -g * r * r * S2 / M;
+    const double be = -g * r * S1 / M - ga * mu;
+    alpha[c] = (float)al; gamma_c[c] = (float)ga; beta_c[c] = (float)be;
+    if (dgamma) dgamma[c] = (float)S2;
+    if (dbeta) dbeta[c] = (float)S1;
+    if (dbias) dbias[c] = scene_sum ? (float)(al * S1 + M * be + ga * Sy) : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// global max-pool (P:114) finalisation and backward
+// ---------------------------------------------------------------------------------------
+__global__ void pool_finalize_kernel(const float *pool, int64_t B, int64_t N, int C, int cps,
+                                     const float *s, const float *t, float *g, int32_t *am,
+                                     float *ysel) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = (int)(i / C), c = (int)(i % C);
+  float mx = -__builtin_huge_valf(), mn = __builtin_huge_valf();
+  int mxi = 0x7fffffff, mni = 0x7fffffff;
+  for (int j = 0; j < cps; ++j) {
+    const float4 q = *reinterpret_cast<const float4 *>(pool + (((int64_t)b * cps + j) * C + c) * 4);
+    const int qi = __float_as_int(q.y), qj = __float_as_int(q.w);
+    if (q.x > mx || (q.x == mx && qi < mxi)) { mx = q.x; mxi = qi; }
+    if (q.z < mn || (q.z == mn && qj < mni)) { mn = q.z; mni = qj; }
+  }
+  const float sc = s[c];
+  float y; int idx;
+  if (sc > 0.f) { y = mx; idx = mxi; }
+  else if (sc < 0.f) { y = mn; idx = mni; }
+  else { y = mx; idx = (int)(b * N); }  // constant z: torch's first index
+  const float z = fmaf(y, sc, t[c]);
+  g[i] = fmaxf(z, 0.f);
+  am[i] = idx;
+  ysel[i] = y;
+}
+
+__global__ void scene_gemv_kernel(const float *g, int64_t B, int Kg, const float *W, int64_t ldw,
+                                  int col_off, const float *bias, int Nout, float *out) {
+  // one wave per (b, n)
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= B * Nout) return;
+  const int b = (int)(wave / Nout), n = (int)(wave % Nout);
+  const float *w = W + (int64_t)n * ldw + col_off;
+  const float *x = g + (int64_t)b * Kg;
+  float acc = 0.f;
+  for (int k = lane; k < Kg; k += 64) acc = fmaf(w[k], x[k], acc);
+  acc = wave_sum(acc);
+  if (lane == 0) out[wave] = acc + (bias ? bias[n] : 0.f);
+}
+
+// csum[b,n] = sum over the rows of scene b of dy_seg1[:, n]
+__global__ void pool_bwd_csum_kernel(pcs_pool_bwd_args a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.num_scenes * a.Cs) return;
+  const int n = (int)(i % a.Cs);
+  a.csum[i] = a.s1_alpha[n] * a.s1_scene_s1[i] + (float)a.scene_rows * a.s1_beta[n] +
+              a.s1_gamma[n] * a.s1_scene_sum[i];
+}
+
+// dW_seg1[n, off+k] = sum_b csum[b,n] g[b,k]
+__global__ void pool_bwd_dw_kernel(pcs_pool_bwd_args a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.Cs * a.Cg) return;
+  const int n = (int)(i / a.Cg), k = (int)(i % a.Cg);
+  float acc = 0.f;
+  for (int64_t b = 0; b < a.num_scenes; ++b) acc = fmaf(a.csum[b * a.Cs + n], a.g[b * a.Cg + k], acc);
+  a.dW_s1_global[(int64_t)n * a.ldw + a.col_off + k] = acc;
+}
+
+// dg = W_g^T csum; dz_g = dg*(g>0); bn_global backward from the B sparse entries
+__global__ void pool_bwd_coef_kernel(pcs_pool_bwd_args a) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.Cg) return;
+  const double M = (double)(a.num_scenes * a.scene_rows);
+  const double r = a.g_rstd[k], gm = a.g_gamma[k], mu = a.g_mean[k];
+  double S1 = 0, S2 = 0, Sy = 0;
+  for (int64_t b = 0; b < a.num_scenes; ++b) {
+    float dg = 0.f;
+    for (int n = 0; n < a.Cs; ++n)
+      dg = fmaf(a.W_s1[(int64_t)n * a.ldw + a.col_off + k], a.csum[b * a.Cs + n], dg);
+    const float dz = a.g[b * a.Cg + k] > 0.f ? dg : 0.f;
+    a.sp[b * a.Cg + k] = dz;  // scaled by alpha below
+    S1 += dz;
+    S2 += (double)dz * ((double)a.ysel[b * a.Cg + k] - mu) * r;
+    Sy += a.g_scene_sum[b * a.Cg + k];
+  }
+  const double al = gm * r;
+  const double ga = -gm * r * r * S2 / M;
+  const double be = -gm * r * S1 / M - ga * mu;
+  for (int64_t b = 0; b < a.num_scenes; ++b) a.sp[b * a.Cg + k] = (float)(al * a.sp[b * a.Cg + k]);
+  a.alpha[k] = (float)al; a.beta_c[k] = (float)be; a.gamma_c[k] = (float)ga;
+  a.dgamma[k] = (float)S2; a.dbeta[k] = (float)S1;
+  a.dbias[k] = (float)(al * S1 + M * be + ga * Sy);
+}
+
+// ---------------------------------------------------------------------------------------
+// segmentation head: seg_conv4 (P:128) + weighted CE (P:216,251) + head backward
+// ---------------------------------------------------------------------------------------
+constexpr int HEAD_R = 64;      // rows per tile
+constexpr int HEAD_CIN = 128;
+constexpr int HEAD_MAXC = 16;
+constexpr int HEAD_LD = HEAD_CIN + 1;
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tiles_per_scene,
+                                                       int tiles_per_chunk) {
+  constexpr int EPC = Elem<T>::EPC;
+  constexpr int QCH = 32;  // channels per thread
+  __shared__ float av[HEAD_R * HEAD_LD];
+  __shared__ float xh[HEAD_R * HEAD_LD];
+  __shared__ float wl[HEAD_MAXC * HEAD_CIN];
+  __shared__ float dl[HEAD_R * HEAD_MAXC];
+  __shared__ float lred[THREADS / 64];
+  const int tid = threadIdx.x;
+  const int C = a.num_classes;
+  const int cps = a.chunks_per_scene;
+  const int scene = blockIdx.x / cps, cis = blockIdx.x % cps;
+  const int64_t N = a.scene_rows;
+  const int r = tid >> 2, q = tid & 3, ch0 = q * QCH;
+  const T *Y = reinterpret_cast<const T *>(a.Y);
+  T *dZ = reinterpret_cast<T *>(a.dZ);
+
+  for (int i = tid; i < C * HEAD_CIN; i += THREADS) wl[i] = a.W[i];
+  float s1[QCH], s2[QCH];
+#pragma unroll
+  for (int e = 0; e < QCH; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  constexpr int NPAIR = (HEAD_MAXC * (HEAD_CIN + 1) + THREADS - 1) / THREADS;
+  float wacc[NPAIR];
+#pragma unroll
+  for (int i = 0; i < NPAIR; ++i) wacc[i] = 0.f;
+  float loss_acc = 0.f;
+  __syncthreads();
+
+  const int t_begin = cis * tiles_per_chunk;
+  const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int64_t row_base = scene * N + (int64_t)tile * HEAD_R;
+    const int valid = (int)pcs_min64(HEAD_R, N - (int64_t)tile * HEAD_R);
+    const bool rv = r < valid;
+    const int64_t grow = row_base + r;
+    // phase 1: load y, a = relu(y*s+t), xhat
+    if (rv) {
+#pragma unroll
+      for (int c = 0; c < QCH; c += EPC) {
+        float y[EPC], s[EPC], t[EPC], mu[EPC], rs[EPC];
+        unpack_chunk(*reinterpret_cast<const uint4 *>(Y + grow * HEAD_CIN + ch0 + c), y);
+        load_vec<EPC>(a.s, ch0 + c, s); load_vec<EPC>(a.t, ch0 + c, t);
+        if constexpr (MODE != PCS_HEAD_FWD) { load_vec<EPC>(a.mean, ch0 + c, mu); load_vec<EPC>(a.rstd, ch0 + c, rs); }
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          av[r * HEAD_LD + ch0 + c + e] = fmaxf(fmaf(y[e], s[e], t[e]), 0.f);
+          if constexpr (MODE != PCS_HEAD_FWD) xh[r * HEAD_LD + ch0 + c + e] = (y[e] - mu[e]) * rs[e];
+        }
+      }
+    }
+    __syncthreads();
+    // phase 2: logits (quad reduction), CE and dlogits
+    {
+      float lg[HEAD_MAXC];
+#pragma unroll
+      for (int c = 0; c < HEAD_MAXC; ++c) {
+        float p = 0.f;
+        if (c < C && rv) {
+          for (int e = 0; e < QCH; ++e) p = fmaf(av[r * HEAD_LD + ch0 + e], wl[c * HEAD_CIN + ch0 + e], p);
+        }
+        p += __shfl_xor(p, 1);
+        p += __shfl_xor(p, 2);
+        lg[c] = c < C ? p + a.bias[c] : 0.f;
+      }
+      if (rv) {
+        if (a.logits) {
+          for (int c = q; c < C; c += 4) a.logits[grow * C + c] = lg[c];
+        }
+        if constexpr (MODE == PCS_HEAD_CE) {
+          float mx = -__builtin_huge_valf();
+#pragma unroll
+          for (int c = 0; c < HEAD_MAXC; ++c) if (c < C) mx = fmaxf(mx, lg[c]);
+          float se = 0.f;
+#pragma unroll
+          for (int c = 0; c < HEAD_MAXC; ++c) if (c < C) se += expf(lg[c] - mx);
+          const float lse = mx + logf(se);
+          const int64_t lab = a.labels[grow];
+          const bool ok = lab >= 0 && lab < C;
+          const float w = ok ? a.class_weight[lab] : 0.f;
+          const float gsc = a.wsum ? 1.f / *a.wsum : 1.f;
+          if (q == 0 && ok) {
+            float zl = 0.f;
+#pragma unroll
+            for (int c = 0; c < HEAD_MAXC; ++c) if (c == lab) zl = lg[c];
+            loss_acc += w * (lse - zl);
+          }
+          for (int c = q; c < C; c += 4) {
+            const float p = expf(lg[c] - lse);
+            dl[r * HEAD_MAXC + c] = ok ? w * gsc * (p - (c == lab ? 1.f : 0.f)) : 0.f;
+          }
+        } else if constexpr (MODE == PCS_HEAD_BWD) {
+          for (int c = q; c < C; c += 4)
+            dl[r * HEAD_MAXC + c] = a.dlogits[grow * a.dl_stride_row + c * a.dl_stride_col];
+        }
+      } else if constexpr (MODE != PCS_HEAD_FWD) {
+        for (int c = q; c < C; c += 4) dl[r * HEAD_MAXC + c] = 0.f;
+      }
+    }
+    if constexpr (MODE != PCS_HEAD_FWD) {
+      __syncthreads();
+      // phase 3: dA = dl W, dz = relu'(z) dA, store, S1/S2
+      if (rv) {
+#pragma unroll
+        for (int c = 0; c < QCH; c += EPC) {
+          float v[EPC];
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            const int ch = ch0 + c + e;
+            float d = 0.f;
+            for (int k = 0; k < C; ++k) d = fmaf(dl[r * HEAD_MAXC + k], wl[k * HEAD_CIN + ch], d);
+            const float dz = av[r * HEAD_LD + ch] > 0.f ? d : 0.f;
+            v[e] = dz;
+            s1[c + e] += dz;
+            s2[c + e] = fmaf(dz, xh[r * HEAD_LD + ch], s2[c + e]);
+          }
+          *reinterpret_cast<uint4 *>(dZ + grow * HEAD_CIN + ch0 + c) = pack_chunk(v);
+        }
+      }
+      // phase 4: dW / db partials (each weight or bias entry owned by one thread);
+      // layout [C*Cin weights | C biases] = flat parameter order of seg_conv4
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        const int p = tid + i * THREADS;
+        if (p < C * (HEAD_CIN + 1)) {
+          const bool isb = p >= C * HEAD_CIN;
+          const int c = isb ? p - C * HEAD_CIN : p / HEAD_CIN, ch = isb ? 0 : p % HEAD_CIN;
+          float acc = wacc[i];
+          for (int rr = 0; rr < valid; ++rr)
+            acc = fmaf(dl[rr * HEAD_MAXC + c], isb ? 1.f : av[rr * HEAD_LD + ch], acc);
+          wacc[i] = acc;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (MODE != PCS_HEAD_FWD) {
+    if (t_begin >= t_end) return;
+    // S1/S2: reduce the 64 row-threads that share a channel quarter
+    float *red = av;  // reuse [64][129] x 2 (av, xh contiguous)
+#pragma unroll
+    for (int e = 0; e < QCH; ++e) {
+      av[r * HEAD_LD + ch0 + e] = s1[e];
+      xh[r * HEAD_LD + ch0 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < HEAD_CIN) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int j = 0; j < HEAD_R; ++j) { a1 += av[j * HEAD_LD + tid]; a2 += xh[j * HEAD_LD + tid]; }
+      *reinterpret_cast<float2 *>(a.stats + ((int64_t)blockIdx.x * HEAD_CIN + tid) * 2) = make_float2(a1, a2);
+    }
+    (void)red;
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      const int p = tid + i * THREADS;
+      if (p < C * (HEAD_CIN + 1)) a.wpartial[(int64_t)blockIdx.x * C * (HEAD_CIN + 1) + p] = wacc[i];
+    }
+    if constexpr (MODE == PCS_HEAD_CE) {
+      const float ls = wave_sum(loss_acc);
+      if ((tid & 63) == 0) lred[tid >> 6] = ls;
+      __syncthreads();
+      if (tid == 0) a.loss_partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// misc
+// ---------------------------------------------------------------------------------------
+__global__ void ce_count_kernel(const int64_t *labels, int64_t M, int C, unsigned long long *counts) {
+  __shared__ unsigned int h[HEAD_MAXC];
+  if (threadIdx.x < HEAD_MAXC) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = labels[i];
+    if (l >= 0 && l < C) atomicAdd(&h[l], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < C && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+__global__ void ce_wsum_kernel(const unsigned long long *counts, const float *w, int C, float *out) {
+  if (threadIdx.x != 0) return;
+  double s = 0, n = 0;
+  for (int c = 0; c < C; ++c) { s += (double)counts[c] * (double)w[c]; n += (double)counts[c]; }
+  out[0] = (float)s;
+  out[1] = (float)n;
+  out[2] = s > 0 ? (float)(1.0 / s) : 0.f;
+}
+
+// Philox4x32-10
+PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr[2];
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    const uint32_t n0 = h1 ^ ctr[1] ^ k0, n2 = h0 ^ ctr[3] ^ k1;
+    ctr[0] = n0; ctr[1] = l1; ctr[2] = n2; ctr[3] = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+__global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbytes, uint32_t thr,
+                                    uint8_t *bits) {
+  // byte j covers elements 8j..8j+7; one Philox call gives 8 16-bit uniforms
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nbytes) return;
+  uint32_t ctr[4] = {(uint32_t)j, (uint32_t)((uint64_t)j >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
+  philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t lo = ctr[i] & 0xffffu, hi = ctr[i] >> 16;
+    b |= (lo >= thr ? 1u : 0u) << (2 * i);
+    b |= (hi >= thr ? 1u : 0u) << (2 * i + 1);
+  }
+  bits[j] = (uint8_t)b;
+}
+
+__global__ void reduce_partials_kernel(const float *partial, int64_t nslabs, int64_t len, float scale,
+                                       float *out, int64_t ldo, int64_t row_len) {
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= len) return;
+  if (i4 + 4 <= len && (row_len & 3) == 0) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t k = 0; k < nslabs; ++k) {
+      const float4 p = *reinterpret_cast<const float4 *>(partial + k * len + i4);
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+    const int64_t row = i4 / row_len, col = i4 % row_len;
+    *reinterpret_cast<float4 *>(out + row * ldo + col) =
+        make_float4(s.x * scale, s.y * scale, s.z * scale, s.w * scale);
+  } else {
+    for (int64_t i = i4; i < len && i < i4 + 4; ++i) {
+      float s = 0.f;
+      for (int64_t k = 0; k < nslabs; ++k) s += partial[k * len + i];
+      out[(i / row_len) * ldo + i % row_len] = s * scale;
+    }
+  }
+}
+
+template <typename T>
+__global__ void cast_weight_kernel(const float *W, int64_t rows, int64_t cols, int64_t ldw, T *Wc, T *WcT) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const float v = W[(i / cols) * ldw + i % cols];
+  T o;
+  if constexpr (sizeof(T) == 4) o = v;
+  else o = (T)(pack2bf(v, 0.f) & 0xffffu);
+  if (Wc) Wc[i] = o;
+  if (WcT) WcT[(i % cols) * rows + i / cols] = o;
+}
+
+__global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_t n,
+                            const float *gscale, float lr, float b1, float b2, float eps, float wd,
+                            float bc1, float bc2_sqrt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gs = gscale ? *gscale : 1.f;
+  const float pi = p[i];
+  const float gi = fmaf(g[i], gs, 0.f) + wd * pi;
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = pi - (lr / bc1) * (mi / denom);
+}
+
+int blocks_for(int64_t n, int per) { return (int)((n + per - 1) / per); }
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+static int64_t chunk_geo(int64_t N, int64_t B, int64_t tile, int32_t *cps_io, int64_t target) {
+  const int64_t tps = (N + tile - 1) / tile;
+  int64_t cps = *cps_io;
+  if (cps <= 0) cps = (target + B - 1) / B;
+  if (cps > tps) cps = tps;
+  if (cps < 1) cps = 1;
+  const int64_t tpc = (tps + cps - 1) / cps;
+  cps = (tps + tpc - 1) / tpc;
+  *cps_io = (int32_t)cps;
+  return tpc;
+}
+
+extern "C" int pcs_conv1_fwd(const pcs_gemm_args *ap, pcs_stream_t stream) {
+  if (!ap || !ap->A || !ap->W || !ap->C) return pcs_set_einval("pcs_conv1_fwd", "missing operand");
+  if (ap->K != 4 || ap->Ncols != 64) return pcs_set_einval("pcs_conv1_fwd", "conv1 is 4 -> 64");
+  pcs_gemm_args a = *ap;
+  const int64_t tpc = chunk_geo(a.scene_rows, a.num_scenes, C1_BM, &a.chunks_per_scene, 1024);
+  const int tps = (int)((a.scene_rows + C1_BM - 1) / C1_BM);
+  const int nb = (int)(a.num_scenes * a.chunks_per_scene);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a.dtype == PCS_BF16)
+    hipLaunchKernelGGL(conv1_fwd_kernel<bf16_t>, dim3(nb), dim3(THREADS), 0, s, a, tps, (int)tpc);
+  else if (a.dtype == PCS_F32)
+    hipLaunchKernelGGL(conv1_fwd_kernel<float>, dim3(nb), dim3(THREADS), 0, s, a, tps, (int)tpc);
+  else return pcs_set_einval("pcs_conv1_fwd", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_conv1_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
+  if (!ap || !ap->dZ || !ap->Y || !ap->X || !ap->partial || !ap->dW)
+    return pcs_set_einval("pcs_conv1_wgrad", "missing operand");
+  if (ap->Cout != 64 || ap->Cin != 4) return pcs_set_einval("pcs_conv1_wgrad", "conv1 is 4 -> 64");
+  pcs_wgrad_args a = *ap;
+  if (a.splits_per_scene <= 0) {
+    int64_t sps = (1024 + a.num_scenes - 1) / a.num_scenes;
+    const int64_t maxs = (a.scene_rows + 255) / 256;
+    if (sps > maxs) sps = maxs;
+    if (sps < 1) sps = 1;
+    a.splits_per_scene = (int32_t)sps;
+  }
+  const int64_t rps = (a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene;
+  const int nb = (int)(a.num_scenes * a.splits_per_scene);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a.dtype == PCS_BF16)
+    hipLaunchKernelGGL(conv1_wgrad_kernel<bf16_t>, dim3(nb), dim3(THREADS), 0, s, a, rps);
+  else if (a.dtype == PCS_F32)
+    hipLaunchKernelGGL(conv1_wgrad_kernel<float>, dim3(nb), dim3(THREADS), 0, s, a, rps);
+  else return pcs_set_einval("pcs_conv1_wgrad", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return pcs_reduce_partials(a.partial, nb, 64 * 4, 1.f, a.dW, a.ldw ? a.ldw : 4, 4, stream);
+}
+
+extern "C" int pcs_bn_fwd_finalize(const float *stats, int64_t B, int64_t N, int32_t C, int32_t cps,
+                                   int64_t rpc, const float *gamma, const float *beta,
+                                   float *running_mean, float *running_var, float momentum,
+                                   float eps, int32_t update_running, float *mean, float *rstd,
+                                   float *scale, float *shift, float *scene_sum,
+                                   pcs_stream_t stream) {
+  if (!stats || !gamma || !beta || !mean || !rstd || !scale || !shift || C <= 0 || cps <= 0 || rpc <= 0)
+    return pcs_set_einval("pcs_bn_fwd_finalize", "bad arguments");
+  if (update_running && (!running_mean || !running_var))
+    return pcs_set_einval("pcs_bn_fwd_finalize", "running buffers required");
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(C), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                     stats, B, N, (int)C, (int)cps, rpc, gamma, beta, running_mean, running_var,
+                     momentum, eps, (int)update_running, mean, rstd, scale, shift, scene_sum);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_bn_eval_coefs(const float *gamma, const float *beta, const float *rm,
+                                 const float *rv, float eps, int32_t C, float *scale, float *shift,
+                                 pcs_stream_t stream) {
+  if (!gamma || !beta || !rm || !rv || !scale || !shift) return pcs_set_einval("pcs_bn_eval_coefs", "null");
+  hipLaunchKernelGGL(bn_eval_kernel, dim3(blocks_for(C, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), gamma, beta, rm, rv, eps, (int)C, scale, shift);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_bn_bwd_finalize(const float *stats, int64_t B, int64_t N, int32_t C, int32_t cps,
+                                   const float *mean, const float *rstd, const float *gamma,
+                                   const float *scene_sum, float *alpha, float *beta_c,
+                                   float *gamma_c, float *dgamma, float *dbeta, float *dbias,
+                                   float *scene_s1, pcs_stream_t stream) {
+  if (!stats || !mean || !rstd || !gamma || !alpha || !beta_c || !gamma_c)
+    return pcs_set_einval("pcs_bn_bwd_finalize", "null argument");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                     stats, B, N, (int)C, (int)cps, mean, rstd, gamma, scene_sum, alpha, beta_c,
+                     gamma_c, dgamma, dbeta, dbias, scene_s1);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_pool_finalize(const float *pool, int64_t B, int64_t N, int32_t C, int32_t cps,
+                                 const float *s, const float *t, float *g, int32_t *am, float *ysel,
+                                 pcs_stream_t stream) {
+  if (!pool || !s || !t || !g || !am || !ysel) return pcs_set_einval("pcs_pool_finalize", "null argument");
+  hipLaunchKernelGGL(pool_finalize_kernel, dim3(blocks_for(B * C, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), pool, B, N, (int)C, (int)cps, s, t, g, am, ysel);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_scene_gemv(const float *g, int64_t B, int32_t Kg, const float *W, int64_t ldw,
+                              int32_t col_off, const float *bias, int32_t Nout, float *out,
+                              pcs_stream_t stream) {
+  if (!g || !W || !out) return pcs_set_einval("pcs_scene_gemv", "null argument");
+  hipLaunchKernelGGL(scene_gemv_kernel, dim3(blocks_for(B * Nout * 64, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), g, B, (int)Kg, W, ldw, (int)col_off, bias,
+                     (int)Nout, out);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_pool_bwd(const pcs_pool_bwd_args *ap, pcs_stream_t stream) {
+  if (!ap) return pcs_set_einval("pcs_pool_bwd", "null args");
+  const pcs_pool_bwd_args &a = *ap;
+  if (!a.s1_alpha || !a.s1_beta || !a.s1_gamma || !a.s1_scene_s1 || !a.s1_scene_sum || !a.W_s1 ||
+      !a.g || !a.ysel || !a.g_mean || !a.g_rstd || !a.g_gamma || !a.g_scene_sum ||
+      !a.dW_s1_global || !a.csum || !a.alpha || !a.beta_c || !a.gamma_c || !a.dgamma || !a.dbeta ||
+      !a.dbias || !a.sp)
+    return pcs_set_einval("pcs_pool_bwd", "null argument");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(pool_bwd_csum_kernel, dim3(blocks_for(a.num_scenes * a.Cs, 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pool_bwd_dw_kernel, dim3(blocks_for((int64_t)a.Cs * a.Cg, 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pool_bwd_coef_kernel, dim3(blocks_for(a.Cg, 64)), dim3(64), 0, s, a);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t pcs_head_geometry(pcs_head_args *a) {
+  if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_head_geometry", "bad geometry");
+  const int64_t tpc = chunk_geo(a->scene_rows, a->num_scenes, HEAD_R, &a->chunks_per_scene, 2048);
+  return tpc * HEAD_R;
+}
+
+extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
+  if (!ap) return pcs_set_einval("pcs_head", "null args");
+  pcs_head_args a = *ap;
+  if (a.Cin != HEAD_CIN) return pcs_set_einval("pcs_head", "head input must have 128 channels");
+  if (a.num_classes < 1 || a.num_classes > HEAD_MAXC) return pcs_set_einval("pcs_head", "1 <= C <= 16");
+  if (!a.Y || !a.s || !a.t || !a.W || !a.bias) return pcs_set_einval("pcs_head", "missing operand");
+  if (a.mode == PCS_HEAD_CE && (!a.labels || !a.class_weight || !a.loss_partial))
+    return pcs_set_einval("pcs_head", "CE mode needs labels, class_weight, loss_partial");
+  if (a.mode == PCS_HEAD_BWD && !a.dlogits) return pcs_set_einval("pcs_head", "BWD mode needs dlogits");
+  if (a.mode != PCS_HEAD_FWD && (!a.dZ || !a.mean || !a.rstd || !a.stats || !a.wpartial))
+    return pcs_set_einval("pcs_head", "backward outputs missing");
+  const int64_t rpc = pcs_head_geometry(&a);
+  if (rpc < 0) return (int)rpc;
+  const int tps = (int)((a.scene_rows + HEAD_R - 1) / HEAD_R);
+  const int tpc = (int)(rpc / HEAD_R);
+  const int nb = (int)(a.num_scenes * a.chunks_per_scene);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define PCS_HEAD_LAUNCH(T, MODE) \
+  hipLaunchKernelGGL((head_kernel<T, MODE>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc)
+  if (a.dtype == PCS_BF16) {
+    if (a.mode == PCS_HEAD_FWD) PCS_HEAD_LAUNCH(bf16_t, PCS_HEAD_FWD);
+    else if (a.mode == PCS_HEAD_CE) PCS_HEAD_LAUNCH(bf16_t, PCS_HEAD_CE);
+    else PCS_HEAD_LAUNCH(bf16_t, PCS_HEAD_BWD);
+  } else if (a.dtype == PCS_F32) {
+    if (a.mode == PCS_HEAD_FWD) PCS_HEAD_LAUNCH(float, PCS_HEAD_FWD);
+    else if (a.mode == PCS_HEAD_CE) PCS_HEAD_LAUNCH(float, PCS_HEAD_CE);
+    else PCS_HEAD_LAUNCH(float, PCS_HEAD_BWD);
+  } else {
+    return pcs_set_einval("pcs_head", "bad dtype");
+  }
+#undef PCS_HEAD_LAUNCH
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weight, int32_t C,
+                                 int64_t *counts_ws, float *out, pcs_stream_t stream) {
+  if (!labels || !class_weight || !counts_ws || !out || C < 1 || C > HEAD_MAXC)
+    return pcs_set_einval("pcs_ce_weight_sum", "bad arguments");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(counts_ws, 0, sizeof(int64_t) * C, s);
+  if (e != hipSuccess) return pcs_set_error(e, "pcs_ce_weight_sum");
+  int nb = blocks_for(M, 256);
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(ce_count_kernel, dim3(nb), dim3(256), 0, s, labels, M, (int)C,
+                     reinterpret_cast<unsigned long long *>(counts_ws));
+  hipLaunchKernelGGL(ce_wsum_kernel, dim3(1), dim3(64), 0, s,
+                     reinterpret_cast<const unsigned long long *>(counts_ws), class_weight, (int)C, out);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                                uint8_t *bits, pcs_stream_t stream) {
+  if (!bits || C % 8 != 0 || p < 0.f || p >= 1.f) return pcs_set_einval("pcs_dropout_bits", "bad arguments");
+  const int64_t nbytes = M * (C / 8);
+  const uint32_t thr = (uint32_t)(p * 65536.0f + 0.5f);
+  hipLaunchKernelGGL(dropout_bits_kernel, dim3(blocks_for(nbytes, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), seed, offset, nbytes, thr, bits);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale, float *out,
+                                   int64_t ldo, int64_t row_len, pcs_stream_t stream) {
+  if (!partial || !out || len <= 0 || nslabs <= 0 || row_len <= 0) return pcs_set_einval("pcs_reduce_partials", "bad arguments");
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks_for((len + 3) / 4, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), partial, nslabs, len, scale, out, ldo, row_len);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_cast_weight(const float *W, int64_t rows, int64_t cols, int64_t ldw, int32_t dtype, void *Wc,
+                               void *WcT, pcs_stream_t stream) {
+  if (!W) return pcs_set_einval("pcs_cast_weight", "null W");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = blocks_for(rows * cols, 256);
+  if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(cast_weight_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, W, rows, cols, ldw,
+                       reinterpret_cast<bf16_t *>(Wc), reinterpret_cast<bf16_t *>(WcT));
+  else if (dtype == PCS_F32)
+    hipLaunchKernelGGL(cast_weight_kernel<float>, dim3(nb), dim3(256), 0, s, W, rows, cols, ldw,
+                       reinterpret_cast<float *>(Wc), reinterpret_cast<float *>(WcT));
+  else return pcs_set_einval("pcs_cast_weight", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                        const float *grad_scale, float lr, float beta1, float beta2, float eps,
+                        float weight_decay, int64_t step, pcs_stream_t stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || step < 1) return pcs_set_einval("pcs_adam", "bad arguments");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     param, grad, exp_avg, exp_avg_sq, n, grad_scale, lr, beta1, beta2, eps,
+                     weight_decay, (float)bc1, (float)sqrt(bc2));
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,470 @@
+"""Kernel orchestration for one PointNetSegmentation training / inference pass.
+
+Host side of the hot path: allocates (through torch's caching allocator) the points-major
+activation buffers, and launches the HIP kernels of libpcs.so in dependency order on the
+current stream.  Nothing here computes on the CPU; every numeric op is a C-ABI call.
+
+Per layer l the forward stores only Y_l = conv_l(a_{l-1}) (pre-BN, fp32 or bf16);
+a_l = relu(bn_l(Y_l)) [* dropout] is recomputed inside whichever kernel consumes it.
+The backward stores dZ_l = dL/d(BN_l output) after the ReLU / dropout masks and forms
+dy_l = alpha*dZ_l + beta + gamma*Y_l on the fly in the dgrad / wgrad kernels.
+
+Reference map (point_cloud_segmentation.py, P:<line>):
+  forward P:98-133, loss P:216/251, backward P:254, running stats (nn.BatchNorm1d).
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as L
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+DROPOUT_P = 0.3
+
+# (conv, Cin, Cout, bn) in registration order; Cin of conv1 / Cout of seg_conv4 filled in
+CONVS = [
+    ("conv1", None, 64, "bn1"),
+    ("conv2", 64, 64, "bn2"),
+    ("conv3", 64, 64, "bn3"),
+    ("conv4", 64, 128, "bn4"),
+    ("conv5", 128, 1024, "bn5"),
+    ("global_feat", 1024, 1024, "bn_global"),
+    ("seg_conv1", 1088, 512, "bn_seg1"),
+    ("seg_conv2", 512, 256, "bn_seg2"),
+    ("seg_conv3", 256, 128, "bn_seg3"),
+    ("seg_conv4", 128, None, None),
+]
+BNS = [(bn, cout) for _, _, cout, bn in CONVS if bn]
+
+
+def param_layout(num_classes: int, input_dim: int = 4):
+    """[(name, shape)] of the parameters in registration order (== module.parameters())."""
+    out = []
+    for conv, cin, cout, _ in CONVS:
+        cin = input_dim if cin is None else cin
+        cout = num_classes if cout is None else cout
+        out += [(f"{conv}.weight", (cout, cin, 1)), (f"{conv}.bias", (cout,))]
+    for bn, c in BNS:
+        out += [(f"{bn}.weight", (c,)), (f"{bn}.bias", (c,))]
+    return out
+
+
+def _dt(dtype: str):
+    if dtype == "fp32":
+        return L.F32, torch.float32
+    if dtype == "bf16":
+        return L.BF16, torch.bfloat16
+    raise ValueError(f"compute dtype must be 'fp32' or 'bf16', got {dtype!r}")
+
+
+@dataclass
+class BNCoef:
+    """Per-BN vectors produced by the forward finalisation (all fp32 [C] / [B,C])."""
+    mean: torch.Tensor
+    rstd: torch.Tensor
+    scale: torch.Tensor
+    shift: torch.Tensor
+    scene_sum: torch.Tensor
+
+
+@dataclass
+class Saved:
+    """Everything the backward needs from one forward."""
+    B: int
+    N: int
+    train: bool
+    ys: dict = field(default_factory=dict)        # conv name -> Y tensor [M, C]
+    bn: dict = field(default_factory=dict)        # bn name -> BNCoef
+    masks: tuple = (None, None)                   # dropout keep bits (seg1 out, seg2 out)
+    g: torch.Tensor = None
+    am: torch.Tensor = None
+    ysel: torch.Tensor = None
+    x: torch.Tensor = None
+    logits: torch.Tensor = None
+    wc: dict = None                               # cast weights used by this pass
+
+
+class Engine:
+    """Launches the PointNetSegmentation kernels for one compute dtype and device."""
+
+    def __init__(self, num_classes: int, dtype: str = "fp32", input_dim: int = 4):
+        if input_dim != 4:
+            raise NotImplementedError("the conv1 kernel is specialised for input_dim=4 (x,y,z,e)")
+        if not 1 <= num_classes <= 16:
+            raise NotImplementedError("the fused head supports 1..16 classes")
+        self.C = num_classes
+        self.dtype = dtype
+        self.dt, self.tdt = _dt(dtype)
+        self.layout = param_layout(num_classes, input_dim)
+        self.numel = {n: int(torch.Size(s).numel()) for n, s in self.layout}
+        self.offsets = {}
+        off = 0
+        for n, _ in self.layout:
+            self.offsets[n] = off
+            off += self.numel[n]
+        self.total_params = off
+        self._geo = {}
+        L.load()
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return L.stream_ptr()
+
+    def geometry(self, B, N, ncols):
+        key = (B, N, ncols)
+        if key not in self._geo:
+            a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=ncols, dtype=self.dt,
+                           chunks_per_scene=0)
+            rpc = L.load().pcs_gemm_geometry(ct.byref(a))
+            if rpc <= 0:
+                raise L.PcsError(L.load().pcs_last_error().decode())
+            self._geo[key] = (a.chunks_per_scene, rpc)
+        return self._geo[key]
+
+    def _empty(self, *shape, dtype=None, device):
+        return torch.empty(*shape, dtype=dtype or self.tdt, device=device)
+
+    def cast_weights(self, P):
+        """fp32 parameters -> compute-dtype W and W^T copies (every call: params may change)."""
+        dev = P["conv2.weight"].device
+        wc = {}
+        s = self._stream()
+        for conv, cin, cout, _ in CONVS:
+            if conv in ("conv1", "seg_conv4"):
+                continue
+            W = P[f"{conv}.weight"]
+            rows, ld = W.shape[0], W.shape[1]
+            cols = 64 if conv == "seg_conv1" else ld     # seg_conv1: local half only
+            Wc = self._empty(rows, cols, device=dev)
+            WcT = self._empty(cols, rows, device=dev)
+            L.call("pcs_cast_weight", L.ptr(W), rows, cols, ld, self.dt, L.ptr(Wc), L.ptr(WcT), s)
+            wc[conv] = (Wc, WcT)
+        return wc
+
+    def _bn_finalize(self, bnname, stats, B, N, C, cps, rpc, P, bufs, train, dev):
+        coef = BNCoef(*(torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4)),
+                      torch.empty(B, C, dtype=torch.float32, device=dev))
+        g, b = P[f"{bnname}.weight"], P[f"{bnname}.bias"]
+        if train:
+            rm, rv = bufs.get(f"{bnname}.running_mean"), bufs.get(f"{bnname}.running_var")
+            upd = int(rm is not None and rv is not None)
+            L.call("pcs_bn_fwd_finalize", L.ptr(stats), B, N, C, cps, rpc, L.ptr(g), L.ptr(b),
+                   L.ptr(rm), L.ptr(rv), BN_MOMENTUM, BN_EPS, upd, L.ptr(coef.mean),
+                   L.ptr(coef.rstd), L.ptr(coef.scale), L.ptr(coef.shift), L.ptr(coef.scene_sum),
+                   self._stream())
+        else:
+            L.call("pcs_bn_eval_coefs", L.ptr(g), L.ptr(b), L.ptr(bufs[f"{bnname}.running_mean"]),
+                   L.ptr(bufs[f"{bnname}.running_var"]), BN_EPS, C, L.ptr(coef.scale),
+                   L.ptr(coef.shift), self._stream())
+        return coef
+
+    def _gemm(self, B, N, K, ncols, pro, epi, A, W, C, **kw):
+        cps, _ = self.geometry(B, N, ncols)
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
+                       prologue=pro, epilogue=epi, chunks_per_scene=cps,
+                       A=L.ptr(A), W=L.ptr(W), C=L.ptr(C),
+                       a_keep_scale=kw.pop("a_keep_scale", 1.0),
+                       c_keep_scale=kw.pop("c_keep_scale", 1.0))
+        for k, v in kw.items():
+            setattr(a, k, L.ptr(v))
+        L.call("pcs_gemm", ct.byref(a), self._stream())
+
+    def _wgrad(self, B, N, cout, cin, dy_mode, x_mode, dW, ldw=0, **kw):
+        a = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=cout, Cin=cin, dtype=self.dt,
+                        splits_per_scene=0, dy_mode=dy_mode, x_mode=x_mode,
+                        x_keep_scale=kw.pop("x_keep_scale", 1.0), dW=L.ptr(dW), ldw=ldw)
+        for k, v in kw.items():
+            setattr(a, k, L.ptr(v))
+        fn = "pcs_conv1_wgrad" if cin == 4 else "pcs_wgrad"
+        if cin == 4:
+            a.splits_per_scene = max(1, min((1024 + B - 1) // B, (N + 255) // 256))
+            nbytes = B * a.splits_per_scene * cout * cin * 4
+        else:
+            nbytes = L.load().pcs_wgrad_workspace(ct.byref(a))
+        ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dW.device)
+        a.partial = ws.data_ptr()
+        L.call(fn, ct.byref(a), self._stream())
+        return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, P, bufs, x, *, train, masks=None, seed=0, head_mode=L.HEAD_FWD,
+                labels=None, class_weight=None, wsum=None, want_logits=True, saved=None):
+        """Forward pass.  P: name -> fp32 parameter tensor; bufs: BN running buffers.
+
+        ``masks`` = (bits1 [M,64] u8, bits2 [M,32] u8) replays dropout keep bits; otherwise
+        train mode draws them with Philox from ``seed``.  With ``head_mode=HEAD_CE`` the
+        head kernel also computes the weighted CE loss and starts the backward (fused
+        train step); returns the Saved context (plus head outputs in ``saved.head``).
+        """
+        if not x.is_cuda:
+            raise RuntimeError("pcs_amd runs on a HIP device only (no CPU fallback)")
+        dev = x.device
+        B, N, D = x.shape
+        M = B * N
+        s = self._stream()
+        x = x.contiguous().float()
+        sv = Saved(B=B, N=N, train=train) if saved is None else saved
+        sv.B, sv.N, sv.train, sv.x = B, N, train, x
+        sv.wc = wc = self.cast_weights(P)
+        T = self.tdt
+
+        def stats_buf(ncols):
+            cps, rpc = self.geometry(B, N, ncols)
+            return torch.empty(B * cps, ncols, 2, dtype=torch.float32, device=dev), cps, rpc
+
+        def bnrelu(prev):
+            c = sv.bn[prev]
+            return dict(pa=c.scale, pb=c.shift)
+
+        # eval: all BN coefficients come from the running buffers
+        if not train:
+            for bn, C in BNS:
+                sv.bn[bn] = self._bn_finalize(bn, None, B, N, C, 1, 1, P, bufs, False, dev)
+
+        # conv1 (K=4)
+        y1 = self._empty(M, 64, device=dev)
+        st, cps, rpc = stats_buf(64) if train else (None, *self.geometry(B, N, 64))
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=4, Ncols=64, dtype=self.dt,
+                       chunks_per_scene=cps, A=L.ptr(x), W=L.ptr(P["conv1.weight"]),
+                       C=L.ptr(y1), bias=L.ptr(P["conv1.bias"]), stats=L.ptr(st))
+        L.call("pcs_conv1_fwd", ct.byref(a), s)
+        sv.ys["conv1"] = y1
+        if train:
+            sv.bn["bn1"] = self._bn_finalize("bn1", st, B, N, 64, cps, rpc, P, bufs, True, dev)
+
+        def layer(conv, src_conv, src_bn, K, ncols, bnname, **kw):
+            y = self._empty(M, ncols, device=dev)
+            st, cps, rpc = stats_buf(ncols) if train else (None, 0, 0)
+            self._gemm(B, N, K, ncols, L.PRO_BNRELU, L.EPI_FWD, sv.ys[src_conv], wc[conv][0], y,
+                       stats=st, **bnrelu(src_bn), **kw)
+            sv.ys[conv] = y
+            if train:
+                sv.bn[bnname] = self._bn_finalize(bnname, st, B, N, ncols, cps, rpc, P, bufs, True, dev)
+            return y
+
+        layer("conv2", "conv1", "bn1", 64, 64, "bn2", bias=P["conv2.bias"])
+        layer("conv3", "conv2", "bn2", 64, 64, "bn3", bias=P["conv3.bias"])
+        layer("conv4", "conv3", "bn3", 64, 128, "bn4", bias=P["conv4.bias"])
+        layer("conv5", "conv4", "bn4", 128, 1024, "bn5", bias=P["conv5.bias"])
+
+        # global_feat + max-pool partials
+        cps_g, _ = self.geometry(B, N, 1024)
+        pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
+        layer("global_feat", "conv5", "bn5", 1024, 1024, "bn_global", bias=P["global_feat.bias"],
+              pool=pool)
+        cg = sv.bn["bn_global"]
+        sv.g = torch.empty(B, 1024, dtype=torch.float32, device=dev)
+        sv.am = torch.empty(B, 1024, dtype=torch.int32, device=dev)
+        sv.ysel = torch.empty(B, 1024, dtype=torch.float32, device=dev)
+        L.call("pcs_pool_finalize", L.ptr(pool), B, N, 1024, cps_g, L.ptr(cg.scale), L.ptr(cg.shift),
+               L.ptr(sv.g), L.ptr(sv.am), L.ptr(sv.ysel), s)
+
+        # seg_conv1 = local 64->512 GEMM + per-scene bias (W_global . g_b + b)   P:117-123
+        sbias = torch.empty(B, 512, dtype=torch.float32, device=dev)
+        Ws1 = P["seg_conv1.weight"]
+        L.call("pcs_scene_gemv", L.ptr(sv.g), B, 1024, L.ptr(Ws1), Ws1.shape[1], 64,
+               L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), s)
+        layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", scene_bias=sbias)
+
+        # dropout keep bits (P:124, P:126)
+        if train:
+            if masks is not None:
+                m1, m2 = masks
+            else:
+                m1 = torch.empty(M, 64, dtype=torch.uint8, device=dev)
+                m2 = torch.empty(M, 32, dtype=torch.uint8, device=dev)
+                L.call("pcs_dropout_bits", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), s)
+                L.call("pcs_dropout_bits", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), s)
+            sv.masks = (m1, m2)
+            keep = 1.0 / (1.0 - DROPOUT_P)
+        else:
+            m1 = m2 = None
+            sv.masks = (None, None)
+            keep = 1.0
+        layer("seg_conv2", "seg_conv1", "bn_seg1", 512, 256, "bn_seg2", bias=P["seg_conv2.bias"],
+              a_mask=m1, a_keep_scale=keep)
+        layer("seg_conv3", "seg_conv2", "bn_seg2", 256, 128, "bn_seg3", bias=P["seg_conv3.bias"],
+              a_mask=m2, a_keep_scale=keep)
+
+        # head: seg_conv4 (+ CE and the start of the backward when fused)
+        sv.logits = (torch.empty(B, N, self.C, dtype=torch.float32, device=dev)
+                     if want_logits else None)
+        if head_mode == L.HEAD_CE:
+            sv.head = self._head(P, sv, L.HEAD_CE, labels=labels, class_weight=class_weight,
+                                 wsum=wsum)
+        else:
+            self._head(P, sv, L.HEAD_FWD)
+        return sv
+
+    def _head(self, P, sv, mode, labels=None, class_weight=None, wsum=None, dlogits=None):
+        """seg_conv4 + (CE | given dlogits) + head backward; returns the backward buffers."""
+        B, N = sv.B, sv.N
+        dev = sv.x.device
+        c3 = sv.bn["bn_seg3"]
+        ha = L.HeadArgs(num_scenes=B, scene_rows=N, Cin=128, num_classes=self.C, dtype=self.dt,
+                        mode=mode, chunks_per_scene=0, Y=L.ptr(sv.ys["seg_conv3"]),
+                        s=L.ptr(c3.scale), t=L.ptr(c3.shift), W=L.ptr(P["seg_conv4.weight"]),
+                        bias=L.ptr(P["seg_conv4.bias"]),
+                        logits=L.ptr(sv.logits) if mode != L.HEAD_BWD else None)
+        hb = None
+        if mode != L.HEAD_FWD:
+            L.load().pcs_head_geometry(ct.byref(ha))
+            nch = B * ha.chunks_per_scene
+            hb = dict(dZ=torch.empty(B * N * 1024, dtype=self.tdt, device=dev),
+                      stats=torch.empty(nch, 128, 2, dtype=torch.float32, device=dev),
+                      wpartial=torch.empty(nch, self.C * 129, dtype=torch.float32, device=dev),
+                      loss_partial=torch.empty(nch, dtype=torch.float32, device=dev),
+                      cps=ha.chunks_per_scene, nch=nch)
+            ha.dZ, ha.stats = L.ptr(hb["dZ"]), L.ptr(hb["stats"])
+            ha.wpartial, ha.loss_partial = L.ptr(hb["wpartial"]), L.ptr(hb["loss_partial"])
+            ha.mean, ha.rstd = L.ptr(c3.mean), L.ptr(c3.rstd)
+        if mode == L.HEAD_CE:
+            ha.labels, ha.class_weight, ha.wsum = L.ptr(labels), L.ptr(class_weight), L.ptr(wsum)
+        if mode == L.HEAD_BWD:
+            dl = dlogits.reshape(B * N, self.C) if dlogits.dim() == 3 else dlogits
+            if dl.dtype != torch.float32:
+                dl = dl.float()
+            ha.dlogits = L.ptr(dl)
+            ha.dl_stride_row, ha.dl_stride_col = dl.stride(0), dl.stride(1)
+            hb["dl"] = dl
+        L.call("pcs_head", ct.byref(ha), self._stream())
+        return hb
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, P, sv, gflat, dlogits=None):
+        """Backward pass: every parameter gradient is written into the flat fp32 buffer
+        ``gflat`` (registration order, see param_layout).  Uses the head buffers of a
+        fused CE forward, or runs the head backward on caller-supplied ``dlogits``."""
+        if not sv.train:
+            raise RuntimeError("backward needs a train-mode forward (BatchNorm batch statistics)")
+        B, N = sv.B, sv.N
+        M = B * N
+        dev = sv.x.device
+        s = self._stream()
+        wc = sv.wc
+        G = lambda name: gflat[self.offsets[name]:]   # noqa: E731  (pointer at a param's slot)
+        hb = self._head(P, sv, L.HEAD_BWD, dlogits=dlogits) if dlogits is not None else sv.head
+        keep = 1.0 / (1.0 - DROPOUT_P)
+        m1, m2 = sv.masks
+
+        # seg_conv4: weight and bias are adjacent in the flat buffer
+        L.call("pcs_reduce_partials", L.ptr(hb["wpartial"]), hb["nch"], self.C * 129, 1.0,
+               L.ptr(G("seg_conv4.weight")), self.C * 129, self.C * 129, s)
+
+        coefs = {}
+
+        def bn_bwd(bnname, conv, stats, cps, scene_s1=None):
+            fc = sv.bn[bnname]
+            C = fc.mean.shape[0]
+            al, be, ga = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(3))
+            L.call("pcs_bn_bwd_finalize", L.ptr(stats), B, N, C, cps, L.ptr(fc.mean), L.ptr(fc.rstd),
+                   L.ptr(P[f"{bnname}.weight"]), L.ptr(fc.scene_sum), L.ptr(al), L.ptr(be), L.ptr(ga),
+                   L.ptr(G(f"{bnname}.weight")), L.ptr(G(f"{bnname}.bias")),
+                   L.ptr(G(f"{conv}.bias")), L.ptr(scene_s1), s)
+            coefs[bnname] = (al, be, ga)
+
+        bn_bwd("bn_seg3", "seg_conv3", hb["stats"], hb["cps"])
+
+        bufA = hb["dZ"]
+        bufB = torch.empty(M * 1024, dtype=self.tdt, device=dev)
+        keepalive = []
+
+        def dgrad(conv, bn, cin, cout, dz, ycur, prev_conv, prev_bn, out, c_mask=None,
+                  addend=None):
+            al, be, ga = coefs[bn]
+            pc = sv.bn[prev_bn]
+            cps, _ = self.geometry(B, N, cin)
+            st = torch.empty(B * cps, cin, 2, dtype=torch.float32, device=dev)
+            self._gemm(B, N, cout, cin, L.PRO_BWD, L.EPI_DGRAD, dz, wc[conv][1], out,
+                       A2=ycur, pa=al, pb=be, pc=ga, Yp=sv.ys[prev_conv], es=pc.scale, et=pc.shift,
+                       emean=pc.mean, erstd=pc.rstd, c_mask=c_mask,
+                       c_keep_scale=keep if c_mask is not None else 1.0, addend=addend, stats=st)
+            return st, cps
+
+        def wgrad(conv, bn, cin, cout, dz, ycur, prev_conv, prev_bn, x_mask=None, ldw=0):
+            al, be, ga = coefs[bn]
+            pc = sv.bn[prev_bn]
+            keepalive.append(self._wgrad(
+                B, N, cout, cin, L.PRO_BWD, L.PRO_BNRELU, G(f"{conv}.weight"), ldw=ldw, dZ=dz,
+                Y=ycur, alpha=al, beta=be, gamma=ga, X=sv.ys[prev_conv], s=pc.scale, t=pc.shift,
+                x_mask=x_mask, x_keep_scale=keep if x_mask is not None else 1.0))
+
+        ys = sv.ys
+        # seg_conv3 (input: dropout(relu(bn_seg2(y_s2))))
+        dz_s3 = bufA
+        st, cps = dgrad("seg_conv3", "bn_seg3", 256, 128, dz_s3, ys["seg_conv3"], "seg_conv2",
+                        "bn_seg2", bufB, c_mask=m2)
+        wgrad("seg_conv3", "bn_seg3", 256, 128, dz_s3, ys["seg_conv3"], "seg_conv2", "bn_seg2", x_mask=m2)
+        bn_bwd("bn_seg2", "seg_conv2", st, cps)
+        # seg_conv2 (input: dropout(relu(bn_seg1(y_s1))))
+        dz_s2 = bufB
+        st, cps = dgrad("seg_conv2", "bn_seg2", 512, 256, dz_s2, ys["seg_conv2"], "seg_conv1",
+                        "bn_seg1", bufA, c_mask=m1)
+        wgrad("seg_conv2", "bn_seg2", 512, 256, dz_s2, ys["seg_conv2"], "seg_conv1", "bn_seg1", x_mask=m1)
+        scene_s1 = torch.empty(B, 512, dtype=torch.float32, device=dev)
+        bn_bwd("bn_seg1", "seg_conv1", st, cps, scene_s1=scene_s1)
+        dz_s1 = bufA
+
+        # repeat/cat + max-pool + bn_global backward (P:113-120)
+        a1, b1, g1 = coefs["bn_seg1"]
+        cg = sv.bn["bn_global"]
+        ag, bg, gg = (torch.empty(1024, dtype=torch.float32, device=dev) for _ in range(3))
+        sp = torch.empty(B, 1024, dtype=torch.float32, device=dev)
+        csum = torch.empty(B, 512, dtype=torch.float32, device=dev)
+        Ws1 = P["seg_conv1.weight"]
+        pa = L.PoolBwdArgs(
+            num_scenes=B, scene_rows=N, Cs=512, Cg=1024, col_off=64,
+            s1_alpha=L.ptr(a1), s1_beta=L.ptr(b1), s1_gamma=L.ptr(g1), s1_scene_s1=L.ptr(scene_s1),
+            s1_scene_sum=L.ptr(sv.bn["bn_seg1"].scene_sum), W_s1=L.ptr(Ws1), ldw=Ws1.shape[1],
+            g=L.ptr(sv.g), ysel=L.ptr(sv.ysel), g_mean=L.ptr(cg.mean), g_rstd=L.ptr(cg.rstd),
+            g_gamma=L.ptr(P["bn_global.weight"]), g_scene_sum=L.ptr(cg.scene_sum),
+            dW_s1_global=L.ptr(G("seg_conv1.weight")), csum=L.ptr(csum), alpha=L.ptr(ag),
+            beta_c=L.ptr(bg), gamma_c=L.ptr(gg), dgamma=L.ptr(G("bn_global.weight")),
+            dbeta=L.ptr(G("bn_global.bias")), dbias=L.ptr(G("global_feat.bias")), sp=L.ptr(sp))
+        L.call("pcs_pool_bwd", ct.byref(pa), s)
+
+        # seg_conv1 local half: dA2 contribution (raw) and dW[:, :64]
+        dA2 = torch.empty(M, 64, dtype=self.tdt, device=dev)
+        self._gemm(B, N, 512, 64, L.PRO_BWD, L.EPI_RAW, dz_s1, wc["seg_conv1"][1], dA2,
+                   A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1)
+        wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
+
+        # global_feat (dy from the sparse max-pool gradient)
+        pc5 = sv.bn["bn5"]
+        cps5, _ = self.geometry(B, N, 1024)
+        st = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
+        self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD, ys["global_feat"],
+                   wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
+                   Yp=ys["conv5"], es=pc5.scale, et=pc5.shift, emean=pc5.mean, erstd=pc5.rstd,
+                   stats=st)
+        keepalive.append(self._wgrad(
+            B, N, 1024, 1024, L.PRO_BWD_POOL, L.PRO_BNRELU, G("global_feat.weight"),
+            Y=ys["global_feat"], beta=bg, gamma=gg, pool_idx=sv.am, pool_coef=sp,
+            X=ys["conv5"], s=pc5.scale, t=pc5.shift))
+        bn_bwd("bn5", "conv5", st, cps5)
+        dz5 = bufB
+
+        st, cps = dgrad("conv5", "bn5", 128, 1024, dz5, ys["conv5"], "conv4", "bn4", bufA)
+        wgrad("conv5", "bn5", 128, 1024, dz5, ys["conv5"], "conv4", "bn4")
+        bn_bwd("bn4", "conv4", st, cps)
+        dz4 = bufA
+        st, cps = dgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3", bufB)
+        wgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3")
+        bn_bwd("bn3", "conv3", st, cps)
+        dz3 = bufB
+        st, cps = dgrad("conv3", "bn3", 64, 64, dz3, ys["conv3"], "conv2", "bn2", bufA, addend=dA2)
+        wgrad("conv3", "bn3", 64, 64, dz3, ys["conv3"], "conv2", "bn2")
+        bn_bwd("bn2", "conv2", st, cps)
+        dz2 = bufA
+        st, cps = dgrad("conv2", "bn2", 64, 64, dz2, ys["conv2"], "conv1", "bn1", bufB)
+        wgrad("conv2", "bn2", 64, 64, dz2, ys["conv2"], "conv1", "bn1")
+        bn_bwd("bn1", "conv1", st, cps)
+        dz1 = bufB
+        al, be, ga = coefs["bn1"]
+        keepalive.append(self._wgrad(B, N, 64, 4, L.PRO_BWD, L.PRO_RAW, G("conv1.weight"), ldw=4,
+                                     dZ=dz1, Y=ys["conv1"], alpha=al, beta=be, gamma=ga, X=sv.x))
+        return hb

@@ -1,0 +1,143 @@
+"""Drop-in ``PointNetSegmentation`` (reference: point_cloud_segmentation.py:65-133).
+
+Same constructor ``(num_classes, input_dim=4)``, same submodule names and registration
+order (10 Conv1d(k=1), 9 BatchNorm1d, Dropout(0.3)) and therefore the same 65-key
+``state_dict`` / ``best_model.pth`` layout; ``forward(x[B,N,4]) -> logits[B,N,C]``.
+``.train()`` / ``.eval()`` switch BatchNorm batch statistics (with running-stat updates)
+and dropout exactly as nn.BatchNorm1d / nn.Dropout do.
+
+The forward/backward run in the HIP kernels of libpcs.so via :class:`engine.Engine`
+(wrapped in a ``torch.autograd.Function`` so a standard
+``loss = CrossEntropyLoss(...)(out.view(-1,C), y); loss.backward(); opt.step()`` loop
+works unchanged).  There is no CPU path: calling the model on a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .engine import BNS, Engine
+
+
+class _PointNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, module, *params):
+        eng = module._engine()
+        P = module._param_dict()
+        bufs = module._buffer_dict()
+        train = module.training
+        masks = module._take_dropout_masks() if train else None
+        seed = module._next_seed() if train and masks is None else 0
+        sv = eng.forward(P, bufs, x, train=train, masks=masks, seed=seed)
+        if train:
+            for bn, _ in BNS:
+                getattr(module, bn).num_batches_tracked.add_(1)
+        ctx.sv = sv
+        ctx.module = module
+        return sv.logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        module, sv = ctx.module, ctx.sv
+        eng = module._engine()
+        P = module._param_dict()
+        gflat = torch.empty(eng.total_params, dtype=torch.float32, device=dlogits.device)
+        eng.backward(P, sv, gflat, dlogits=dlogits)
+        grads = []
+        for name, shape in eng.layout:
+            off = eng.offsets[name]
+            grads.append(gflat[off:off + eng.numel[name]].view(shape))
+        ctx.sv = None
+        return (None, None, *grads)
+
+
+class PointNetSegmentation(nn.Module):
+    """MI355X-native PointNetSegmentation (P:65-133).
+
+    ``compute_dtype``: ``"fp32"`` (default; exact-f32 MFMA, parity with the reference's
+    fp32 CPU path) or ``"bf16"`` (bf16 MFMA, fp32 accumulation and BN statistics).
+    """
+
+    def __init__(self, num_classes, input_dim=4, *, compute_dtype: str = "fp32"):
+        super().__init__()
+        # Point-wise MLPs for feature extraction (P:70-74)
+        self.conv1 = nn.Conv1d(input_dim, 64, 1)
+        self.conv2 = nn.Conv1d(64, 64, 1)
+        self.conv3 = nn.Conv1d(64, 64, 1)
+        self.conv4 = nn.Conv1d(64, 128, 1)
+        self.conv5 = nn.Conv1d(128, 1024, 1)
+        self.global_feat = nn.Conv1d(1024, 1024, 1)            # P:77
+        self.seg_conv1 = nn.Conv1d(1088, 512, 1)               # P:80-83
+        self.seg_conv2 = nn.Conv1d(512, 256, 1)
+        self.seg_conv3 = nn.Conv1d(256, 128, 1)
+        self.seg_conv4 = nn.Conv1d(128, num_classes, 1)
+        self.bn1 = nn.BatchNorm1d(64)                          # P:86-94
+        self.bn2 = nn.BatchNorm1d(64)
+        self.bn3 = nn.BatchNorm1d(64)
+        self.bn4 = nn.BatchNorm1d(128)
+        self.bn5 = nn.BatchNorm1d(1024)
+        self.bn_global = nn.BatchNorm1d(1024)
+        self.bn_seg1 = nn.BatchNorm1d(512)
+        self.bn_seg2 = nn.BatchNorm1d(256)
+        self.bn_seg3 = nn.BatchNorm1d(128)
+        self.dropout = nn.Dropout(0.3)                         # P:96
+        self.num_classes = num_classes
+        self.input_dim = input_dim
+        self.compute_dtype = compute_dtype
+        self._eng = None
+        self._masks = None
+        self._seed_gen = torch.Generator().manual_seed(0x5eed)
+
+    # ---------------------------------------------------------------- internals
+    def _engine(self) -> Engine:
+        if self._eng is None or self._eng.dtype != self.compute_dtype:
+            self._eng = Engine(self.num_classes, self.compute_dtype, self.input_dim)
+        return self._eng
+
+    def _param_dict(self):
+        return {n: p for n, p in self.named_parameters()}
+
+    def _buffer_dict(self):
+        return {n: b for n, b in self.named_buffers()}
+
+    def _next_seed(self):
+        return int(torch.randint(0, 2 ** 62, (1,), generator=self._seed_gen).item())
+
+    def set_dropout_masks(self, bits1, bits2):
+        """Replay dropout keep masks in the next train forward (tests / reference parity).
+
+        bits1: uint8 [B*N, 64] (512 channels after bn_seg1, P:124), bits2: uint8 [B*N, 32]
+        (256 channels after bn_seg2, P:126); bit i of byte j = channel 8j+i.
+        """
+        self._masks = (bits1.contiguous(), bits2.contiguous())
+
+    def _take_dropout_masks(self):
+        m, self._masks = self._masks, None
+        return m
+
+    def seed_dropout(self, seed: int):
+        self._seed_gen.manual_seed(seed)
+
+    # ---------------------------------------------------------------- API
+    def forward(self, x):
+        """x: (batch_size, max_points, 4) -> logits (batch_size, max_points, num_classes)."""
+        if x.dim() != 3 or x.shape[-1] != self.input_dim:
+            raise ValueError(f"expected x of shape (B, N, {self.input_dim}), got {tuple(x.shape)}")
+        if not x.is_cuda:
+            raise RuntimeError("pcs_amd.PointNetSegmentation runs on a HIP device only; "
+                               "move the model and inputs with .to('cuda')")
+        return _PointNetFunction.apply(x, self, *self.parameters())
+
+
+def load_reference_checkpoint(path, map_location="cpu"):
+    """Load a reference ``best_model.pth`` (P:373-382) safely (weights_only=True).
+
+    Returns (state_dict without any 'module.' prefix, checkpoint dict).  The prefix
+    handling mirrors P:409-428.
+    """
+    ckpt = torch.load(path, map_location=map_location, weights_only=True)
+    sd = ckpt["model_state_dict"] if "model_state_dict" in ckpt else ckpt
+    if any(k.startswith("module.") for k in sd):
+        sd = {k.replace("module.", "", 1): v for k, v in sd.items()}
+    return sd, ckpt

@@ -1,0 +1,65 @@
+"""CPU-side checks of the C ABI: the library loads and exports every declared symbol."""
+import ctypes as ct
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "pcs.h")
+LIB = os.path.join(REPO, "point-cloud-cnn-segmentation_amd", "csrc", "libpcs.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pcs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    for n in ["pcs_gemm", "pcs_wgrad", "pcs_head", "pcs_adam", "pcs_bn_fwd_finalize",
+              "pcs_bn_bwd_finalize", "pcs_pool_finalize", "pcs_pool_bwd", "pcs_dropout_bits"]:
+        assert n in names
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built (run __graft_entry__.build())")
+def test_library_exports_every_declared_symbol():
+    import torch  # noqa: F401  (same HIP runtime as the product path)
+    lib = ct.CDLL(LIB)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    lib.pcs_abi_version.restype = ct.c_int
+    assert lib.pcs_abi_version() == 1
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
+def test_binding_signatures_cover_header():
+    import pcs_amd._lib as L
+    bound = {n for n, _, _ in L.SIGNATURES}
+    assert set(declared_functions()) == bound
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
+def test_argument_validation_without_gpu():
+    """Invalid arguments are rejected on the host, before any launch (no GPU needed)."""
+    import pcs_amd._lib as L
+    lib = L.load()
+    a = L.GemmArgs(num_scenes=1, scene_rows=128, K=60, Ncols=64, dtype=L.BF16)
+    assert lib.pcs_gemm(ct.byref(a), None) == -1000
+    assert b"multiple" in lib.pcs_last_error()
+    h = L.HeadArgs(num_scenes=1, scene_rows=64, Cin=128, num_classes=40)
+    assert lib.pcs_head(ct.byref(h), None) == -1000
+    assert lib.pcs_dropout_bits(1, 0, 16, 12, 0.3, None, None) == -1000
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
+def test_geometry_is_scene_aligned():
+    import pcs_amd._lib as L
+    lib = L.load()
+    for N, B in [(4096, 4), (3000, 3), (2097152, 4), (1, 1), (129, 2)]:
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=1024, dtype=L.BF16)
+        rpc = lib.pcs_gemm_geometry(ct.byref(a))
+        assert rpc % 128 == 0 and rpc > 0
+        cps = a.chunks_per_scene
+        assert (cps - 1) * rpc < N <= cps * rpc      # no empty chunk, full coverage
