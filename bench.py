@@ -1,0 +1,216 @@
+"""Benchmark: PointNetSegmentation training step (forward + weighted CE + backward + Adam)
+on MI355X, points/s on a dense 128^3 grid, batch 4 scenes per GPU (BASELINE.json configs[1];
+SURVEY.md §8(d) cfg2).  One process per GPU; for N>1 launch with torch.distributed.run.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32] [--grid 128]
+
+Prints ONE JSON line (rank 0).  value = points processed by all ranks / max-over-ranks
+wall time of K steps (bracketed by barrier + synchronize).  ``roofline`` describes the
+dominant kernel from HIP events recorded on its launch stream inside the timed region;
+``cpu_baseline`` times the numpy oracle (the reference restated) on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import pcs_amd  # noqa: E402
+from pcs_amd.data import class_weights, synthetic_batch  # noqa: E402
+from pcs_amd.model import PointNetSegmentation  # noqa: E402
+from pcs_amd.optim import FusedAdam  # noqa: E402
+from pcs_amd.train import FusedTrainStep  # noqa: E402
+
+PEAK = {"bf16": {"mfma": 2516.6, "hbm": 8000.0}, "fp32": {"mfma": 157.3, "hbm": 8000.0}}
+LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (64, 128),
+              "conv5": (128, 1024), "global_feat": (1024, 1024), "seg_conv1": (64, 512),
+              "seg_conv2": (512, 256), "seg_conv3": (256, 128)}
+
+
+def kernel_model(tag, M, ab):
+    """Algorithmic FLOPs and HBM bytes of one launch (SURVEY.md §8(d) accounting)."""
+    kind, conv = tag.split(":", 1)
+    if conv not in LAYER_DIMS:
+        return None
+    cin, cout = LAYER_DIMS[conv]
+    flops = 2.0 * M * cin * cout
+    if kind == "fwd":
+        nbytes = M * (cin + cout) * ab
+    elif kind == "dgrad":
+        extra = 0 if conv == "global_feat" else cout      # pool path reads no dZ
+        nbytes = M * (cout + extra + 2 * cin) * ab
+        if conv == "seg_conv1":
+            nbytes = M * (2 * cout + cin) * ab
+    else:  # wgrad
+        extra = 0 if conv == "global_feat" else cout
+        nbytes = M * (cout + extra + cin) * ab
+    return flops, nbytes
+
+
+def cpu_baseline(max_seconds=12.0):
+    """Numpy oracle (fp32) fwd+bwd on the reference's CPU-runnable case (B=4, N=4096, C=2)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pointnet_oracle as orc
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()
+                     if i.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    B, N = 4, 4096
+    sd = orc.init_params(2, 7)
+    pts, lab, _ = synthetic_batch(1234, [N] * B, 2, grid=32)
+    masks = orc.dropout_masks(3, B * N)
+    w = np.array([0.5, 1.5], np.float32)
+    orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32)   # warm-up
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= max_seconds or steps >= 20:
+            break
+    return {"value": B * N * steps / el / 1e6, "unit": "M points/s", "cores": int(cores),
+            "kind": "port",
+            "sample": f"numpy fp32 oracle fwd+CE+bwd, B=4 x N=4096 (32^3 lattice), C=2, "
+                      f"{steps} steps in {el:.1f}s after 1 warm-up"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--grid", type=int, default=128)
+    ap.add_argument("--scenes", type=int, default=4)
+    ap.add_argument("--classes", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, G, C = args.scenes, args.grid, args.classes
+    N = G ** 3
+    pts, lab, _ = synthetic_batch(1234 + rank, [N] * B, C, grid=G, dense=True)
+    w = class_weights([lab[b] for b in range(B)], num_classes=C)
+    x = torch.from_numpy(pts).to(dev)
+    y = torch.from_numpy(lab).to(dev)
+    del pts, lab
+
+    torch.manual_seed(0)
+    model = PointNetSegmentation(C, compute_dtype=args.dtype).to(dev)
+    if world > 1:   # identical initial weights on every rank (DataParallel replicates them)
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    opt = FusedAdam(model, lr=1e-3, weight_decay=1e-4)
+    step = FusedTrainStep(model, opt, class_weight=w)
+
+    for i in range(args.warmup):
+        loss = step(x, y)
+    torch.cuda.synchronize()
+    timing = {} if not args.no_kernel_timing else None
+    step.timing = timing
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    step.timing = None
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss_v = float(loss.item())
+
+    M = B * N
+    total_points = world * M * args.steps
+    ab = 2 if args.dtype == "bf16" else 4
+    roof = None
+    kernels = {}
+    if timing:
+        for tag, evs in timing.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            kernels[tag] = (sum(ms), len(ms))
+        dom = max(kernels, key=lambda k: kernels[k][0])
+        tot, cnt = kernels[dom]
+        avg_s = tot / cnt / 1e3
+        mdl = kernel_model(dom, M, ab)
+        if mdl:
+            flops, nbytes = mdl
+            ai = flops / nbytes
+            ridge = PEAK[args.dtype]["mfma"] * 1e12 / (PEAK[args.dtype]["hbm"] * 1e9)
+            if ai >= ridge:
+                ach = flops / avg_s / 1e12
+                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
+                        "peak": PEAK[args.dtype]["mfma"], "unit": "TFLOP/s",
+                        "frac": round(ach / PEAK[args.dtype]["mfma"], 4), "traffic": None,
+                        "algorithmic_flops": flops, "avg_ms": round(avg_s * 1e3, 4)}
+            else:
+                ach = nbytes / avg_s / 1e9
+                roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
+                        "peak": PEAK[args.dtype]["hbm"], "unit": "GB/s",
+                        "frac": round(ach / PEAK[args.dtype]["hbm"], 4), "traffic": None,
+                        "algorithmic_bytes": nbytes, "avg_ms": round(avg_s * 1e3, 4)}
+        if rank == 0:
+            step_ms = el / args.steps * 1e3
+            print(f"# per-kernel (avg ms, share of {step_ms:.2f} ms step):", file=sys.stderr)
+            for tag, (tot, cnt) in sorted(kernels.items(), key=lambda kv: -kv[1][0]):
+                mdl = kernel_model(tag, M, ab)
+                extra = ""
+                if mdl:
+                    a = tot / cnt / 1e3
+                    extra = f"  {mdl[0] / a / 1e12:8.1f} TF/s  {mdl[1] / a / 1e9:8.1f} GB/s"
+                print(f"#  {tag:22s} {tot / cnt:9.3f} ms  {100 * tot / cnt / step_ms:5.1f}%{extra}",
+                      file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        rec = {
+            "metric": "M voxels/sec fwd+bwd, 128^3 grid batch=4 (points/s of the PointNet "
+                      "training step: forward + weighted CE + backward + Adam)",
+            "value": round(total_points / el / 1e6, 3),
+            "unit": "M points/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (dense voxel-centre clouds, seeded)",
+            "config": {"workload": f"PointNetSegmentation train step, {B} scenes x {G}^3 points "
+                                   f"per GPU, C={C}", "global_batch": B * world,
+                       "points_per_scene": N, "parallelism": f"dp{world}"},
+            "loss": round(loss_v, 6),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

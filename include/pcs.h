@@ -131,18 +131,21 @@ int pcs_conv1_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream); /* X = poi
  * per-chunk (mean, M2) partials (Chan, fp64) into the batch mean / biased variance over
  * all B*N rows (pads included), derive the fused affine y*scale+shift, and update the
  * running buffers (momentum, unbiased variance) when update_running != 0.
- * scene_sum[B, C] receives the per-scene sum of y (may be NULL).
+ * The stored pre-BN activations may omit a per-channel constant (the conv bias, which BN
+ * cancels): mean_offset[C] (NULL = 0) is added back for running_mean only.
+ * scene_sum[B, C] receives the per-scene sum of the stored y (may be NULL).
  */
 int pcs_bn_fwd_finalize(const float *stats, int64_t num_scenes, int64_t scene_rows,
                         int32_t C, int32_t chunks_per_scene, int64_t rows_per_chunk,
-                        const float *gamma, const float *beta, float *running_mean,
-                        float *running_var, float momentum, float eps, int32_t update_running,
-                        float *mean, float *rstd, float *scale, float *shift,
-                        float *scene_sum, pcs_stream_t stream);
-/* eval-mode BatchNorm: scale/shift from the running buffers (P:432 eval path) */
+                        const float *gamma, const float *beta, const float *mean_offset,
+                        float *running_mean, float *running_var, float momentum, float eps,
+                        int32_t update_running, float *mean, float *rstd, float *scale,
+                        float *shift, float *scene_sum, pcs_stream_t stream);
+/* eval-mode BatchNorm: scale/shift from the running buffers (P:432 eval path), for stored
+ * activations that omit mean_offset (NULL = 0) */
 int pcs_bn_eval_coefs(const float *gamma, const float *beta, const float *running_mean,
-                      const float *running_var, float eps, int32_t C, float *scale,
-                      float *shift, pcs_stream_t stream);
+                      const float *running_var, const float *mean_offset, float eps, int32_t C,
+                      float *scale, float *shift, pcs_stream_t stream);
 /*
  * BatchNorm1d backward from per-chunk (S1 = sum dz, S2 = sum dz*xhat) partials:
  * dy = alpha*dz + beta_c + gamma_c*y, dgamma = S2, dbeta = S1, and the conv-bias
@@ -162,9 +165,11 @@ int pcs_pool_finalize(const float *pool, int64_t num_scenes, int64_t scene_rows,
                       int32_t chunks_per_scene, const float *s, const float *t, float *g,
                       int32_t *am, float *ysel, pcs_stream_t stream);
 
-/* out[b, n] = bias[n] + sum_k W[n, col_off + k] * g[b, k]   (seg_conv1 global half, P:117-123) */
+/* v[b, n] = bias[n] + sum_k W[n, col_off + k] * g[b, k]   (seg_conv1 global half, P:117-123).
+ * offset == NULL: out = v.  Otherwise out[b,n] = v[b,n] - mean_b v[b,n] (centred: the stored
+ * seg_conv1 activations keep full precision) and offset[n] = mean_b v[b,n]. */
 int pcs_scene_gemv(const float *g, int64_t num_scenes, int32_t Kg, const float *W, int64_t ldw,
-                   int32_t col_off, const float *bias, int32_t Nout, float *out,
+                   int32_t col_off, const float *bias, int32_t Nout, float *out, float *offset,
                    pcs_stream_t stream);
 
 /*

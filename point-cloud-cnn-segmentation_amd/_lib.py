@@ -90,12 +90,12 @@ SIGNATURES = [
     ("pcs_wgrad", ct.c_int, [ct.POINTER(WgradArgs), _vp]),
     ("pcs_conv1_wgrad", ct.c_int, [ct.POINTER(WgradArgs), _vp]),
     ("pcs_bn_fwd_finalize", ct.c_int, [_vp, _i64, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp,
-                                       _f, _f, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
-    ("pcs_bn_eval_coefs", ct.c_int, [_vp, _vp, _vp, _vp, _f, _i32, _vp, _vp, _vp]),
+                                       _vp, _f, _f, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("pcs_bn_eval_coefs", ct.c_int, [_vp, _vp, _vp, _vp, _vp, _f, _i32, _vp, _vp, _vp]),
     ("pcs_bn_bwd_finalize", ct.c_int, [_vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("pcs_pool_finalize", ct.c_int, [_vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
-    ("pcs_scene_gemv", ct.c_int, [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    ("pcs_scene_gemv", ct.c_int, [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
     ("pcs_pool_bwd", ct.c_int, [ct.POINTER(PoolBwdArgs), _vp]),
     ("pcs_head_geometry", _i64, [ct.POINTER(HeadArgs)]),
     ("pcs_head", ct.c_int, [ct.POINTER(HeadArgs), _vp]),

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(THREADS) void conv1_wgrad_kernel(pcs_wgrad_args a, 
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(THREADS) void bn_fwd_finalize_kernel(
     const float *stats, int64_t B, int64_t N, int C, int cps, int64_t rpc, const float *gamma,
-    const float *beta, float *rmean, float *rvar, float momentum, float eps, int update,
+    const float *beta, const float *moff, float *rmean, float *rvar, float momentum, float eps, int update,
     float *mean_o, float *rstd_o, float *scale_o, float *shift_o, float *scene_sum) {
   __shared__ double sh[THREADS][3];
   const int c = blockIdx.x, tid = threadIdx.x;
@@ -187,19 +187,21 @@ __global__ __launch_bounds__(THREADS) void bn_fwd_finalize_kernel(
     shift_o[c] = (float)((double)beta[c] - gmean * sc);
     if (update) {
       const double unb = gn > 1 ? gm2 / (gn - 1) : gm2;
-      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * gmean);
+      const double tm = gmean + (moff ? (double)moff[c] : 0.0);
+      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * tm);
       rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
     }
   }
 }
 
 __global__ void bn_eval_kernel(const float *gamma, const float *beta, const float *rm,
-                               const float *rv, float eps, int C, float *scale, float *shift) {
+                               const float *rv, const float *moff, float eps, int C, float *scale,
+                               float *shift) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double sc = (double)gamma[c] / sqrt((double)rv[c] + (double)eps);
   scale[c] = (float)sc;
-  shift[c] = (float)((double)beta[c] - (double)rm[c] * sc);
+  shift[c] = (float)((double)beta[c] - ((double)rm[c] - (moff ? (double)moff[c] : 0.0)) * sc);
 }
 
 __global__ __launch_bounds__(THREADS) void bn_bwd_finalize_kernel(
@@ -270,18 +272,29 @@ __global__ void pool_finalize_kernel(const float *pool, int64_t B, int64_t N, in
 }
 
 __global__ void scene_gemv_kernel(const float *g, int64_t B, int Kg, const float *W, int64_t ldw,
-                                  int col_off, const float *bias, int Nout, float *out) {
-  // one wave per (b, n)
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+                                  int col_off, const float *bias, int Nout, float *out,
+                                  float *offset) {
+  // one wave per output channel n, looping over the scenes
+  const int n = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
-  if (wave >= B * Nout) return;
-  const int b = (int)(wave / Nout), n = (int)(wave % Nout);
+  if (n >= Nout) return;
   const float *w = W + (int64_t)n * ldw + col_off;
-  const float *x = g + (int64_t)b * Kg;
-  float acc = 0.f;
-  for (int k = lane; k < Kg; k += 64) acc = fmaf(w[k], x[k], acc);
-  acc = wave_sum(acc);
-  if (lane == 0) out[wave] = acc + (bias ? bias[n] : 0.f);
+  const float bn = bias ? bias[n] : 0.f;
+  double mean = 0.0;
+  for (int64_t b = 0; b < B; ++b) {
+    const float *x = g + b * Kg;
+    float acc = 0.f;
+    for (int k = lane; k < Kg; k += 64) acc = fmaf(w[k], x[k], acc);
+    acc = wave_sum(acc) + bn;
+    mean += acc;
+    if (lane == 0) out[b * Nout + n] = acc;
+  }
+  if (!offset) return;
+  const float m = (float)(mean / (double)B);
+  if (lane == 0) {
+    for (int64_t b = 0; b < B; ++b) out[b * Nout + n] -= m;
+    offset[n] = m;
+  }
 }
 
 // csum[b,n] = sum over the rows of scene b of dy_seg1[:, n]
@@ -671,7 +684,8 @@ extern "C" int pcs_conv1_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
 
 extern "C" int pcs_bn_fwd_finalize(const float *stats, int64_t B, int64_t N, int32_t C, int32_t cps,
                                    int64_t rpc, const float *gamma, const float *beta,
-                                   float *running_mean, float *running_var, float momentum,
+                                   const float *mean_offset, float *running_mean,
+                                   float *running_var, float momentum,
                                    float eps, int32_t update_running, float *mean, float *rstd,
                                    float *scale, float *shift, float *scene_sum,
                                    pcs_stream_t stream) {
@@ -680,18 +694,18 @@ extern "C" int pcs_bn_fwd_finalize(const float *stats, int64_t B, int64_t N, int
   if (update_running && (!running_mean || !running_var))
     return pcs_set_einval("pcs_bn_fwd_finalize", "running buffers required");
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(C), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
-                     stats, B, N, (int)C, (int)cps, rpc, gamma, beta, running_mean, running_var,
+                     stats, B, N, (int)C, (int)cps, rpc, gamma, beta, mean_offset, running_mean, running_var,
                      momentum, eps, (int)update_running, mean, rstd, scale, shift, scene_sum);
   PCS_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int pcs_bn_eval_coefs(const float *gamma, const float *beta, const float *rm,
-                                 const float *rv, float eps, int32_t C, float *scale, float *shift,
-                                 pcs_stream_t stream) {
+                                 const float *rv, const float *mean_offset, float eps, int32_t C,
+                                 float *scale, float *shift, pcs_stream_t stream) {
   if (!gamma || !beta || !rm || !rv || !scale || !shift) return pcs_set_einval("pcs_bn_eval_coefs", "null");
   hipLaunchKernelGGL(bn_eval_kernel, dim3(blocks_for(C, 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), gamma, beta, rm, rv, eps, (int)C, scale, shift);
+                     reinterpret_cast<hipStream_t>(stream), gamma, beta, rm, rv, mean_offset, eps, (int)C, scale, shift);
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -721,12 +735,12 @@ extern "C" int pcs_pool_finalize(const float *pool, int64_t B, int64_t N, int32_
 }
 
 extern "C" int pcs_scene_gemv(const float *g, int64_t B, int32_t Kg, const float *W, int64_t ldw,
-                              int32_t col_off, const float *bias, int32_t Nout, float *out,
+                              int32_t col_off, const float *bias, int32_t Nout, float *out, float *offset,
                               pcs_stream_t stream) {
   if (!g || !W || !out) return pcs_set_einval("pcs_scene_gemv", "null argument");
-  hipLaunchKernelGGL(scene_gemv_kernel, dim3(blocks_for(B * Nout * 64, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(scene_gemv_kernel, dim3(blocks_for((int64_t)Nout * 64, 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), g, B, (int)Kg, W, ldw, (int)col_off, bias,
-                     (int)Nout, out);
+                     (int)Nout, out, offset);
   PCS_CHECK_LAUNCH();
   return 0;
 }

@@ -108,7 +108,20 @@ class Engine:
             off += self.numel[n]
         self.total_params = off
         self._geo = {}
+        self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
         L.load()
+
+    def _launch(self, tag, name, *args):
+        """C-ABI call, bracketed by HIP events on the launch stream when timing is on."""
+        if self.timing is None or tag is None:
+            return L.call(name, *args)
+        st = torch.cuda.Event(enable_timing=True)
+        en = torch.cuda.Event(enable_timing=True)
+        st.record()
+        r = L.call(name, *args)
+        en.record()
+        self.timing.setdefault(tag, []).append((st, en))
+        return r
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -145,7 +158,8 @@ class Engine:
             wc[conv] = (Wc, WcT)
         return wc
 
-    def _bn_finalize(self, bnname, stats, B, N, C, cps, rpc, P, bufs, train, dev):
+    def _bn_finalize(self, bnname, stats, B, N, C, cps, rpc, P, bufs, train, dev, offset=None):
+        """BN coefficients for stored activations that omit ``offset`` (the conv bias)."""
         coef = BNCoef(*(torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4)),
                       torch.empty(B, C, dtype=torch.float32, device=dev))
         g, b = P[f"{bnname}.weight"], P[f"{bnname}.bias"]
@@ -153,16 +167,17 @@ class Engine:
             rm, rv = bufs.get(f"{bnname}.running_mean"), bufs.get(f"{bnname}.running_var")
             upd = int(rm is not None and rv is not None)
             L.call("pcs_bn_fwd_finalize", L.ptr(stats), B, N, C, cps, rpc, L.ptr(g), L.ptr(b),
-                   L.ptr(rm), L.ptr(rv), BN_MOMENTUM, BN_EPS, upd, L.ptr(coef.mean),
+                   L.ptr(offset), L.ptr(rm), L.ptr(rv), BN_MOMENTUM, BN_EPS, upd, L.ptr(coef.mean),
                    L.ptr(coef.rstd), L.ptr(coef.scale), L.ptr(coef.shift), L.ptr(coef.scene_sum),
                    self._stream())
         else:
             L.call("pcs_bn_eval_coefs", L.ptr(g), L.ptr(b), L.ptr(bufs[f"{bnname}.running_mean"]),
-                   L.ptr(bufs[f"{bnname}.running_var"]), BN_EPS, C, L.ptr(coef.scale),
+                   L.ptr(bufs[f"{bnname}.running_var"]), L.ptr(offset), BN_EPS, C, L.ptr(coef.scale),
                    L.ptr(coef.shift), self._stream())
         return coef
 
     def _gemm(self, B, N, K, ncols, pro, epi, A, W, C, **kw):
+        tag = kw.pop("tag", None)
         cps, _ = self.geometry(B, N, ncols)
         a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
                        prologue=pro, epilogue=epi, chunks_per_scene=cps,
@@ -171,9 +186,10 @@ class Engine:
                        c_keep_scale=kw.pop("c_keep_scale", 1.0))
         for k, v in kw.items():
             setattr(a, k, L.ptr(v))
-        L.call("pcs_gemm", ct.byref(a), self._stream())
+        self._launch(tag, "pcs_gemm", ct.byref(a), self._stream())
 
     def _wgrad(self, B, N, cout, cin, dy_mode, x_mode, dW, ldw=0, **kw):
+        tag = kw.pop("tag", None)
         a = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=cout, Cin=cin, dtype=self.dt,
                         splits_per_scene=0, dy_mode=dy_mode, x_mode=x_mode,
                         x_keep_scale=kw.pop("x_keep_scale", 1.0), dW=L.ptr(dW), ldw=ldw)
@@ -187,7 +203,7 @@ class Engine:
             nbytes = L.load().pcs_wgrad_workspace(ct.byref(a))
         ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dW.device)
         a.partial = ws.data_ptr()
-        L.call(fn, ct.byref(a), self._stream())
+        self._launch(tag, fn, ct.byref(a), self._stream())
         return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
     # ------------------------------------------------------------------ forward
@@ -220,41 +236,38 @@ class Engine:
             c = sv.bn[prev]
             return dict(pa=c.scale, pb=c.shift)
 
-        # eval: all BN coefficients come from the running buffers
-        if not train:
-            for bn, C in BNS:
-                sv.bn[bn] = self._bn_finalize(bn, None, B, N, C, 1, 1, P, bufs, False, dev)
-
+        # Stored pre-BN activations omit the conv bias (BN cancels it exactly; it only
+        # shifts running_mean), which keeps them centred: full precision in fp32/bf16.
         # conv1 (K=4)
         y1 = self._empty(M, 64, device=dev)
         st, cps, rpc = stats_buf(64) if train else (None, *self.geometry(B, N, 64))
         a = L.GemmArgs(num_scenes=B, scene_rows=N, K=4, Ncols=64, dtype=self.dt,
                        chunks_per_scene=cps, A=L.ptr(x), W=L.ptr(P["conv1.weight"]),
-                       C=L.ptr(y1), bias=L.ptr(P["conv1.bias"]), stats=L.ptr(st))
-        L.call("pcs_conv1_fwd", ct.byref(a), s)
+                       C=L.ptr(y1), bias=None, stats=L.ptr(st))
+        self._launch("fwd:conv1", "pcs_conv1_fwd", ct.byref(a), s)
         sv.ys["conv1"] = y1
-        if train:
-            sv.bn["bn1"] = self._bn_finalize("bn1", st, B, N, 64, cps, rpc, P, bufs, True, dev)
+        sv.bn["bn1"] = self._bn_finalize("bn1", st, B, N, 64, cps, rpc, P, bufs, train, dev,
+                                         offset=P["conv1.bias"])
 
-        def layer(conv, src_conv, src_bn, K, ncols, bnname, **kw):
+        def layer(conv, src_conv, src_bn, K, ncols, bnname, offset, **kw):
             y = self._empty(M, ncols, device=dev)
             st, cps, rpc = stats_buf(ncols) if train else (None, 0, 0)
             self._gemm(B, N, K, ncols, L.PRO_BNRELU, L.EPI_FWD, sv.ys[src_conv], wc[conv][0], y,
-                       stats=st, **bnrelu(src_bn), **kw)
+                       stats=st, tag=f"fwd:{conv}", **bnrelu(src_bn), **kw)
             sv.ys[conv] = y
-            if train:
-                sv.bn[bnname] = self._bn_finalize(bnname, st, B, N, ncols, cps, rpc, P, bufs, True, dev)
+            sv.bn[bnname] = self._bn_finalize(bnname, st, B, N, ncols, cps, rpc, P, bufs, train,
+                                              dev, offset=offset)
             return y
 
-        layer("conv2", "conv1", "bn1", 64, 64, "bn2", bias=P["conv2.bias"])
-        layer("conv3", "conv2", "bn2", 64, 64, "bn3", bias=P["conv3.bias"])
-        layer("conv4", "conv3", "bn3", 64, 128, "bn4", bias=P["conv4.bias"])
-        layer("conv5", "conv4", "bn4", 128, 1024, "bn5", bias=P["conv5.bias"])
+        layer("conv2", "conv1", "bn1", 64, 64, "bn2", P["conv2.bias"])
+        layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"])
+        layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"])
+        layer("conv5", "conv4", "bn4", 128, 1024, "bn5", P["conv5.bias"])
 
         # global_feat + max-pool partials
         cps_g, _ = self.geometry(B, N, 1024)
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
-        layer("global_feat", "conv5", "bn5", 1024, 1024, "bn_global", bias=P["global_feat.bias"],
+        layer("global_feat", "conv5", "bn5", 1024, 1024, "bn_global", P["global_feat.bias"],
               pool=pool)
         cg = sv.bn["bn_global"]
         sv.g = torch.empty(B, 1024, dtype=torch.float32, device=dev)
@@ -264,11 +277,13 @@ class Engine:
                L.ptr(sv.g), L.ptr(sv.am), L.ptr(sv.ysel), s)
 
         # seg_conv1 = local 64->512 GEMM + per-scene bias (W_global . g_b + b)   P:117-123
+        # the per-scene bias is centred over the scenes; its mean joins the BN offset
         sbias = torch.empty(B, 512, dtype=torch.float32, device=dev)
+        soff = torch.empty(512, dtype=torch.float32, device=dev)
         Ws1 = P["seg_conv1.weight"]
         L.call("pcs_scene_gemv", L.ptr(sv.g), B, 1024, L.ptr(Ws1), Ws1.shape[1], 64,
-               L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), s)
-        layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", scene_bias=sbias)
+               L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), L.ptr(soff), s)
+        layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", soff, scene_bias=sbias)
 
         # dropout keep bits (P:124, P:126)
         if train:
@@ -285,9 +300,9 @@ class Engine:
             m1 = m2 = None
             sv.masks = (None, None)
             keep = 1.0
-        layer("seg_conv2", "seg_conv1", "bn_seg1", 512, 256, "bn_seg2", bias=P["seg_conv2.bias"],
+        layer("seg_conv2", "seg_conv1", "bn_seg1", 512, 256, "bn_seg2", P["seg_conv2.bias"],
               a_mask=m1, a_keep_scale=keep)
-        layer("seg_conv3", "seg_conv2", "bn_seg2", 256, 128, "bn_seg3", bias=P["seg_conv3.bias"],
+        layer("seg_conv3", "seg_conv2", "bn_seg2", 256, 128, "bn_seg3", P["seg_conv3.bias"],
               a_mask=m2, a_keep_scale=keep)
 
         # head: seg_conv4 (+ CE and the start of the backward when fused)
@@ -331,7 +346,7 @@ class Engine:
             ha.dlogits = L.ptr(dl)
             ha.dl_stride_row, ha.dl_stride_col = dl.stride(0), dl.stride(1)
             hb["dl"] = dl
-        L.call("pcs_head", ct.byref(ha), self._stream())
+        self._launch(f"head:{mode}", "pcs_head", ct.byref(ha), self._stream())
         return hb
 
     # ------------------------------------------------------------------ backward
@@ -382,14 +397,15 @@ class Engine:
             self._gemm(B, N, cout, cin, L.PRO_BWD, L.EPI_DGRAD, dz, wc[conv][1], out,
                        A2=ycur, pa=al, pb=be, pc=ga, Yp=sv.ys[prev_conv], es=pc.scale, et=pc.shift,
                        emean=pc.mean, erstd=pc.rstd, c_mask=c_mask,
-                       c_keep_scale=keep if c_mask is not None else 1.0, addend=addend, stats=st)
+                       c_keep_scale=keep if c_mask is not None else 1.0, addend=addend, stats=st,
+                       tag=f"dgrad:{conv}")
             return st, cps
 
         def wgrad(conv, bn, cin, cout, dz, ycur, prev_conv, prev_bn, x_mask=None, ldw=0):
             al, be, ga = coefs[bn]
             pc = sv.bn[prev_bn]
             keepalive.append(self._wgrad(
-                B, N, cout, cin, L.PRO_BWD, L.PRO_BNRELU, G(f"{conv}.weight"), ldw=ldw, dZ=dz,
+                B, N, cout, cin, L.PRO_BWD, L.PRO_BNRELU, G(f"{conv}.weight"), ldw=ldw, tag=f"wgrad:{conv}", dZ=dz,
                 Y=ycur, alpha=al, beta=be, gamma=ga, X=sv.ys[prev_conv], s=pc.scale, t=pc.shift,
                 x_mask=x_mask, x_keep_scale=keep if x_mask is not None else 1.0))
 
@@ -430,7 +446,7 @@ class Engine:
         # seg_conv1 local half: dA2 contribution (raw) and dW[:, :64]
         dA2 = torch.empty(M, 64, dtype=self.tdt, device=dev)
         self._gemm(B, N, 512, 64, L.PRO_BWD, L.EPI_RAW, dz_s1, wc["seg_conv1"][1], dA2,
-                   A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1)
+                   A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
         wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
 
         # global_feat (dy from the sparse max-pool gradient)
@@ -440,10 +456,10 @@ class Engine:
         self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD, ys["global_feat"],
                    wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
                    Yp=ys["conv5"], es=pc5.scale, et=pc5.shift, emean=pc5.mean, erstd=pc5.rstd,
-                   stats=st)
+                   stats=st, tag="dgrad:global_feat")
         keepalive.append(self._wgrad(
             B, N, 1024, 1024, L.PRO_BWD_POOL, L.PRO_BNRELU, G("global_feat.weight"),
-            Y=ys["global_feat"], beta=bg, gamma=gg, pool_idx=sv.am, pool_coef=sp,
+            tag="wgrad:global_feat", Y=ys["global_feat"], beta=bg, gamma=gg, pool_idx=sv.am, pool_coef=sp,
             X=ys["conv5"], s=pc5.scale, t=pc5.shift))
         bn_bwd("bn5", "conv5", st, cps5)
         dz5 = bufB
@@ -466,5 +482,6 @@ class Engine:
         dz1 = bufB
         al, be, ga = coefs["bn1"]
         keepalive.append(self._wgrad(B, N, 64, 4, L.PRO_BWD, L.PRO_RAW, G("conv1.weight"), ldw=4,
+                                     tag="wgrad:conv1",
                                      dZ=dz1, Y=ys["conv1"], alpha=al, beta=be, gamma=ga, X=sv.x))
         return hb

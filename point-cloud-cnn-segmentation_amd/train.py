@@ -1,0 +1,76 @@
+"""Fused training step: the reference inner loop P:241-255 as one stream of HIP kernels.
+
+    optimizer.zero_grad(); out = model(points); loss = criterion(out.view(-1,C), labels)
+    loss.backward(); optimizer.step()
+
+becomes ``loss = step(points, labels)``: forward, weighted CE (P:216, P:251) fused into the
+head kernel, backward into one flat gradient buffer, optional RCCL all-reduce of that
+buffer, and the fused Adam update.  Nothing synchronises with the host; ``loss`` is a
+device scalar (read it once per epoch, not per step as P:258-269 does).
+
+Data parallelism (replaces nn.DataParallel, P:208-211) is one process per GPU: each rank
+runs its own scenes, the CE denominator sum_w is all-reduced before the head so every
+rank's gradient is already normalised by the GLOBAL weight sum (exactly DataParallel's
+single gathered loss), BatchNorm statistics stay per rank (DataParallel has no SyncBN),
+and the gradient buffer is summed with one all-reduce.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from .engine import BNS
+from .optim import FusedAdam, flat_buffers
+
+
+class FusedTrainStep:
+    def __init__(self, model, optimizer: FusedAdam | None = None, class_weight=None,
+                 process_group=None, lr=1e-3, weight_decay=1e-4):
+        self.model = model
+        self.opt = optimizer or FusedAdam(model, lr=lr, weight_decay=weight_decay)
+        dev = next(model.parameters()).device
+        C = model.num_classes
+        w = torch.ones(C) if class_weight is None else torch.as_tensor(class_weight, dtype=torch.float32)
+        self.class_weight = w.to(dev, torch.float32).contiguous()
+        self.pg = process_group
+        self.wsum = torch.empty(3, dtype=torch.float32, device=dev)
+        self.counts = torch.empty(16, dtype=torch.int64, device=dev)
+        self.loss_num = torch.empty(1, dtype=torch.float32, device=dev)
+        self.timing = None   # optional dict tag -> list of (start, end) events
+
+    def _distributed(self):
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.pg) > 1
+
+    def __call__(self, points, labels, masks=None, seed=None):
+        model = self.model
+        eng = model._engine()
+        eng.timing = self.timing
+        model.train()
+        P = model._param_dict()
+        bufs = model._buffer_dict()
+        pflat, gflat = flat_buffers(model)
+        labels = labels.reshape(-1)
+        if labels.dtype != torch.int64:
+            labels = labels.long()
+        s = L.stream_ptr()
+        L.call("pcs_ce_weight_sum", L.ptr(labels), labels.numel(), L.ptr(self.class_weight),
+               model.num_classes, L.ptr(self.counts), L.ptr(self.wsum), s)
+        if self._distributed():
+            dist.all_reduce(self.wsum[:2], group=self.pg)   # global CE denominator
+        if seed is None:
+            seed = model._next_seed()
+        sv = eng.forward(P, bufs, points, train=True, masks=masks, seed=seed,
+                         head_mode=L.HEAD_CE, labels=labels, class_weight=self.class_weight,
+                         wsum=self.wsum, want_logits=False)
+        for bn, _ in BNS:
+            getattr(model, bn).num_batches_tracked.add_(1)
+        hb = eng.backward(P, sv, gflat)
+        L.call("pcs_reduce_partials", L.ptr(hb["loss_partial"]), hb["nch"], 1, 1.0,
+               L.ptr(self.loss_num), 1, 1, s)
+        del sv, hb
+        if self._distributed():
+            dist.all_reduce(gflat, group=self.pg)
+            dist.all_reduce(self.loss_num, group=self.pg)
+        self.opt.step()
+        return self.loss_num / self.wsum[0]

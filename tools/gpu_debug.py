@@ -51,8 +51,11 @@ def main():
         torch.from_numpy(np.packbits(masks[0], axis=1, bitorder="little")).to(dev),
         torch.from_numpy(np.packbits(masks[1], axis=1, bitorder="little")).to(dev)), seed=0)
     torch.cuda.synchronize()
-    for conv, ys in sv.ys.items():
-        print(f"  y[{conv:12s}] rel err {rel_err(ys.float().cpu().numpy(), cache[conv]['y']):.3e}")
+    for conv, ys in sv.ys.items():   # stored activations omit the per-channel BN offset
+        yv = ys.float().cpu().numpy()
+        ref = cache[conv]["y"]
+        d = (yv - yv.mean(0)) - (ref - ref.mean(0))
+        print(f"  y[{conv:12s}] centred rel err {np.abs(d).max() / np.abs(ref - ref.mean(0)).max():.3e}")
     print(f"  pooled g rel err {rel_err(sv.g.cpu().numpy(), cache['pool']['g']):.3e}")
     am = sv.am.cpu().numpy() - (np.arange(sv.B) * sv.N)[:, None]
     print(f"  argmax mismatches {(am != cache['pool']['idx']).sum()} / {am.size}")
@@ -67,7 +70,9 @@ def main():
         gv = p.grad.detach().cpu().numpy().reshape(-1)
         rv = grads[n].reshape(-1)
         e = np.abs(gv - rv).max() / max(np.abs(rv).max(), 1e-3 * gmax)
-        print(f"  grad[{n:22s}] rel err {e:.3e}  |g|={np.linalg.norm(rv):.3e}")
+        en = np.linalg.norm(gv - rv) / max(np.linalg.norm(rv), 1e-3 * gmax)
+        cs = gv @ rv / (np.linalg.norm(gv) * np.linalg.norm(rv) + 1e-30)
+        print(f"  grad[{n:22s}] max-rel {e:.3e} norm-rel {en:.3e} cos {cs:.6f} |g|={np.linalg.norm(rv):.3e}")
 
 
 if __name__ == "__main__":
