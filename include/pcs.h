@@ -32,6 +32,8 @@ typedef struct ihipStream_t *pcs_stream_t; /* == hipStream_t */
 
 enum { PCS_F32 = 0, PCS_BF16 = 1 };
 enum { PCS_OK = 0, PCS_EINVAL = -1000 };
+/* pcs_gemm_args.flags */
+enum { PCS_FLAG_GENERIC = 1 /* force the generic 128x{64,128} kernel (cross-checks) */ };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
 enum {
@@ -87,9 +89,12 @@ typedef struct {
   const float *emean, *erstd; /* [Ncols] BN_{l-1} batch mean / rstd (DGRAD S2) */
   float *stats;         /* [B*chunks_per_scene, Ncols, 2] partials (FWD, DGRAD) or NULL */
   float *pool;          /* [B*chunks_per_scene, Ncols, 4] (maxv, argmax, minv, argmin) or NULL */
+  int32_t flags;        /* PCS_FLAG_* */
 } pcs_gemm_args;
 
-/* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error. */
+/* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error.  The
+ * kernel (and so the row tile: 256 for the bf16 wide-layer kernel, 128 otherwise) is chosen
+ * from dtype, K, Ncols and flags, so call it with the same values as pcs_gemm. */
 int64_t pcs_gemm_geometry(pcs_gemm_args *args);
 /* Launch the GEMM. */
 int pcs_gemm(const pcs_gemm_args *args, pcs_stream_t stream);

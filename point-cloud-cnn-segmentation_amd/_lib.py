@@ -36,8 +36,11 @@ class GemmArgs(ct.Structure):
         ("W", _vp), ("C", _vp), ("bias", _vp), ("scene_bias", _vp), ("addend", _vp),
         ("c_mask", _vp), ("c_keep_scale", _f),
         ("Yp", _vp), ("es", _vp), ("et", _vp), ("emean", _vp), ("erstd", _vp),
-        ("stats", _vp), ("pool", _vp),
+        ("stats", _vp), ("pool", _vp), ("flags", _i32),
     ]
+
+
+FLAG_GENERIC = 1
 
 
 class WgradArgs(ct.Structure):

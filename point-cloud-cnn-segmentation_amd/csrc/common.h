@@ -5,14 +5,22 @@
 
 #include "../../include/pcs.h"
 
+#define PCS_DEV __device__ __forceinline__
+#define PCS_DEV_FWD __device__ __forceinline__
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short bf16_t;  // storage type of one bf16 element
+// 16-byte chunk as a native vector: HIP's uint4 is a struct whose plain copies lower to
+// memcpy through a private alloca (scratch); an ext_vector stays in VGPRs.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+PCS_DEV u32x4 mk_u32x4(unsigned a, unsigned b, unsigned c, unsigned d) {
+  u32x4 v = {a, b, c, d};
+  return v;
+}
 
-#define PCS_DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------------------------------
 // element traits: T = float (parity path, f32 MFMA) or bf16_t (bench path, bf16 MFMA)
@@ -37,22 +45,22 @@ PCS_DEV uint32_t pack2bf(float a, float b) {
 }
 
 // 16-byte chunk <-> float[EPC]
-PCS_DEV void unpack_chunk(const uint4 &c, float (&v)[4]) {
+PCS_DEV void unpack_chunk(const u32x4 &c, float (&v)[4]) {
   v[0] = __uint_as_float(c.x); v[1] = __uint_as_float(c.y);
   v[2] = __uint_as_float(c.z); v[3] = __uint_as_float(c.w);
 }
-PCS_DEV void unpack_chunk(const uint4 &c, float (&v)[8]) {
+PCS_DEV void unpack_chunk(const u32x4 &c, float (&v)[8]) {
   v[0] = bf2f(c.x & 0xffffu); v[1] = bf2f(c.x >> 16);
   v[2] = bf2f(c.y & 0xffffu); v[3] = bf2f(c.y >> 16);
   v[4] = bf2f(c.z & 0xffffu); v[5] = bf2f(c.z >> 16);
   v[6] = bf2f(c.w & 0xffffu); v[7] = bf2f(c.w >> 16);
 }
-PCS_DEV uint4 pack_chunk(const float (&v)[4]) {
-  return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+PCS_DEV u32x4 pack_chunk(const float (&v)[4]) {
+  return mk_u32x4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                     __float_as_uint(v[3]));
 }
-PCS_DEV uint4 pack_chunk(const float (&v)[8]) {
-  return make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
+PCS_DEV u32x4 pack_chunk(const float (&v)[8]) {
+  return mk_u32x4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
                     pack2bf(v[6], v[7]));
 }
 
@@ -104,6 +112,26 @@ struct ChunkGeo {
 };
 
 PCS_DEV int64_t pcs_min64(int64_t a, int64_t b) { return a < b ? a : b; }
+
+// Scene-aligned chunk geometry: fills a->chunks_per_scene (auto when <= 0, aiming at
+// ~target workgroups over ncb column blocks) and returns rows per chunk.
+inline int64_t pcs_fill_geometry(pcs_gemm_args *a, int64_t tile, int64_t target, int64_t ncb) {
+  const int64_t tps = (a->scene_rows + tile - 1) / tile;
+  int64_t cps = a->chunks_per_scene;
+  if (cps <= 0) cps = (target + a->num_scenes * ncb - 1) / (a->num_scenes * ncb);
+  if (cps > tps) cps = tps;
+  if (cps < 1) cps = 1;
+  const int64_t tpc = (tps + cps - 1) / cps;
+  cps = (tps + tpc - 1) / tpc;  // no empty chunks
+  a->chunks_per_scene = (int32_t)cps;
+  return tpc * tile;
+}
+
+// wide-layer bf16 kernel (gemm_big.hip)
+bool pcs_gemm_big_applicable(const pcs_gemm_args &a);
+int pcs_gemm_big_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
+                        hipStream_t s);
+constexpr int PCS_BIG_BM = 256;
 
 #define PCS_CHECK_LAUNCH()                                     \
   do {                                                         \

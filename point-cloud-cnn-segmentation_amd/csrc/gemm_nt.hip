@@ -57,6 +57,79 @@ PCS_DEV int xcd_remap(int bid, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
+// Staging of one k-step: global -> registers (issued early) ...
+template <typename T, int BM, int BN, int PRO>
+PCS_DEV void nt_load(const T *__restrict__ Ag, const T *__restrict__ A2g, const T *__restrict__ Wg,
+                     int64_t row_base, int valid, int K, int n0, int k0, int srow,
+                     u32x4 (&ra)[BM / 64], u32x4 (&ra2)[BM / 64], u32x4 (&rb)[BN / 64]) {
+#pragma unroll
+  for (int i = 0; i < BM / 64; ++i) {
+    const int r = min(srow + 64 * i, valid - 1);   // clamped: rows >= valid are zeroed later
+    const int64_t off = (row_base + r) * K + k0;
+    ra[i] = *reinterpret_cast<const u32x4 *>(Ag + off);
+    if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const u32x4 *>(A2g + off);
+  }
+#pragma unroll
+  for (int i = 0; i < BN / 64; ++i)
+    rb[i] = *reinterpret_cast<const u32x4 *>(Wg + (int64_t)(n0 + srow + 64 * i) * K + k0);
+}
+
+// ... then prologue transform and registers -> LDS (after the current k-step's MFMAs)
+template <typename T, int BM, int BN, int PRO>
+PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, int scene, int64_t row_base, int valid, int K,
+                      int k0, int slot, int srow, const u32x4 (&ra)[BM / 64],
+                      const u32x4 (&ra2)[BM / 64], const u32x4 (&rb)[BN / 64]) {
+  constexpr int EPC = Elem<T>::EPC;
+  char *tB = tA + BM * ROWB;
+  float c0[EPC], c1[EPC], c2[EPC];
+  if constexpr (PRO == PCS_PRO_BNRELU) {
+    load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1);
+  } else if constexpr (PRO == PCS_PRO_BWD) {
+    load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
+  } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+    load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
+    load_vec<EPC>(a.pool_coef + scene * K, k0, c0);
+  }
+#pragma unroll
+  for (int i = 0; i < BM / 64; ++i) {
+    const int r = srow + 64 * i;
+    float v[EPC];
+    unpack_chunk(ra[i], v);
+    if constexpr (PRO == PCS_PRO_BNRELU) {
+      uint32_t bits = 0xffu;
+      if (a.a_mask) bits = mask_bits(a.a_mask, row_base + min(r, valid - 1), K, k0, EPC);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+        if (a.a_mask) x *= ((bits >> e) & 1u) ? a.a_keep_scale : 0.f;
+        v[e] = x;
+      }
+    } else if constexpr (PRO == PCS_PRO_BWD) {
+      float y[EPC];
+      unpack_chunk(ra2[i], y);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) v[e] = fmaf(c0[e], v[e], fmaf(c2[e], y[e], c1[e]));
+    } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+      const int grow = (int)(row_base + r);
+      const int *am = a.pool_idx + scene * K + k0;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float x = fmaf(c2[e], v[e], c1[e]);
+        if (am[e] == grow) x += c0[e];
+        v[e] = x;
+      }
+    }
+    u32x4 out = pack_chunk(v);
+    if (r >= valid) out = mk_u32x4(0, 0, 0, 0);
+    *reinterpret_cast<u32x4 *>(tA + r * ROWB + swz(r, slot) * 16) = out;
+  }
+#pragma unroll
+  for (int i = 0; i < BN / 64; ++i) {
+    const int r = srow + 64 * i;
+    *reinterpret_cast<u32x4 *>(tB + r * ROWB + swz(r, slot) * 16) = rb[i];
+  }
+}
+
 template <typename T, int BM, int BN, int PRO, int EPI, bool POOL>
 __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                           int tiles_per_chunk, int ncb) {
@@ -117,92 +190,21 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
     const int64_t row_base = scene * N + (int64_t)tile * BM;
     const int valid = (int)pcs_min64(BM, N - (int64_t)tile * BM);
 
-    uint4 ra[ACH], ra2[ACH], rb[BCH];
-    auto load_stage = [&](int ks) {
-      const int k0 = ks * KSTEP + slot * EPC;
-#pragma unroll
-      for (int i = 0; i < ACH; ++i) {
-        const int r = srow + 64 * i;
-        if (r < valid) {
-          const int64_t off = (row_base + r) * K + k0;
-          ra[i] = *reinterpret_cast<const uint4 *>(Ag + off);
-          if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const uint4 *>(A2g + off);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < BCH; ++i) {
-        const int r = srow + 64 * i;
-        rb[i] = *reinterpret_cast<const uint4 *>(Wg + (int64_t)(n0 + r) * K + k0);
-      }
-    };
-    auto store_stage = [&](int ks, int buf) {
-      char *tA = lds + buf * (BM + BN) * ROWB;
-      char *tB = tA + BM * ROWB;
-      const int k0 = ks * KSTEP + slot * EPC;
-      float c0[EPC], c1[EPC], c2[EPC];
-      if constexpr (PRO == PCS_PRO_BNRELU) {
-        load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1);
-      } else if constexpr (PRO == PCS_PRO_BWD) {
-        load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
-      } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
-        load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
-        load_vec<EPC>(a.pool_coef + scene * K, k0, c0);
-      }
-#pragma unroll
-      for (int i = 0; i < ACH; ++i) {
-        const int r = srow + 64 * i;
-        uint4 out = make_uint4(0, 0, 0, 0);
-        if (r < valid) {
-          float v[EPC];
-          unpack_chunk(ra[i], v);
-          if constexpr (PRO == PCS_PRO_BNRELU) {
-            uint32_t bits = 0xffu;
-            if (a.a_mask) bits = mask_bits(a.a_mask, row_base + r, K, k0, EPC);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-              float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
-              if (a.a_mask) x *= ((bits >> e) & 1u) ? a.a_keep_scale : 0.f;
-              v[e] = x;
-            }
-          } else if constexpr (PRO == PCS_PRO_BWD) {
-            float y[EPC];
-            unpack_chunk(ra2[i], y);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] = fmaf(c0[e], v[e], fmaf(c2[e], y[e], c1[e]));
-          } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
-            // A holds Y_l here; the sparse dz lives at the argmax rows
-            const int grow = (int)(row_base + r);
-            const int *am = a.pool_idx + scene * K + k0;
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-              float x = fmaf(c2[e], v[e], c1[e]);
-              if (am[e] == grow) x += c0[e];
-              v[e] = x;
-            }
-          }
-          out = pack_chunk(v);
-        }
-        *reinterpret_cast<uint4 *>(tA + r * ROWB + swz(r, slot) * 16) = out;
-      }
-#pragma unroll
-      for (int i = 0; i < BCH; ++i) {
-        const int r = srow + 64 * i;
-        *reinterpret_cast<uint4 *>(tB + r * ROWB + swz(r, slot) * 16) = rb[i];
-      }
-    };
-
+    u32x4 ra[ACH], ra2[ACH], rb[BCH];
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    load_stage(0);
-    store_stage(0, 0);
+    nt_load<T, BM, BN, PRO>(Ag, A2g, Wg, row_base, valid, K, n0, slot * EPC, srow, ra, ra2, rb);
+    nt_store<T, BM, BN, PRO>(a, lds, scene, row_base, valid, K, slot * EPC, slot, srow, ra, ra2, rb);
     __syncthreads();
     for (int ks = 0; ks < nks; ++ks) {
       const int buf = ks & 1;
-      if (ks + 1 < nks) load_stage(ks + 1);
+      if (ks + 1 < nks)
+        nt_load<T, BM, BN, PRO>(Ag, A2g, Wg, row_base, valid, K, n0, (ks + 1) * KSTEP + slot * EPC,
+                                srow, ra, ra2, rb);
       const char *tA = lds + buf * (BM + BN) * ROWB;
       const char *tB = tA + BM * ROWB;
 #pragma unroll
@@ -217,7 +219,9 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
 #pragma unroll
           for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::mma(bf[j], af[i], acc[i][j]);
       }
-      if (ks + 1 < nks) store_stage(ks + 1, buf ^ 1);
+      if (ks + 1 < nks)
+        nt_store<T, BM, BN, PRO>(a, lds + (buf ^ 1) * (BM + BN) * ROWB, scene, row_base, valid, K,
+                                 (ks + 1) * KSTEP + slot * EPC, slot, srow, ra, ra2, rb);
       __syncthreads();
     }
 
@@ -262,10 +266,10 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
         const int64_t grow = row_base + rr;
         const int64_t goff = grow * Ncols + ecol;
         float v[EPC];
-        unpack_chunk(*reinterpret_cast<const uint4 *>(lds + rr * CROW + ecc * 16), v);
+        unpack_chunk(*reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16), v);
         if constexpr (EPI == PCS_EPI_FWD) {
-          if (Cg) *reinterpret_cast<uint4 *>(Cg + goff) =
-              *reinterpret_cast<const uint4 *>(lds + rr * CROW + ecc * 16);
+          if (Cg) *reinterpret_cast<u32x4 *>(Cg + goff) =
+              *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
           if (a.stats) {
             st_cnt += 1.f;
             const float rn = 1.f / st_cnt;
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
         } else if constexpr (EPI == PCS_EPI_DGRAD) {
           if (Addg) {
             float ad[EPC];
-            unpack_chunk(*reinterpret_cast<const uint4 *>(Addg + goff), ad);
+            unpack_chunk(*reinterpret_cast<const u32x4 *>(Addg + goff), ad);
 #pragma unroll
             for (int e = 0; e < EPC; ++e) v[e] += ad[e];
           }
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
             for (int e = 0; e < EPC; ++e) v[e] *= ((bits >> e) & 1u) ? a.c_keep_scale : 0.f;
           }
           float y[EPC];
-          unpack_chunk(*reinterpret_cast<const uint4 *>(Ypg + goff), y);
+          unpack_chunk(*reinterpret_cast<const u32x4 *>(Ypg + goff), y);
 #pragma unroll
           for (int e = 0; e < EPC; ++e) {
             const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? v[e] : 0.f;
@@ -304,10 +308,10 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
             st_mean[e] += dz;                                   // S1
             st_m2[e] = fmaf(dz, (y[e] - em[e]) * er[e], st_m2[e]);  // S2
           }
-          *reinterpret_cast<uint4 *>(Cg + goff) = pack_chunk(v);
+          *reinterpret_cast<u32x4 *>(Cg + goff) = pack_chunk(v);
         } else {  // RAW
-          *reinterpret_cast<uint4 *>(Cg + goff) =
-              *reinterpret_cast<const uint4 *>(lds + rr * CROW + ecc * 16);
+          *reinterpret_cast<u32x4 *>(Cg + goff) =
+              *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
         }
       }
     }
@@ -411,21 +415,12 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
 static constexpr int GEMM_BM = 128;
 
 extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
-  if (!a || a->num_scenes <= 0 || a->scene_rows <= 0)
+  if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Ncols <= 0)
     return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
-  const int64_t tps = (a->scene_rows + GEMM_BM - 1) / GEMM_BM;
-  int64_t cps = a->chunks_per_scene;
-  if (cps <= 0) {
-    const int ncb = a->Ncols >= 128 ? a->Ncols / 128 : 1;
-    const int64_t target = 2048;  // ~8 workgroups per CU
-    cps = (target + a->num_scenes * ncb - 1) / (a->num_scenes * ncb);
-  }
-  if (cps > tps) cps = tps;
-  if (cps < 1) cps = 1;
-  const int64_t tpc = (tps + cps - 1) / cps;
-  cps = (tps + tpc - 1) / tpc;  // no empty chunks
-  a->chunks_per_scene = (int32_t)cps;
-  return tpc * GEMM_BM;
+  if (pcs_gemm_big_applicable(*a))
+    return pcs_fill_geometry(a, PCS_BIG_BM, 256, a->Ncols / 256);   // one 512-thread WG per CU
+  const int64_t ncb = a->Ncols >= 128 ? a->Ncols / 128 : 1;
+  return pcs_fill_geometry(a, GEMM_BM, 2048, ncb);                 // ~8 WGs per CU
 }
 
 extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
@@ -449,9 +444,13 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
     return pcs_set_einval("pcs_gemm", "M must be < 2^31 rows");
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (pcs_gemm_big_applicable(a)) {
+    const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
+    return pcs_gemm_big_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
+  }
   const int tps = (int)((a.scene_rows + GEMM_BM - 1) / GEMM_BM);
   const int tpc = (int)(rpc / GEMM_BM);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool bn128 = a.Ncols % 128 == 0;
   if (a.dtype == PCS_BF16)
     return bn128 ? dispatch_pro_epi<bf16_t, 128>(a, tps, tpc, s) : dispatch_pro_epi<bf16_t, 64>(a, tps, tpc, s);

@@ -98,21 +98,21 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
     load_vec<EPC>(a.t, bk, xt);
   }
 
-  uint4 rz[OA::NCH], ry[OA::NCH], rx[OB::NCH];
+  u32x4 rz[OA::NCH], ry[OA::NCH], rx[OB::NCH];
   auto load_stage = [&](int64_t m0) {
 #pragma unroll
     for (int i = 0; i < OA::NCH; ++i) {
       const int64_t r = m0 + ar0 + OA::RP * i;
       if (r < hi) {
         const int64_t off = (scene * N + r) * Cout + an;
-        if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const uint4 *>(dZ + off);
-        ry[i] = *reinterpret_cast<const uint4 *>(Yg + off);
+        if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
+        ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
       }
     }
 #pragma unroll
     for (int i = 0; i < OB::NCH; ++i) {
       const int64_t r = m0 + br0 + OB::RP * i;
-      if (r < hi) rx[i] = *reinterpret_cast<const uint4 *>(Xg + (scene * N + r) * Cin + bk);
+      if (r < hi) rx[i] = *reinterpret_cast<const u32x4 *>(Xg + (scene * N + r) * Cin + bk);
     }
   };
   auto store_stage = [&](int64_t m0, int buf) {
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
     for (int i = 0; i < OA::NCH; ++i) {
       const int rl = ar0 + OA::RP * i;
       const int64_t r = m0 + rl;
-      uint4 out = make_uint4(0, 0, 0, 0);
+      u32x4 out = mk_u32x4(0, 0, 0, 0);
       if (r < hi) {
         float y[EPC], v[EPC];
         unpack_chunk(ry[i], y);
@@ -141,13 +141,13 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
         }
         out = pack_chunk(v);
       }
-      *reinterpret_cast<uint4 *>(tA + TnCfg<T>::prow(rl) * OA::ROWB + acc_c * 16) = out;
+      *reinterpret_cast<u32x4 *>(tA + TnCfg<T>::prow(rl) * OA::ROWB + acc_c * 16) = out;
     }
 #pragma unroll
     for (int i = 0; i < OB::NCH; ++i) {
       const int rl = br0 + OB::RP * i;
       const int64_t r = m0 + rl;
-      uint4 out = make_uint4(0, 0, 0, 0);
+      u32x4 out = mk_u32x4(0, 0, 0, 0);
       if (r < hi) {
         if constexpr (XMODE == PCS_PRO_BNRELU) {
           float v[EPC];
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
           out = rx[i];
         }
       }
-      *reinterpret_cast<uint4 *>(tB + TnCfg<T>::prow(rl) * OB::ROWB + bcc * 16) = out;
+      *reinterpret_cast<u32x4 *>(tB + TnCfg<T>::prow(rl) * OB::ROWB + bcc * 16) = out;
     }
   };
 

@@ -54,8 +54,8 @@ __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int
       acc = fmaf(w[e][3], x.w, acc);
       v[e] = acc;
     }
-    const uint4 packed = pack_chunk(v);
-    *reinterpret_cast<uint4 *>(Cg + grow * COLS + c0) = packed;
+    const u32x4 packed = pack_chunk(v);
+    *reinterpret_cast<u32x4 *>(Cg + grow * COLS + c0) = packed;
     unpack_chunk(packed, v);  // statistics of the stored (rounded) values
     cnt += 1.f;
     const float rn = 1.f / cnt;
@@ -109,8 +109,8 @@ __global__ __launch_bounds__(THREADS) void conv1_wgrad_kernel(pcs_wgrad_args a, 
   for (int64_t r = lo + r0; r < hi; r += RPP) {
     const int64_t grow = scene * N + r;
     float dz[EPC], y[EPC];
-    unpack_chunk(*reinterpret_cast<const uint4 *>(dZ + grow * COLS + c0), dz);
-    unpack_chunk(*reinterpret_cast<const uint4 *>(Y + grow * COLS + c0), y);
+    unpack_chunk(*reinterpret_cast<const u32x4 *>(dZ + grow * COLS + c0), dz);
+    unpack_chunk(*reinterpret_cast<const u32x4 *>(Y + grow * COLS + c0), y);
     const float4 x = *reinterpret_cast<const float4 *>(X + grow * 4);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tile
 #pragma unroll
       for (int c = 0; c < QCH; c += EPC) {
         float y[EPC], s[EPC], t[EPC], mu[EPC], rs[EPC];
-        unpack_chunk(*reinterpret_cast<const uint4 *>(Y + grow * HEAD_CIN + ch0 + c), y);
+        unpack_chunk(*reinterpret_cast<const u32x4 *>(Y + grow * HEAD_CIN + ch0 + c), y);
         load_vec<EPC>(a.s, ch0 + c, s); load_vec<EPC>(a.t, ch0 + c, t);
         if constexpr (MODE != PCS_HEAD_FWD) { load_vec<EPC>(a.mean, ch0 + c, mu); load_vec<EPC>(a.rstd, ch0 + c, rs); }
 #pragma unroll
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tile
             s1[c + e] += dz;
             s2[c + e] = fmaf(dz, xh[r * HEAD_LD + ch], s2[c + e]);
           }
-          *reinterpret_cast<uint4 *>(dZ + grow * HEAD_CIN + ch0 + c) = pack_chunk(v);
+          *reinterpret_cast<u32x4 *>(dZ + grow * HEAD_CIN + ch0 + c) = pack_chunk(v);
         }
       }
       // phase 4: dW / db partials (each weight or bias entry owned by one thread);
@@ -645,7 +645,7 @@ extern "C" int pcs_conv1_fwd(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (!ap || !ap->A || !ap->W || !ap->C) return pcs_set_einval("pcs_conv1_fwd", "missing operand");
   if (ap->K != 4 || ap->Ncols != 64) return pcs_set_einval("pcs_conv1_fwd", "conv1 is 4 -> 64");
   pcs_gemm_args a = *ap;
-  const int64_t tpc = chunk_geo(a.scene_rows, a.num_scenes, C1_BM, &a.chunks_per_scene, 1024);
+  const int64_t tpc = pcs_fill_geometry(&a, C1_BM, 2048, 1) / C1_BM;
   const int tps = (int)((a.scene_rows + C1_BM - 1) / C1_BM);
   const int nb = (int)(a.num_scenes * a.chunks_per_scene);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -108,6 +108,7 @@ class Engine:
             off += self.numel[n]
         self.total_params = off
         self._geo = {}
+        self.flags = 0       # L.FLAG_GENERIC forces the generic GEMM (cross-checks)
         self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
         L.load()
 
@@ -127,11 +128,12 @@ class Engine:
     def _stream(self):
         return L.stream_ptr()
 
-    def geometry(self, B, N, ncols):
-        key = (B, N, ncols)
+    def geometry(self, B, N, K, ncols, pro=L.PRO_BNRELU, epi=L.EPI_FWD):
+        """(chunks_per_scene, rows_per_chunk) of the kernel pcs_gemm picks for these args."""
+        key = (B, N, K, ncols, pro, epi, self.flags)
         if key not in self._geo:
-            a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=ncols, dtype=self.dt,
-                           chunks_per_scene=0)
+            a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
+                           prologue=pro, epilogue=epi, chunks_per_scene=0, flags=self.flags)
             rpc = L.load().pcs_gemm_geometry(ct.byref(a))
             if rpc <= 0:
                 raise L.PcsError(L.load().pcs_last_error().decode())
@@ -178,9 +180,9 @@ class Engine:
 
     def _gemm(self, B, N, K, ncols, pro, epi, A, W, C, **kw):
         tag = kw.pop("tag", None)
-        cps, _ = self.geometry(B, N, ncols)
+        cps, _ = self.geometry(B, N, K, ncols, pro, epi)
         a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
-                       prologue=pro, epilogue=epi, chunks_per_scene=cps,
+                       prologue=pro, epilogue=epi, chunks_per_scene=cps, flags=self.flags,
                        A=L.ptr(A), W=L.ptr(W), C=L.ptr(C),
                        a_keep_scale=kw.pop("a_keep_scale", 1.0),
                        c_keep_scale=kw.pop("c_keep_scale", 1.0))
@@ -228,8 +230,8 @@ class Engine:
         sv.wc = wc = self.cast_weights(P)
         T = self.tdt
 
-        def stats_buf(ncols):
-            cps, rpc = self.geometry(B, N, ncols)
+        def stats_buf(K, ncols):
+            cps, rpc = self.geometry(B, N, K, ncols)
             return torch.empty(B * cps, ncols, 2, dtype=torch.float32, device=dev), cps, rpc
 
         def bnrelu(prev):
@@ -240,7 +242,11 @@ class Engine:
         # shifts running_mean), which keeps them centred: full precision in fp32/bf16.
         # conv1 (K=4)
         y1 = self._empty(M, 64, device=dev)
-        st, cps, rpc = stats_buf(64) if train else (None, *self.geometry(B, N, 64))
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=4, Ncols=64, dtype=L.F32, chunks_per_scene=0,
+                       flags=L.FLAG_GENERIC)
+        rpc = L.load().pcs_gemm_geometry(ct.byref(a))    # conv1: generic 128-row geometry
+        cps = a.chunks_per_scene
+        st = torch.empty(B * cps, 64, 2, dtype=torch.float32, device=dev) if train else None
         a = L.GemmArgs(num_scenes=B, scene_rows=N, K=4, Ncols=64, dtype=self.dt,
                        chunks_per_scene=cps, A=L.ptr(x), W=L.ptr(P["conv1.weight"]),
                        C=L.ptr(y1), bias=None, stats=L.ptr(st))
@@ -251,7 +257,7 @@ class Engine:
 
         def layer(conv, src_conv, src_bn, K, ncols, bnname, offset, **kw):
             y = self._empty(M, ncols, device=dev)
-            st, cps, rpc = stats_buf(ncols) if train else (None, 0, 0)
+            st, cps, rpc = stats_buf(K, ncols) if train else (None, 0, 0)
             self._gemm(B, N, K, ncols, L.PRO_BNRELU, L.EPI_FWD, sv.ys[src_conv], wc[conv][0], y,
                        stats=st, tag=f"fwd:{conv}", **bnrelu(src_bn), **kw)
             sv.ys[conv] = y
@@ -265,7 +271,7 @@ class Engine:
         layer("conv5", "conv4", "bn4", 128, 1024, "bn5", P["conv5.bias"])
 
         # global_feat + max-pool partials
-        cps_g, _ = self.geometry(B, N, 1024)
+        cps_g, _ = self.geometry(B, N, 1024, 1024)
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
         layer("global_feat", "conv5", "bn5", 1024, 1024, "bn_global", P["global_feat.bias"],
               pool=pool)
@@ -392,7 +398,7 @@ class Engine:
                   addend=None):
             al, be, ga = coefs[bn]
             pc = sv.bn[prev_bn]
-            cps, _ = self.geometry(B, N, cin)
+            cps, _ = self.geometry(B, N, cout, cin, L.PRO_BWD, L.EPI_DGRAD)
             st = torch.empty(B * cps, cin, 2, dtype=torch.float32, device=dev)
             self._gemm(B, N, cout, cin, L.PRO_BWD, L.EPI_DGRAD, dz, wc[conv][1], out,
                        A2=ycur, pa=al, pb=be, pc=ga, Yp=sv.ys[prev_conv], es=pc.scale, et=pc.shift,
@@ -451,7 +457,7 @@ class Engine:
 
         # global_feat (dy from the sparse max-pool gradient)
         pc5 = sv.bn["bn5"]
-        cps5, _ = self.geometry(B, N, 1024)
+        cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD)
         st = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
         self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD, ys["global_feat"],
                    wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
