@@ -125,11 +125,23 @@ typedef struct {
   float *partial;       /* workspace: pcs_wgrad_workspace() bytes */
   float *dW;            /* [Cout, Cin] f32 output, row stride ldw */
   int64_t ldw;          /* 0 = Cin */
+  int32_t flags;        /* PCS_FLAG_GENERIC: never use the 256x256 wide-layer kernel */
 } pcs_wgrad_args;
 
 int64_t pcs_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_per_scene */
 int pcs_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream);
 int pcs_conv1_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream); /* X = points f32 */
+
+/*
+ * Streaming column statistics of a stored activation Y [M, C] (C/8 (bf16) or C/4 (fp32)
+ * must divide 256): per-chunk (mean, M2) BN partials and optional max-pool partials, in
+ * pcs_gemm's epilogue formats.  One HBM pass; used for the 1024-wide global_feat output.
+ */
+int64_t pcs_colstats_geometry(int64_t num_scenes, int64_t scene_rows, int32_t C,
+                              int32_t *chunks_per_scene);
+int pcs_colstats(const void *Y, int64_t num_scenes, int64_t scene_rows, int32_t C, int32_t dtype,
+                 int32_t chunks_per_scene, int64_t rows_per_chunk, float *stats, float *pool,
+                 pcs_stream_t stream);
 
 /*
  * BatchNorm1d train-mode statistics (P:86-94 semantics used at P:106-127): merge the

@@ -52,7 +52,7 @@ class WgradArgs(ct.Structure):
         ("pool_idx", _vp), ("pool_coef", _vp),
         ("x_mode", _i32),
         ("X", _vp), ("s", _vp), ("t", _vp), ("x_mask", _vp), ("x_keep_scale", _f),
-        ("partial", _vp), ("dW", _vp), ("ldw", _i64),
+        ("partial", _vp), ("dW", _vp), ("ldw", _i64), ("flags", _i32),
     ]
 
 
@@ -107,6 +107,8 @@ SIGNATURES = [
     ("pcs_reduce_partials", ct.c_int, [_vp, _i64, _i64, _f, _vp, _i64, _i64, _vp]),
     ("pcs_cast_weight", ct.c_int, [_vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     ("pcs_adam", ct.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _f, _i64, _vp]),
+    ("pcs_colstats_geometry", _i64, [_i64, _i64, _i32, ct.POINTER(_i32)]),
+    ("pcs_colstats", ct.c_int, [_vp, _i64, _i64, _i32, _i32, _i32, _i64, _vp, _vp, _vp]),
     ("pcs_abi_version", ct.c_int, []),
     ("pcs_last_error", ct.c_char_p, []),
 ]

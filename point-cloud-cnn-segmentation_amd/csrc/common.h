@@ -132,6 +132,10 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a);
 int pcs_gemm_big_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                         hipStream_t s);
 constexpr int PCS_BIG_BM = 256;
+// wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)
+bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a);
+int pcs_wgrad_big_splits(const pcs_wgrad_args &a);
+int pcs_wgrad_big_launch(const pcs_wgrad_args &a, hipStream_t s);
 
 #define PCS_CHECK_LAUNCH()                                     \
   do {                                                         \

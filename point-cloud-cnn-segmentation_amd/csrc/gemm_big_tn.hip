@@ -1,0 +1,213 @@
+// bf16 256x256 weight-gradient kernel for the wide layer (global_feat, 1024 x 1024:
+// dW = dy^T x summed over all M points; autograd of P:113 at P:254).
+//
+// * 512 threads = 8 waves as 2 (Cout) x 4 (Cin); each wave owns 128 x 64 outputs
+//   (8 x 4 v_mfma_f32_16x16x32_bf16 accumulators), 64 MFMAs per 64-row step.
+// * dy = beta + gamma*y_g (+ alpha*dz at the max-pool argmax rows) and x = relu(bn5(y5))
+//   are formed while staging [64 rows x 256 cols] tiles global -> VGPR -> LDS; the MFMA
+//   operands are read back transposed with ds_read_b64_tr_b16 (rows permuted + 32-B
+//   padded: the 8 rows one transposed read touches hit 8 distinct bank groups).
+// * the M reduction is split into scene-aligned row slices; each workgroup writes one
+//   fp32 partial tile and pcs_reduce_partials sums them in a fixed order.
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 512;
+constexpr int TM = 256, TN = 256, MS = 64;
+constexpr int ROWB = TM * 2 + 32;          // 544 B: padded LDS row
+constexpr int OPB = MS * ROWB;             // one operand tile (34 KB)
+constexpr int STAGE = 2 * OPB;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+PCS_DEV int xcd_remap(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+PCS_DEV bf16x8 tr_frag(const char *tile, int r0, int r1, int col) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tile + r0 * ROWB + col * 2));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tile + r1 * ROWB + col * 2));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int DYMODE>
+PCS_DEV void tn_load(const bf16_t *__restrict__ dZ, const bf16_t *__restrict__ Yg,
+                     const bf16_t *__restrict__ Xg, int64_t rbase, int64_t rlast, int Cout, int Cin,
+                     int an, int bk, int r0, u32x4 (&rz)[4], u32x4 (&ry)[4], u32x4 (&rx)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = rbase + r0 + 16 * i < rlast ? rbase + r0 + 16 * i : rlast - 1;
+    if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + r * Cout + an);
+    ry[i] = *reinterpret_cast<const u32x4 *>(Yg + r * Cout + an);
+    rx[i] = *reinterpret_cast<const u32x4 *>(Xg + r * Cin + bk);
+  }
+}
+
+template <int DYMODE>
+PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, int scene, int64_t rbase, int64_t rlast,
+                      int an, int bk, int cc, int r0, const u32x4 (&rz)[4], const u32x4 (&ry)[4],
+                      const u32x4 (&rx)[4]) {
+  char *tB = tA + OPB;
+  float ca[8], cb[8], cg[8], xs[8], xt[8];
+  int am[8];
+  load_vec<8>(a.beta, an, cb);
+  load_vec<8>(a.gamma, an, cg);
+  if constexpr (DYMODE == PCS_PRO_BWD) {
+    load_vec<8>(a.alpha, an, ca);
+  } else {
+    load_vec<8>(a.pool_coef + scene * a.Cout, an, ca);
+    const int4 i0 = *reinterpret_cast<const int4 *>(a.pool_idx + scene * a.Cout + an);
+    const int4 i1 = *reinterpret_cast<const int4 *>(a.pool_idx + scene * a.Cout + an + 4);
+    am[0] = i0.x; am[1] = i0.y; am[2] = i0.z; am[3] = i0.w;
+    am[4] = i1.x; am[5] = i1.y; am[6] = i1.z; am[7] = i1.w;
+  }
+  load_vec<8>(a.s, bk, xs);
+  load_vec<8>(a.t, bk, xt);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = r0 + 16 * i;
+    const int64_t r = rbase + rl;
+    const bool ok = r < rlast;
+    float y[8], v[8];
+    unpack_chunk(ry[i], y);
+    if constexpr (DYMODE == PCS_PRO_BWD) {
+      unpack_chunk(rz[i], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = fmaf(cg[e], y[e], cb[e]);
+        if (am[e] == (int)r) x += ca[e];
+        v[e] = x;
+      }
+    }
+    u32x4 o = pack_chunk(v);
+    if (!ok) o = mk_u32x4(0, 0, 0, 0);
+    *reinterpret_cast<u32x4 *>(tA + prow(rl) * ROWB + cc * 16) = o;
+    float w[8];
+    unpack_chunk(rx[i], w);
+    uint32_t bits = 0xffu;
+    if (a.x_mask) bits = mask_bits(a.x_mask, ok ? r : rlast - 1, a.Cin, bk, 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = fmaxf(fmaf(w[e], xs[e], xt[e]), 0.f);
+      if (a.x_mask) x *= ((bits >> e) & 1u) ? a.x_keep_scale : 0.f;
+      w[e] = x;
+    }
+    u32x4 ox = pack_chunk(w);
+    if (!ok) ox = mk_u32x4(0, 0, 0, 0);
+    *reinterpret_cast<u32x4 *>(tB + prow(rl) * ROWB + cc * 16) = ox;
+  }
+}
+
+template <int DYMODE>
+__global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, int64_t rows_per_split,
+                                                            int ntn, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / ntiles, tile = L % ntiles;
+  const int n0 = (tile / ntn) * TM, k0 = (tile % ntn) * TN;
+  const int sps = a.splits_per_scene;
+  const int scene = split / sps, sis = split % sps;
+  const int64_t N = a.scene_rows;
+  const int64_t lo = (int64_t)sis * rows_per_split;
+  const int64_t hi = pcs_min64(lo + rows_per_split, N);
+  const int64_t rlast = scene * N + hi;           // global row bound of this slice
+  const int Cout = a.Cout, Cin = a.Cin;
+  const bf16_t *dZ = reinterpret_cast<const bf16_t *>(a.dZ);
+  const bf16_t *Yg = reinterpret_cast<const bf16_t *>(a.Y);
+  const bf16_t *Xg = reinterpret_cast<const bf16_t *>(a.X);
+  const int cc = tid & 31, r0 = tid >> 5;   // staging: fixed 8-column chunk, rows r0 + 16 i
+  const int an = n0 + cc * 8, bk = k0 + cc * 8;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (int)((hi - lo + MS - 1) / MS);
+  u32x4 rz[4], ry[4], rx[4];
+  if (nsteps > 0) {
+    const int64_t rb = scene * N + lo;
+    tn_load<DYMODE>(dZ, Yg, Xg, rb, rlast, Cout, Cin, an, bk, r0, rz, ry, rx);
+    tn_store<DYMODE>(a, lds, scene, rb, rlast, an, bk, cc, r0, rz, ry, rx);
+    __syncthreads();
+  }
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const int64_t rb = scene * N + lo + (int64_t)st * MS;
+    if (st + 1 < nsteps) tn_load<DYMODE>(dZ, Yg, Xg, rb + MS, rlast, Cout, Cin, an, bk, r0, rz, ry, rx);
+    const char *tA = lds + buf * STAGE;
+    const char *tB = tA + OPB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ra = prow(32 * kk + 8 * g + q), rb1 = prow(32 * kk + 8 * g + 4 + q);
+      bf16x8 xf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[j] = tr_frag(tB, ra, rb1, wn * 64 + j * 16 + 4 * p);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 yf = tr_frag(tA, ra, rb1, wm * 128 + i * 16 + 4 * p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], yf, acc[i][j], 0, 0, 0);
+      }
+    }
+    if (st + 1 < nsteps)
+      tn_store<DYMODE>(a, lds + (buf ^ 1) * STAGE, scene, rb + MS, rlast, an, bk, cc, r0, rz, ry, rx);
+    __syncthreads();
+  }
+  // lane holds dW[n = n0 + wm*128 + i*16 + (lane&15)][k = k0 + wn*64 + j*16 + 4*(lane>>4) + r]
+  float *out = a.partial + (int64_t)split * Cout * Cin;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = n0 + wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<float4 *>(out + (int64_t)n * Cin + k) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+}
+
+}  // namespace
+
+bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a) {
+  return !(a.flags & PCS_FLAG_GENERIC) && a.dtype == PCS_BF16 && a.Cout % TM == 0 && a.Cin % TN == 0 && a.x_mode == PCS_PRO_BNRELU &&
+         (a.dy_mode == PCS_PRO_BWD || a.dy_mode == PCS_PRO_BWD_POOL);
+}
+
+int pcs_wgrad_big_splits(const pcs_wgrad_args &a) {
+  const int64_t ntiles = (int64_t)(a.Cout / TM) * (a.Cin / TN);
+  int64_t sps = (256 + a.num_scenes * ntiles - 1) / (a.num_scenes * ntiles);  // 1 WG per CU
+  const int64_t max_sps = (a.scene_rows + 8 * MS - 1) / (8 * MS);
+  if (sps > max_sps) sps = max_sps;
+  if (sps < 1) sps = 1;
+  return (int)sps;
+}
+
+int pcs_wgrad_big_launch(const pcs_wgrad_args &a, hipStream_t s) {
+  int64_t rps = (a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene;
+  rps = (rps + MS - 1) / MS * MS;
+  const int ntn = a.Cin / TN, ntiles = (a.Cout / TM) * ntn;
+  const int nb = ntiles * (int)(a.num_scenes * a.splits_per_scene);
+  if (a.dy_mode == PCS_PRO_BWD_POOL)
+    hipLaunchKernelGGL(wgrad_big_kernel<PCS_PRO_BWD_POOL>, dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  else
+    hipLaunchKernelGGL(wgrad_big_kernel<PCS_PRO_BWD>, dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

@@ -194,7 +194,8 @@ class Engine:
         tag = kw.pop("tag", None)
         a = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=cout, Cin=cin, dtype=self.dt,
                         splits_per_scene=0, dy_mode=dy_mode, x_mode=x_mode,
-                        x_keep_scale=kw.pop("x_keep_scale", 1.0), dW=L.ptr(dW), ldw=ldw)
+                        x_keep_scale=kw.pop("x_keep_scale", 1.0), dW=L.ptr(dW), ldw=ldw,
+                        flags=self.flags)
         for k, v in kw.items():
             setattr(a, k, L.ptr(v))
         fn = "pcs_conv1_wgrad" if cin == 4 else "pcs_wgrad"
@@ -270,11 +271,21 @@ class Engine:
         layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"])
         layer("conv5", "conv4", "bn4", 128, 1024, "bn5", P["conv5.bias"])
 
-        # global_feat + max-pool partials
-        cps_g, _ = self.geometry(B, N, 1024, 1024)
+        # global_feat: plain GEMM + store, then one streaming pass for BN stats + max-pool
+        # partials (cheaper than reducing 1024 columns inside the GEMM epilogue)
+        yg = self._empty(M, 1024, device=dev)
+        self._gemm(B, N, 1024, 1024, L.PRO_BNRELU, L.EPI_FWD, sv.ys["conv5"], wc["global_feat"][0], yg,
+                   tag="fwd:global_feat", **bnrelu("bn5"))
+        sv.ys["global_feat"] = yg
+        cps_g = ct.c_int32(0)
+        rpc_g = L.load().pcs_colstats_geometry(B, N, 1024, ct.byref(cps_g))
+        cps_g = cps_g.value
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
-        layer("global_feat", "conv5", "bn5", 1024, 1024, "bn_global", P["global_feat.bias"],
-              pool=pool)
+        st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
+        self._launch("stats:global_feat", "pcs_colstats", L.ptr(yg), B, N, 1024, self.dt, cps_g, rpc_g,
+                     L.ptr(st), L.ptr(pool), s)
+        sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_g, rpc_g, P, bufs,
+                                               train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]
         sv.g = torch.empty(B, 1024, dtype=torch.float32, device=dev)
         sv.am = torch.empty(B, 1024, dtype=torch.int32, device=dev)
