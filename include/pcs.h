@@ -144,6 +144,16 @@ int pcs_colstats(const void *Y, int64_t num_scenes, int64_t scene_rows, int32_t 
                  pcs_stream_t stream);
 
 /*
+ * The EPI_DGRAD epilogue as a streaming pass, in place on a raw dgrad output D [M, C]
+ * (written by pcs_gemm with PCS_EPI_RAW): D = (Yp*s+t > 0) ? (D + addend)*keep : 0 and
+ * per-chunk (S1, S2) partials; chunking as pcs_colstats_geometry.
+ */
+int pcs_bnrelu_bwd(void *D, const void *Yp, const void *addend, const uint8_t *mask, float keep_scale,
+                   const float *s, const float *t, const float *mean, const float *rstd,
+                   int64_t num_scenes, int64_t scene_rows, int32_t C, int32_t dtype,
+                   int32_t chunks_per_scene, int64_t rows_per_chunk, float *stats, pcs_stream_t stream);
+
+/*
  * BatchNorm1d train-mode statistics (P:86-94 semantics used at P:106-127): merge the
  * per-chunk (mean, M2) partials (Chan, fp64) into the batch mean / biased variance over
  * all B*N rows (pads included), derive the fused affine y*scale+shift, and update the

@@ -109,6 +109,8 @@ SIGNATURES = [
     ("pcs_adam", ct.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _f, _i64, _vp]),
     ("pcs_colstats_geometry", _i64, [_i64, _i64, _i32, ct.POINTER(_i32)]),
     ("pcs_colstats", ct.c_int, [_vp, _i64, _i64, _i32, _i32, _i32, _i64, _vp, _vp, _vp]),
+    ("pcs_bnrelu_bwd", ct.c_int, [_vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32,
+                                  _i32, _i64, _vp, _vp]),
     ("pcs_abi_version", ct.c_int, []),
     ("pcs_last_error", ct.c_char_p, []),
 ]

@@ -119,3 +119,94 @@ extern "C" int pcs_colstats(const void *Y, int64_t num_scenes, int64_t scene_row
   PCS_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// Streaming BN_{l-1} backward input stage, in place on a raw dgrad output:
+//   v = dA (+ addend) (* keep * keep_scale);  dz = (Yp*s + t > 0) ? v : 0;  store dz;
+//   per-chunk S1 = sum dz, S2 = sum dz * (Yp - mean) * rstd.
+// (the EPI_DGRAD epilogue of pcs_gemm as a separate HBM pass, for the wide layer)
+// ---------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+__global__ __launch_bounds__(THREADS) void bnrelu_bwd_kernel(T *__restrict__ D, const T *__restrict__ Yp,
+                                                             const T *__restrict__ addend, const uint8_t *mask,
+                                                             float keep_scale, const float *es, const float *et,
+                                                             const float *em, const float *er, int64_t N, int C,
+                                                             int cps, int64_t rows_per_chunk, float *stats) {
+  constexpr int EPC = Elem<T>::EPC;
+  __shared__ float2 red[THREADS];
+  const int cpr = C / EPC, rpp = THREADS / cpr;
+  const int tid = threadIdx.x, cc = tid % cpr, r0 = tid / cpr, c0 = cc * EPC;
+  const int chunk = blockIdx.x, scene = chunk / cps, cis = chunk % cps;
+  const int64_t lo = (int64_t)cis * rows_per_chunk;
+  const int64_t hi = pcs_min64(lo + rows_per_chunk, N);
+  float s[EPC], t[EPC], mu[EPC], rs[EPC], s1[EPC], s2[EPC];
+  load_vec<EPC>(es, c0, s); load_vec<EPC>(et, c0, t);
+  load_vec<EPC>(em, c0, mu); load_vec<EPC>(er, c0, rs);
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll 4
+  for (int64_t r = lo + r0; r < hi; r += rpp) {
+    const int64_t row = scene * N + r;
+    const int64_t off = row * C + c0;
+    float v[EPC], y[EPC];
+    unpack_chunk(*reinterpret_cast<const u32x4 *>(D + off), v);
+    unpack_chunk(*reinterpret_cast<const u32x4 *>(Yp + off), y);
+    if (addend) {
+      float ad[EPC];
+      unpack_chunk(*reinterpret_cast<const u32x4 *>(addend + off), ad);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) v[e] += ad[e];
+    }
+    if (mask) {
+      const uint32_t bits = mask_bits(mask, row, C, c0, EPC);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) v[e] *= ((bits >> e) & 1u) ? keep_scale : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const float dz = fmaf(y[e], s[e], t[e]) > 0.f ? v[e] : 0.f;
+      v[e] = dz;
+      s1[e] += dz;
+      s2[e] = fmaf(dz, (y[e] - mu[e]) * rs[e], s2[e]);
+    }
+    *reinterpret_cast<u32x4 *>(D + off) = pack_chunk(v);
+  }
+  for (int e = 0; e < EPC; ++e) {
+    red[tid] = make_float2(s1[e], s2[e]);
+    __syncthreads();
+    if (r0 == 0) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int j = 0; j < rpp; ++j) { a1 += red[j * cpr + cc].x; a2 += red[j * cpr + cc].y; }
+      *reinterpret_cast<float2 *>(stats + ((int64_t)chunk * C + c0 + e) * 2) = make_float2(a1, a2);
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+extern "C" int pcs_bnrelu_bwd(void *D, const void *Yp, const void *addend, const uint8_t *mask,
+                              float keep_scale, const float *s, const float *t, const float *mean,
+                              const float *rstd, int64_t num_scenes, int64_t scene_rows, int32_t C,
+                              int32_t dtype, int32_t chunks_per_scene, int64_t rows_per_chunk, float *stats,
+                              pcs_stream_t stream) {
+  const int epc = dtype == PCS_BF16 ? 8 : 4;
+  if (!D || !Yp || !s || !t || !mean || !rstd || !stats || C % epc || C / epc > THREADS ||
+      THREADS % (C / epc) || chunks_per_scene <= 0 || rows_per_chunk <= 0)
+    return pcs_set_einval("pcs_bnrelu_bwd", "bad arguments");
+  const int nb = (int)(num_scenes * chunks_per_scene);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(bnrelu_bwd_kernel<bf16_t>, dim3(nb), dim3(THREADS), 0, st, reinterpret_cast<bf16_t *>(D),
+                       reinterpret_cast<const bf16_t *>(Yp), reinterpret_cast<const bf16_t *>(addend), mask,
+                       keep_scale, s, t, mean, rstd, scene_rows, (int)C, (int)chunks_per_scene, rows_per_chunk,
+                       stats);
+  else if (dtype == PCS_F32)
+    hipLaunchKernelGGL(bnrelu_bwd_kernel<float>, dim3(nb), dim3(THREADS), 0, st, reinterpret_cast<float *>(D),
+                       reinterpret_cast<const float *>(Yp), reinterpret_cast<const float *>(addend), mask,
+                       keep_scale, s, t, mean, rstd, scene_rows, (int)C, (int)chunks_per_scene, rows_per_chunk,
+                       stats);
+  else return pcs_set_einval("pcs_bnrelu_bwd", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

@@ -9,10 +9,11 @@
 //   16-B slots XOR-swizzled with (row>>1)&7 so the ds_read_b128 fragment reads are
 //   bank-conflict free; two LDS stages, one barrier per k-step; the next k-step's global
 //   loads are issued before the current MFMAs.
-// * forward epilogue: BN statistics (tile two-pass mean/M2, Chan-merged per column) and
-//   the max-pool max/min+argrow are reduced straight from the accumulators with
-//   cross-lane shuffles; the tile is staged through LDS for 16-B coalesced stores.
-// * dgrad epilogue: ReLU/BN-backward of the previous layer on coalesced row chunks.
+// * forward epilogue: bias, tile staged through LDS for 16-B coalesced stores (BN
+//   statistics and max-pool partials come from one streaming pass, pcs_colstats: fused
+//   here as cross-lane reductions they cost ~1/3 of the kernel).
+// * dgrad: raw store (PCS_EPI_RAW); the ReLU / BN-backward stage of the previous layer runs
+//   as one streaming pass (pcs_bnrelu_bwd).
 #include "common.h"
 
 namespace {
@@ -65,15 +66,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
 
   const int slot = tid & 7, srow = tid >> 3;  // staging: rows srow + 64*i, fixed k-slot
 
-  // running per-column state (thread t < BN owns column n0 + t)
-  float run_n = 0.f, run_mean = 0.f, run_m2 = 0.f;
-  float run_max = -__builtin_huge_valf(), run_min = __builtin_huge_valf();
-  int run_maxi = 0x7fffffff, run_mini = 0x7fffffff;
-  // DGRAD: per-thread S1/S2 for the phase-2 column chunk
   const int ecc = tid % CPR, er0 = tid / CPR, ecol = n0 + ecc * EPC;
-  float s1[EPC], s2[EPC];
-#pragma unroll
-  for (int e = 0; e < EPC; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
 
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int64_t row_base = scene * N + (int64_t)tile * BM;
@@ -187,104 +180,13 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     // lane owns rows m = wm*128 + i*16 + (lane&15), cols n = wn*64 + j*16 + 4*(lane>>4) + r
     const int lrow = lane & 15, lcol = 4 * (lane >> 4);
     if constexpr (EPI == PCS_EPI_FWD) {
-      // bias and bf16 rounding (statistics describe the stored values)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a.bias) bb = *reinterpret_cast<const float4 *>(a.bias + n0 + wn * 64 + j * 16 + lcol);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          acc[i][j][0] = round_bf16(acc[i][j][0] + bb.x);
-          acc[i][j][1] = round_bf16(acc[i][j][1] + bb.y);
-          acc[i][j][2] = round_bf16(acc[i][j][2] + bb.z);
-          acc[i][j][3] = round_bf16(acc[i][j][3] + bb.w);
-        }
-      }
-      if (a.stats) {
-        // pass 1: column sums over the valid rows of this tile
+      if (a.bias) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+          const float4 bb = *reinterpret_cast<const float4 *>(a.bias + n0 + wn * 64 + j * 16 + lcol);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float sum = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-              if (wm * 128 + i * 16 + lrow < valid) sum += acc[i][j][r];
-            sum += __shfl_xor(sum, 1); sum += __shfl_xor(sum, 2);
-            sum += __shfl_xor(sum, 4); sum += __shfl_xor(sum, 8);
-            if (lrow == 0) sred[wm * BN + wn * 64 + j * 16 + lcol + r] = sum;
-          }
-        }
-        __syncthreads();
-        const float inv = 1.f / (float)valid;
-        // pass 2: squared deviations around the tile mean
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int c = wn * 64 + j * 16 + lcol + r;
-            const float mu = (sred[c] + sred[BN + c]) * inv;
-            float q = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const float d = acc[i][j][r] - mu;
-              if (wm * 128 + i * 16 + lrow < valid) q = fmaf(d, d, q);
-            }
-            q += __shfl_xor(q, 1); q += __shfl_xor(q, 2);
-            q += __shfl_xor(q, 4); q += __shfl_xor(q, 8);
-            if (lrow == 0) sred[2 * BN + wm * BN + c] = q;
-          }
-        }
-        __syncthreads();
-        if (tid < BN) {
-          const float mu = (sred[tid] + sred[BN + tid]) * inv;
-          const float m2 = sred[2 * BN + tid] + sred[3 * BN + tid];
-          chan_merge(run_n, run_mean, run_m2, (float)valid, mu, m2);
-        }
-      }
-      if constexpr (POOL) {
-        int *sredi = reinterpret_cast<int *>(sred);
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float mx = -__builtin_huge_valf(), mn = __builtin_huge_valf();
-            int mxi = 0x7fffffff, mni = 0x7fffffff;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const int m = wm * 128 + i * 16 + lrow;
-              if (m < valid) {
-                const float v = acc[i][j][r];
-                const int g = (int)(row_base + m);
-                if (v > mx) { mx = v; mxi = g; }   // rows visited in increasing order
-                if (v < mn) { mn = v; mni = g; }
-              }
-            }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-              const float omx = __shfl_xor(mx, o), omn = __shfl_xor(mn, o);
-              const int omxi = __shfl_xor(mxi, o), omni = __shfl_xor(mni, o);
-              if (omx > mx || (omx == mx && omxi < mxi)) { mx = omx; mxi = omxi; }
-              if (omn < mn || (omn == mn && omni < mni)) { mn = omn; mni = omni; }
-            }
-            if (lrow == 0) {
-              const int c = wn * 64 + j * 16 + lcol + r;
-              sred[wm * BN + c] = mx;
-              sredi[2 * BN + wm * BN + c] = mxi;
-              sred[4 * BN + wm * BN + c] = mn;
-              sredi[6 * BN + wm * BN + c] = mni;
-            }
-          }
-        }
-        __syncthreads();
-        if (tid < BN) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float mx = sred[h * BN + tid], mn = sred[4 * BN + h * BN + tid];
-            const int mxi = sredi[2 * BN + h * BN + tid], mni = sredi[6 * BN + h * BN + tid];
-            if (mx > run_max || (mx == run_max && mxi < run_maxi)) { run_max = mx; run_maxi = mxi; }
-            if (mn < run_min || (mn == run_min && mni < run_mini)) { run_min = mn; run_mini = mni; }
+          for (int i = 0; i < 8; ++i) {
+            acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
           }
         }
       }
@@ -302,72 +204,15 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       }
     }
     __syncthreads();
-    {
-      float es[EPC], et[EPC], em[EPC], er[EPC];
-      if constexpr (EPI == PCS_EPI_DGRAD) {
-        load_vec<EPC>(a.es, ecol, es); load_vec<EPC>(a.et, ecol, et);
-        load_vec<EPC>(a.emean, ecol, em); load_vec<EPC>(a.erstd, ecol, er);
-      }
-      const bf16_t *Ypg = reinterpret_cast<const bf16_t *>(a.Yp);
-      const bf16_t *Addg = reinterpret_cast<const bf16_t *>(a.addend);
-      for (int rr = er0; rr < valid; rr += RPP) {
-        const int64_t grow = row_base + rr;
-        const int64_t goff = grow * Ncols + ecol;
-        const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
-        if constexpr (EPI == PCS_EPI_DGRAD) {
-          float v[EPC], y[EPC];
-          unpack_chunk(raw, v);
-          if (Addg) {
-            float ad[EPC];
-            unpack_chunk(*reinterpret_cast<const u32x4 *>(Addg + goff), ad);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] += ad[e];
-          }
-          if (a.c_mask) {
-            const uint32_t bits = mask_bits(a.c_mask, grow, Ncols, ecol, EPC);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] *= ((bits >> e) & 1u) ? a.c_keep_scale : 0.f;
-          }
-          unpack_chunk(*reinterpret_cast<const u32x4 *>(Ypg + goff), y);
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? v[e] : 0.f;
-            v[e] = dz;
-            s1[e] += dz;
-            s2[e] = fmaf(dz, (y[e] - em[e]) * er[e], s2[e]);
-          }
-          *reinterpret_cast<u32x4 *>(Cg + goff) = pack_chunk(v);
-        } else {
-          if (Cg) *reinterpret_cast<u32x4 *>(Cg + goff) = raw;
-        }
-      }
+    if (Cg) {
+#pragma unroll 4
+      for (int rr = er0; rr < valid; rr += RPP)
+        *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) =
+            *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
     }
     __syncthreads();
   }
 
-  if (t_begin >= t_end) return;
-  const int64_t chunk_id = (int64_t)scene * cps + cis;
-  if constexpr (EPI == PCS_EPI_FWD) {
-    if (a.stats && tid < BN)
-      *reinterpret_cast<float2 *>(a.stats + (chunk_id * Ncols + n0 + tid) * 2) = make_float2(run_mean, run_m2);
-    if constexpr (POOL) {
-      if (tid < BN)
-        *reinterpret_cast<float4 *>(a.pool + (chunk_id * Ncols + n0 + tid) * 4) =
-            make_float4(run_max, __int_as_float(run_maxi), run_min, __int_as_float(run_mini));
-    }
-  } else if constexpr (EPI == PCS_EPI_DGRAD) {
-    if (a.stats) {
-      float2 *red = reinterpret_cast<float2 *>(lds);  // [RPP][BN]
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) red[er0 * BN + ecc * EPC + e] = make_float2(s1[e], s2[e]);
-      __syncthreads();
-      if (tid < BN) {
-        float a1 = 0.f, a2 = 0.f;
-        for (int j = 0; j < RPP; ++j) { a1 += red[j * BN + tid].x; a2 += red[j * BN + tid].y; }
-        *reinterpret_cast<float2 *>(a.stats + (chunk_id * Ncols + n0 + tid) * 2) = make_float2(a1, a2);
-      }
-    }
-  }
 }
 
 template <int PRO, int EPI, bool POOL>
@@ -384,16 +229,15 @@ int launch(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
 bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 512) return false;
   if (a.flags & PCS_FLAG_GENERIC) return false;
-  if (a.epilogue == PCS_EPI_FWD) return a.prologue == PCS_PRO_BNRELU;
-  if (a.epilogue == PCS_EPI_DGRAD) return a.prologue == PCS_PRO_BWD_POOL || a.prologue == PCS_PRO_BWD;
+  if (a.epilogue == PCS_EPI_FWD)   // statistics / pool: pcs_colstats on the stored output
+    return a.prologue == PCS_PRO_BNRELU && !a.stats && !a.pool && !a.scene_bias;
+  if (a.epilogue == PCS_EPI_RAW) return a.prologue != PCS_PRO_RAW;   // dgrad: pcs_bnrelu_bwd after
   return false;
 }
 
 int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s) {
-  const bool pool = g.pool != nullptr;
-  if (g.epilogue == PCS_EPI_FWD)
-    return pool ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
-                : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
-  if (g.prologue == PCS_PRO_BWD_POOL) return launch<PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
-  return launch<PCS_PRO_BWD, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
+  if (g.epilogue == PCS_EPI_FWD) return launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
+  if (g.prologue == PCS_PRO_BWD_POOL) return launch<PCS_PRO_BWD_POOL, PCS_EPI_RAW, false>(g, tps, tpc, s);
+  if (g.prologue == PCS_PRO_BNRELU) return launch<PCS_PRO_BNRELU, PCS_EPI_RAW, false>(g, tps, tpc, s);
+  return launch<PCS_PRO_BWD, PCS_EPI_RAW, false>(g, tps, tpc, s);
 }

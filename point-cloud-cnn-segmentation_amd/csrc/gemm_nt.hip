@@ -401,6 +401,8 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
     case PCS_EPI_RAW:
       switch (a.prologue) {
         case PCS_PRO_BWD: return launch_t<T, BM, BN, PCS_PRO_BWD, PCS_EPI_RAW, false>(a, tps, tpc, s);
+        case PCS_PRO_BWD_POOL:
+          return launch_t<T, BM, BN, PCS_PRO_BWD_POOL, PCS_EPI_RAW, false>(a, tps, tpc, s);
         case PCS_PRO_BNRELU:
           return launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_RAW, false>(a, tps, tpc, s);
         default: break;

@@ -466,14 +466,19 @@ class Engine:
                    A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
         wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
 
-        # global_feat (dy from the sparse max-pool gradient)
+        # global_feat (dy from the sparse max-pool gradient): raw dgrad GEMM, then the
+        # ReLU/BN5-backward input stage as one streaming pass
         pc5 = sv.bn["bn5"]
-        cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD)
-        st = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
-        self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD, ys["global_feat"],
+        self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_RAW, ys["global_feat"],
                    wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
-                   Yp=ys["conv5"], es=pc5.scale, et=pc5.shift, emean=pc5.mean, erstd=pc5.rstd,
-                   stats=st, tag="dgrad:global_feat")
+                   tag="dgrad:global_feat")
+        cps5 = ct.c_int32(0)
+        rpc5 = L.load().pcs_colstats_geometry(B, N, 1024, ct.byref(cps5))
+        cps5 = cps5.value
+        st = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
+        self._launch("bnrelu_bwd:global_feat", "pcs_bnrelu_bwd", L.ptr(bufB), L.ptr(ys["conv5"]), None, None,
+                     1.0, L.ptr(pc5.scale), L.ptr(pc5.shift), L.ptr(pc5.mean), L.ptr(pc5.rstd), B, N, 1024,
+                     self.dt, cps5, rpc5, L.ptr(st), s)
         keepalive.append(self._wgrad(
             B, N, 1024, 1024, L.PRO_BWD_POOL, L.PRO_BNRELU, G("global_feat.weight"),
             tag="wgrad:global_feat", Y=ys["global_feat"], beta=bg, gamma=gg, pool_idx=sv.am, pool_coef=sp,
