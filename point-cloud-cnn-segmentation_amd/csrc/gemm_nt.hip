@@ -260,58 +260,77 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
       }
       const T *Ypg = reinterpret_cast<const T *>(a.Yp);
       const T *Addg = reinterpret_cast<const T *>(a.addend);
-#pragma unroll 2
-      for (int rr = er0; rr < BM; rr += RPP) {
-        if (rr >= valid) break;
-        const int64_t grow = row_base + rr;
-        const int64_t goff = grow * Ncols + ecol;
-        float v[EPC];
-        unpack_chunk(*reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16), v);
-        if constexpr (EPI == PCS_EPI_FWD) {
-          if (Cg) *reinterpret_cast<u32x4 *>(Cg + goff) =
-              *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
-          if (a.stats) {
-            st_cnt += 1.f;
-            const float rn = 1.f / st_cnt;
+      // BM/RPP rows per thread; the global loads of each batch are issued together so the
+      // epilogue is bandwidth- rather than latency-bound (accumulators are dead here)
+      constexpr int NP = BM / RPP;
+      constexpr int BATCH = NP < 4 ? NP : 4;
 #pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-              const float d = v[e] - st_mean[e];
-              st_mean[e] = fmaf(d, rn, st_mean[e]);
-              st_m2[e] = fmaf(d, v[e] - st_mean[e], st_m2[e]);
+      for (int p0 = 0; p0 < NP; p0 += BATCH) {
+        u32x4 yv[BATCH], adv[BATCH];
+        uint32_t mb[BATCH];
+        if constexpr (EPI == PCS_EPI_DGRAD) {
+#pragma unroll
+          for (int q = 0; q < BATCH; ++q) {
+            const int rr = min(er0 + RPP * (p0 + q), valid - 1);
+            const int64_t goff = (row_base + rr) * Ncols + ecol;
+            yv[q] = *reinterpret_cast<const u32x4 *>(Ypg + goff);
+            adv[q] = Addg ? *reinterpret_cast<const u32x4 *>(Addg + goff) : mk_u32x4(0, 0, 0, 0);
+            mb[q] = a.c_mask ? mask_bits(a.c_mask, row_base + rr, Ncols, ecol, EPC) : 0xffu;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {
+          const int rr = er0 + RPP * (p0 + q);
+          if (rr < valid) {
+            const int64_t grow = row_base + rr;
+            const int64_t goff = grow * Ncols + ecol;
+            const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+            float v[EPC];
+            unpack_chunk(raw, v);
+            if constexpr (EPI == PCS_EPI_FWD) {
+              if (Cg) *reinterpret_cast<u32x4 *>(Cg + goff) = raw;
+              if (a.stats) {
+                st_cnt += 1.f;
+                const float rn = 1.f / st_cnt;
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                  const float d = v[e] - st_mean[e];
+                  st_mean[e] = fmaf(d, rn, st_mean[e]);
+                  st_m2[e] = fmaf(d, v[e] - st_mean[e], st_m2[e]);
+                }
+              }
+              if constexpr (POOL) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                  if (v[e] > pmax[e]) { pmax[e] = v[e]; pmaxi[e] = (int)grow; }
+                  if (v[e] < pmin[e]) { pmin[e] = v[e]; pmini[e] = (int)grow; }
+                }
+              }
+            } else if constexpr (EPI == PCS_EPI_DGRAD) {
+              if (Addg) {
+                float ad[EPC];
+                unpack_chunk(adv[q], ad);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) v[e] += ad[e];
+              }
+              if (a.c_mask) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) v[e] *= ((mb[q] >> e) & 1u) ? a.c_keep_scale : 0.f;
+              }
+              float y[EPC];
+              unpack_chunk(yv[q], y);
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) {
+                const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? v[e] : 0.f;
+                v[e] = dz;
+                st_mean[e] += dz;                                        // S1
+                st_m2[e] = fmaf(dz, (y[e] - em[e]) * er[e], st_m2[e]);   // S2
+              }
+              *reinterpret_cast<u32x4 *>(Cg + goff) = pack_chunk(v);
+            } else {  // RAW
+              *reinterpret_cast<u32x4 *>(Cg + goff) = raw;
             }
           }
-          if constexpr (POOL) {
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-              if (v[e] > pmax[e]) { pmax[e] = v[e]; pmaxi[e] = (int)grow; }
-              if (v[e] < pmin[e]) { pmin[e] = v[e]; pmini[e] = (int)grow; }
-            }
-          }
-        } else if constexpr (EPI == PCS_EPI_DGRAD) {
-          if (Addg) {
-            float ad[EPC];
-            unpack_chunk(*reinterpret_cast<const u32x4 *>(Addg + goff), ad);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] += ad[e];
-          }
-          if (a.c_mask) {
-            const uint32_t bits = mask_bits(a.c_mask, grow, Ncols, ecol, EPC);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] *= ((bits >> e) & 1u) ? a.c_keep_scale : 0.f;
-          }
-          float y[EPC];
-          unpack_chunk(*reinterpret_cast<const u32x4 *>(Ypg + goff), y);
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? v[e] : 0.f;
-            v[e] = dz;
-            st_mean[e] += dz;                                   // S1
-            st_m2[e] = fmaf(dz, (y[e] - em[e]) * er[e], st_m2[e]);  // S2
-          }
-          *reinterpret_cast<u32x4 *>(Cg + goff) = pack_chunk(v);
-        } else {  // RAW
-          *reinterpret_cast<u32x4 *>(Cg + goff) =
-              *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
         }
       }
     }

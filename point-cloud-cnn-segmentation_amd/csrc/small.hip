@@ -517,6 +517,172 @@ __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tile
   }
 }
 
+// Register-resident head for C <= 4 classes: 16 threads per point (one 8-channel bf16 /
+// 4-channel fp32 chunk each; 2 chunks per thread for fp32), logits all-reduced across
+// those 16 lanes by shuffles, seg_conv4 weights, dW/db partials and bn_seg3 S1/S2 kept
+// in registers for the whole chunk, row loads batched.  No LDS in the main loop.
+template <typename T, int C, int MODE>
+__global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, int64_t rows_per_chunk) {
+  constexpr int EPC = Elem<T>::EPC;
+  constexpr int CPT = 8 / EPC;            // chunks per thread (8 channels per thread)
+  constexpr int TPR = HEAD_CIN / 8;       // 16 threads per row
+  constexpr int RPP = THREADS / TPR;      // 16 rows per pass
+  constexpr int BATCH = 4;
+  __shared__ float red[THREADS];
+  const int tid = threadIdx.x, sub = tid % TPR, r0 = tid / TPR, ch0 = sub * 8;
+  const int cps = a.chunks_per_scene;
+  const int scene = blockIdx.x / cps, cis = blockIdx.x % cps;
+  const int64_t N = a.scene_rows;
+  const int64_t lo = (int64_t)cis * rows_per_chunk, hi = pcs_min64(lo + rows_per_chunk, N);
+  const T *Y = reinterpret_cast<const T *>(a.Y);
+  T *dZ = reinterpret_cast<T *>(a.dZ);
+  float s[8], t[8], mu[8], rs[8], w[C][8], bias[C];
+  load_vec<8>(a.s, ch0, s);
+  load_vec<8>(a.t, ch0, t);
+  if constexpr (MODE != PCS_HEAD_FWD) { load_vec<8>(a.mean, ch0, mu); load_vec<8>(a.rstd, ch0, rs); }
+#pragma unroll
+  for (int c = 0; c < C; ++c) { load_vec<8>(a.W + c * HEAD_CIN, ch0, w[c]); bias[c] = a.bias[c]; }
+  float s1[8], s2[8], dw[C][8], db[C], lsum = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    db[c] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dw[c][e] = 0.f;
+  }
+  const float gsc = (MODE == PCS_HEAD_CE && a.wsum) ? 1.f / *a.wsum : 1.f;
+  for (int64_t rb = lo; rb < hi; rb += (int64_t)RPP * BATCH) {
+    u32x4 yv[BATCH][CPT];
+    int64_t lab[BATCH];
+    float dlg[BATCH][C];
+#pragma unroll
+    for (int q = 0; q < BATCH; ++q) {
+      const int64_t r = rb + r0 + RPP * q;
+      const int64_t row = scene * N + (r < hi ? r : hi - 1);
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+        yv[q][k] = *reinterpret_cast<const u32x4 *>(Y + row * HEAD_CIN + ch0 + k * EPC);
+      if constexpr (MODE == PCS_HEAD_CE) lab[q] = a.labels[row];
+      if constexpr (MODE == PCS_HEAD_BWD) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) dlg[q][c] = a.dlogits[row * a.dl_stride_row + c * a.dl_stride_col];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BATCH; ++q) {
+      const int64_t r = rb + r0 + RPP * q;
+      const bool ok = r < hi;
+      const int64_t row = scene * N + (ok ? r : hi - 1);
+      float y[8], av[8];
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        float tmp[EPC];
+        unpack_chunk(yv[q][k], tmp);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) y[k * EPC + e] = tmp[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = fmaxf(fmaf(y[e], s[e], t[e]), 0.f);
+      float lg[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float p = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p = fmaf(av[e], w[c][e], p);
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) p += __shfl_xor(p, o);
+        lg[c] = p + bias[c];
+      }
+      if (ok && a.logits && sub < C) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          if (c == sub) a.logits[row * C + c] = lg[c];
+      }
+      if constexpr (MODE == PCS_HEAD_FWD) continue;
+      float dl[C];
+      if constexpr (MODE == PCS_HEAD_CE) {
+        float mx = lg[0];
+#pragma unroll
+        for (int c = 1; c < C; ++c) mx = fmaxf(mx, lg[c]);
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) se += expf(lg[c] - mx);
+        const float lse = mx + logf(se);
+        const int64_t l = lab[q];
+        const bool valid = ok && l >= 0 && l < C;
+        const float wt = valid ? a.class_weight[l] : 0.f;
+        float zl = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          if (c == l) zl = lg[c];
+          dl[c] = valid ? wt * gsc * (expf(lg[c] - lse) - (c == l ? 1.f : 0.f)) : 0.f;
+        }
+        if (valid && sub == 0) lsum += wt * (lse - zl);
+      } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) dl[c] = ok ? dlg[q][c] : 0.f;
+      }
+      float dz[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float d = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) d = fmaf(dl[c], w[c][e], d);
+        dz[e] = av[e] > 0.f ? d : 0.f;
+        s1[e] += dz[e];
+        s2[e] = fmaf(dz[e], (y[e] - mu[e]) * rs[e], s2[e]);
+#pragma unroll
+        for (int c = 0; c < C; ++c) dw[c][e] = fmaf(dl[c], av[e], dw[c][e]);
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) db[c] += dl[c];
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          float tmp[EPC];
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) tmp[e] = dz[k * EPC + e];
+          *reinterpret_cast<u32x4 *>(dZ + row * HEAD_CIN + ch0 + k * EPC) = pack_chunk(tmp);
+        }
+      }
+    }
+  }
+  if constexpr (MODE != PCS_HEAD_FWD) {
+    // reduce over the RPP threads sharing a channel chunk (same `sub`), one value at a time
+    const int64_t chunk = blockIdx.x;
+    auto reduce_store = [&](float v, float *dst) {
+      red[tid] = v;
+      __syncthreads();
+      if (r0 == 0 && dst) {
+        float acc = 0.f;
+        for (int j = 0; j < RPP; ++j) acc += red[j * TPR + sub];
+        *dst = acc;
+      }
+      __syncthreads();
+    };
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      reduce_store(s1[e], a.stats + (chunk * HEAD_CIN + ch0 + e) * 2);
+      reduce_store(s2[e], a.stats + (chunk * HEAD_CIN + ch0 + e) * 2 + 1);
+    }
+    float *wp = a.wpartial + chunk * (C * HEAD_CIN + C);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) reduce_store(dw[c][e], wp + c * HEAD_CIN + ch0 + e);
+      // every thread of a row holds the same db: sum over rows = over the r0 threads of sub 0
+      reduce_store(db[c], sub == 0 ? wp + C * HEAD_CIN + c : nullptr);
+    }
+    if constexpr (MODE == PCS_HEAD_CE) {
+      const float ls = wave_sum(lsum);
+      if ((tid & 63) == 0) red[tid >> 6] = ls;
+      __syncthreads();
+      if (tid == 0) a.loss_partial[chunk] = red[0] + red[1] + red[2] + red[3];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // misc
 // ---------------------------------------------------------------------------------------
@@ -763,6 +929,10 @@ extern "C" int pcs_pool_bwd(const pcs_pool_bwd_args *ap, pcs_stream_t stream) {
 
 extern "C" int64_t pcs_head_geometry(pcs_head_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_head_geometry", "bad geometry");
+  if (a->num_classes <= 4) {   // register-resident kernel: 64-row granules, ~8 WGs per CU
+    const int64_t tpc = chunk_geo(a->scene_rows, a->num_scenes, 64, &a->chunks_per_scene, 2048);
+    return tpc * 64;
+  }
   const int64_t tpc = chunk_geo(a->scene_rows, a->num_scenes, HEAD_R, &a->chunks_per_scene, 2048);
   return tpc * HEAD_R;
 }
@@ -784,6 +954,29 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
   const int tpc = (int)(rpc / HEAD_R);
   const int nb = (int)(a.num_scenes * a.chunks_per_scene);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a.num_classes <= 4) {
+#define PCS_HS(T, CC, MODE) \
+  hipLaunchKernelGGL((head_small_kernel<T, CC, MODE>), dim3(nb), dim3(THREADS), 0, s, a, rpc)
+#define PCS_HS_C(T, MODE)                                                   \
+  switch (a.num_classes) {                                                 \
+    case 1: PCS_HS(T, 1, MODE); break;                                     \
+    case 2: PCS_HS(T, 2, MODE); break;                                     \
+    case 3: PCS_HS(T, 3, MODE); break;                                     \
+    default: PCS_HS(T, 4, MODE); break;                                    \
+  }
+#define PCS_HS_M(T)                                                          \
+  if (a.mode == PCS_HEAD_FWD) { PCS_HS_C(T, PCS_HEAD_FWD) }                   \
+  else if (a.mode == PCS_HEAD_CE) { PCS_HS_C(T, PCS_HEAD_CE) }                \
+  else { PCS_HS_C(T, PCS_HEAD_BWD) }
+    if (a.dtype == PCS_BF16) { PCS_HS_M(bf16_t) }
+    else if (a.dtype == PCS_F32) { PCS_HS_M(float) }
+    else return pcs_set_einval("pcs_head", "bad dtype");
+#undef PCS_HS_M
+#undef PCS_HS_C
+#undef PCS_HS
+    PCS_CHECK_LAUNCH();
+    return 0;
+  }
 #define PCS_HEAD_LAUNCH(T, MODE) \
   hipLaunchKernelGGL((head_kernel<T, MODE>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc)
   if (a.dtype == PCS_BF16) {
