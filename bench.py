@@ -36,10 +36,31 @@ LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (
               "seg_conv2": (512, 256), "seg_conv3": (256, 128)}
 
 
+# bench tag -> HIP kernel symbol (as summarised from rocprofv3 in profiles/pmc_<round>.json)
+TAG_KERNEL = {
+    "wgrad:global_feat": "wgrad_big_kernel<3>",
+    "fwd:global_feat": "gemm_big_kernel<1, 0, false>",
+    "dgrad:global_feat": "gemm_big_kernel<3, 2, false>",
+    "bnrelu_bwd:global_feat": "bnrelu_bwd_kernel<unsigned short>",
+    "stats:global_feat": "colstats_kernel<unsigned short, true>",
+}
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_r01.json")
+
+
+def pmc_traffic(tag, dtype):
+    """HBM bytes per launch of the kernel behind ``tag`` from the committed PMC summary
+    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/profile_round.sh)."""
+    if dtype != "bf16" or tag not in TAG_KERNEL or not os.path.exists(PMC_FILE):
+        return None
+    with open(PMC_FILE) as f:
+        ent = json.load(f).get(TAG_KERNEL[tag], {})
+    return ent.get("hbm_bytes_per_launch")
+
+
 def kernel_model(tag, M, ab):
     """Algorithmic FLOPs and HBM bytes of one launch (SURVEY.md §8(d) accounting)."""
     kind, conv = tag.split(":", 1)
-    if conv not in LAYER_DIMS:
+    if conv not in LAYER_DIMS or kind not in ("fwd", "dgrad", "wgrad"):
         return None
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
@@ -166,13 +187,15 @@ def main():
                 ach = flops / avg_s / 1e12
                 roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
                         "peak": PEAK[args.dtype]["mfma"], "unit": "TFLOP/s",
-                        "frac": round(ach / PEAK[args.dtype]["mfma"], 4), "traffic": None,
+                        "frac": round(ach / PEAK[args.dtype]["mfma"], 4),
+                        "traffic": pmc_traffic(dom, args.dtype), "algorithmic_bytes": nbytes,
                         "algorithmic_flops": flops, "avg_ms": round(avg_s * 1e3, 4)}
             else:
                 ach = nbytes / avg_s / 1e9
                 roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
                         "peak": PEAK[args.dtype]["hbm"], "unit": "GB/s",
-                        "frac": round(ach / PEAK[args.dtype]["hbm"], 4), "traffic": None,
+                        "frac": round(ach / PEAK[args.dtype]["hbm"], 4),
+                        "traffic": pmc_traffic(dom, args.dtype),
                         "algorithmic_bytes": nbytes, "avg_ms": round(avg_s * 1e3, 4)}
         if rank == 0:
             step_ms = el / args.steps * 1e3
