@@ -16,6 +16,7 @@ _LAZY = {
     "FusedTrainStep": ("train", "FusedTrainStep"),
     "FusedAdam": ("optim", "FusedAdam"),
     "collate_fn": ("data", "collate_fn"),
+    "load_reference_checkpoint": ("model", "load_reference_checkpoint"),
 }
 
 
@@ -24,4 +25,7 @@ def __getattr__(name):
         import importlib
         mod, attr = _LAZY[name]
         return getattr(importlib.import_module(f"{__name__}.{mod}"), attr)
+    if name in ("data", "model", "optim", "train", "engine"):
+        import importlib
+        return importlib.import_module(f"{__name__}.{name}")
     raise AttributeError(name)
