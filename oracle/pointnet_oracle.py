@@ -209,10 +209,12 @@ def forward(sd, x, train=True, masks=None, p=DROPOUT_P, dtype=np.float64):
     return logits.reshape(B, N, -1), cache                  # P:131
 
 
-def cross_entropy(logits, labels, weight, ignore_index=-1):
+def cross_entropy(logits, labels, weight, ignore_index=-1, denom=None):
     """nn.CrossEntropyLoss(weight=w, ignore_index=-1) mean reduction (P:216, P:251).
 
     loss = sum_{y!=-1} w[y] (logsumexp(z) - z[y]) / sum_{y!=-1} w[y]; returns (loss, dlogits).
+    ``denom`` overrides the weight sum: under nn.DataParallel (P:208-211) the loss is taken
+    once over the gathered outputs, so a replica's share uses the GLOBAL weight sum.
     """
     z = logits.reshape(-1, logits.shape[-1])
     y = labels.reshape(-1)
@@ -224,7 +226,8 @@ def cross_entropy(logits, labels, weight, ignore_index=-1):
     lse = (m + np.log(se))[:, 0]
     w = np.where(valid, np.asarray(weight, z.dtype)[ys], 0.0)
     nll = lse - z[np.arange(z.shape[0]), ys]
-    denom = w.sum()
+    if denom is None:
+        denom = w.sum()
     loss = (w * nll).sum() / denom
     sm = e / se
     d = sm.copy()
@@ -357,9 +360,21 @@ def miou(cm):
     return float((tp[present] / denom[present]).mean()) if present.any() else 0.0
 
 
-def train_step(sd, x, labels, weight, masks=None, dtype=np.float64):
-    """One reference training step (P:241-255) without the optimizer: loss, grads, cache."""
+def ce_weight_sum(labels, weight, ignore_index=-1):
+    """sum_{y != ignore} w[y]: the CE denominator of P:216 for one shard."""
+    y = np.asarray(labels).reshape(-1)
+    y = y[y != ignore_index]
+    return float(np.asarray(weight, np.float64)[y].sum())
+
+
+def train_step(sd, x, labels, weight, masks=None, dtype=np.float64, denom=None):
+    """One reference training step (P:241-255) without the optimizer: loss, grads, cache.
+
+    With ``denom`` (the global CE weight sum) this is one DataParallel replica's share:
+    its loss numerator / denom and the gradient of that, computed with the replica's own
+    BatchNorm batch statistics (P:208-211; nn.DataParallel has no SyncBN).
+    """
     logits, cache = forward(sd, x, train=True, masks=masks, dtype=dtype)
-    loss, dl = cross_entropy(logits, labels, weight)
+    loss, dl = cross_entropy(logits, labels, weight, denom=denom)
     grads = backward(sd, cache, dl)
     return loss, logits, grads, cache

@@ -24,6 +24,32 @@ from .engine import BNS
 from .optim import FusedAdam, flat_buffers
 
 
+def _all_reduce(t, group=None):
+    """SUM all-reduce in place.  RCCL ("nccl") reduces device tensors directly; a gloo group
+    (CPU rendezvous, e.g. several ranks sharing one device in tests) is staged through host
+    memory."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+
+
+def allreduce_ce_denominator(wsum, group=None):
+    """Sum the per-rank CE weight sums (wsum[0]) and valid counts (wsum[1]) in place so every
+    rank normalises by the global denominator (DataParallel's single gathered loss, P:251)."""
+    _all_reduce(wsum[:2], group)
+
+
+def allreduce_gradients(gflat, loss_num, group=None):
+    """Sum the flat gradient buffer and the loss numerator over ranks (DataParallel's
+    reduce-add of replica gradients into the base module, P:208-211, P:254).  One flat
+    buffer (7.7 MB) -> one collective; RCCL over xGMI moves it in ~0.1 ms."""
+    _all_reduce(gflat, group)
+    _all_reduce(loss_num, group)
+
+
 class FusedTrainStep:
     def __init__(self, model, optimizer: FusedAdam | None = None, class_weight=None,
                  process_group=None, lr=1e-3, weight_decay=1e-4):
@@ -57,7 +83,7 @@ class FusedTrainStep:
         L.call("pcs_ce_weight_sum", L.ptr(labels), labels.numel(), L.ptr(self.class_weight),
                model.num_classes, L.ptr(self.counts), L.ptr(self.wsum), s)
         if self._distributed():
-            dist.all_reduce(self.wsum[:2], group=self.pg)   # global CE denominator
+            allreduce_ce_denominator(self.wsum, self.pg)
         if seed is None:
             seed = model._next_seed()
         sv = eng.forward(P, bufs, points, train=True, masks=masks, seed=seed,
@@ -70,7 +96,6 @@ class FusedTrainStep:
                L.ptr(self.loss_num), 1, 1, s)
         del sv, hb
         if self._distributed():
-            dist.all_reduce(gflat, group=self.pg)
-            dist.all_reduce(self.loss_num, group=self.pg)
+            allreduce_gradients(gflat, self.loss_num, self.pg)
         self.opt.step()
         return self.loss_num / self.wsum[0]

@@ -117,19 +117,80 @@ def make_case(ref, name, *, C, n_points, seed, train, bn_rand, dropout, grid=32)
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
 
 
-def main():
+def make_dp_case(ref, name, *, C, n_points, seed, world, bn_rand=False):
+    """nn.DataParallel semantics (P:208-211), emulated on CPU with the reference module:
+    the padded batch is chunked over ``world`` replicas (scatter = tensor.chunk), each
+    replica runs forward on its scenes with its own BatchNorm batch statistics, outputs are
+    gathered and ONE loss is taken over all of them (P:251), replica gradients are
+    reduce-added into the base module, and Adam steps the base.  Replica 0 shares the base
+    module's buffers (DataParallel's guarantee), so the running stats are replica 0's."""
+    import copy
+    sd = orc.init_params(C, seed, bn_affine_random=bn_rand)
+    pts, lab, msk = pdata.synthetic_batch(seed + 1, n_points, C, grid=32)
+    B, N, _ = pts.shape
+    masks = orc.dropout_masks(seed + 2, B * N)
+    base = ref.PointNetSegmentation(num_classes=C)
+    base.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in sd.items()})
+    base.train()
+    replicas = [base] + [copy.deepcopy(base) for _ in range(world - 1)]
+    weight = pdata.class_weights([lab[b][msk[b]] for b in range(B)], num_classes=C)
+    outs = []
+    for r, mod in enumerate(replicas):
+        lo, hi = pdata.shard_bounds(B, r, world)
+        rows = slice(lo * N, hi * N)
+        mod.dropout = ReplayDropout((masks[0][rows], masks[1][rows]))
+        outs.append(mod(torch.from_numpy(pts[lo:hi])))
+    logits = torch.cat(outs, 0)
+    crit = torch.nn.CrossEntropyLoss(ignore_index=-1, weight=torch.tensor(weight))
+    loss = crit(logits.contiguous().view(-1, C), torch.from_numpy(lab).view(-1))
+    loss.backward()
+    for mod in replicas[1:]:
+        for pb, pr in zip(base.parameters(), mod.parameters()):
+            pb.grad += pr.grad
+    out = {"C": C, "seed": seed, "n_points": np.array(n_points), "train": 1, "world": world,
+           "bn_rand": int(bn_rand), "dropout": 1, "grid": 32, "weight": np.array(weight, np.float32),
+           "logits": logits.detach().contiguous().numpy(), "loss": np.float64(loss.item())}
+    names = [n for n, _ in base.named_parameters()]
+    out["param_names"] = np.array(names)
+    for i, (n, p) in enumerate(base.named_parameters()):
+        g = p.grad.detach().numpy().reshape(-1)
+        idx = sample_idx(1000 + i, g.size)
+        out[f"gnorm/{n}"] = np.float64(np.linalg.norm(g.astype(np.float64)))
+        out[f"gidx/{n}"] = idx
+        out[f"gval/{n}"] = g[idx]
+    opt = torch.optim.Adam(base.parameters(), lr=1e-3, weight_decay=1e-4)
+    opt.step()
+    for n, p in base.named_parameters():
+        out[f"pval/{n}"] = p.detach().numpy().reshape(-1)[out[f"gidx/{n}"]]
+    for k, v in base.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            out[f"buf/{k}"] = v.numpy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+
+
+def main(only=()):
     torch.set_num_threads(8)
     ref = load_reference()
-    make_case(ref, "eval_c2_bnrand", C=2, n_points=[512, 512], seed=11, train=False,
-              bn_rand=True, dropout=False)
-    make_case(ref, "train_c2", C=2, n_points=[1024] * 4, seed=21, train=True,
-              bn_rand=False, dropout=True)
-    make_case(ref, "train_c3_ragged_bnrand", C=3, n_points=[600, 1024, 401, 800], seed=31,
-              train=True, bn_rand=True, dropout=True)
-    make_case(ref, "train_c2_nodrop_small", C=2, n_points=[300, 300], seed=41, train=True,
-              bn_rand=False, dropout=False)
+    cases = {
+        "eval_c2_bnrand": lambda: make_case(ref, "eval_c2_bnrand", C=2, n_points=[512, 512],
+                                            seed=11, train=False, bn_rand=True, dropout=False),
+        "train_c2": lambda: make_case(ref, "train_c2", C=2, n_points=[1024] * 4, seed=21,
+                                      train=True, bn_rand=False, dropout=True),
+        "train_c3_ragged_bnrand": lambda: make_case(ref, "train_c3_ragged_bnrand", C=3,
+                                                    n_points=[600, 1024, 401, 800], seed=31,
+                                                    train=True, bn_rand=True, dropout=True),
+        "train_c2_nodrop_small": lambda: make_case(ref, "train_c2_nodrop_small", C=2,
+                                                   n_points=[300, 300], seed=41, train=True,
+                                                   bn_rand=False, dropout=False),
+        "train_c3_dp2": lambda: make_dp_case(ref, "train_c3_dp2", C=3,
+                                             n_points=[700, 1024, 512, 900], seed=51, world=2,
+                                             bn_rand=True),
+    }
+    for name, fn in cases.items():
+        if not only or name in only:
+            fn()
     print("golden vectors written to", OUT)
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))     # optionally: names of the cases to (re)generate
