@@ -84,6 +84,13 @@ PCS_DEV uint32_t mask_bits(const uint8_t *__restrict__ bits, int64_t row, int K,
   return n == 8 ? byte : ((byte >> (k & 7)) & 0xFu);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, then
+// s_barrier.  Unlike __syncthreads() (a workgroup-scope fence) it never waits on vmcnt, so
+// global loads issued for a later pipeline stage stay in flight across it (spill stores
+// would otherwise make the fence drain them).  One asm statement with a "memory" clobber:
+// the compiler moves no memory access across it.
+PCS_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // wave-level helpers (wave64)
 PCS_DEV float wave_sum(float v) {
 #pragma unroll

@@ -20,15 +20,16 @@ namespace {
 
 constexpr int THREADS = 512;
 constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int KMAX = 1024;                   // per-channel coefficient arrays live in LDS
 constexpr int ROWB = BK * 2;                 // 128 B per LDS row
 constexpr int STAGE = (BM + BN) * ROWB;      // 64 KB
 constexpr int CROW = BN * 2 + 16;            // epilogue tile row stride
-constexpr int CTILE = BM * CROW;             // 135 KB
+constexpr int CTILE = BM * CROW;             // 132 KB
 constexpr int CPR = BN * 2 / 16;             // 32 chunks per output row
 constexpr int RPP = THREADS / CPR;           // 16 rows per pass
 constexpr int LDS_MAIN = (2 * STAGE > CTILE) ? 2 * STAGE : CTILE;
-constexpr int SRED = 4 * 2 * BN * 4;         // small cross-wave reduction area (16 KB)
-constexpr int LDS_BYTES = LDS_MAIN + SRED;
+constexpr int COEF = 4 * KMAX * 4;           // up to 4 per-channel arrays (16 KB)
+constexpr int LDS_BYTES = LDS_MAIN + COEF + 32;   // + per-tile argmax-row bitmap (256 bits)
 
 PCS_DEV int swz8(int row, int slot) { return slot ^ ((row >> 1) & 7); }
 
@@ -37,14 +38,26 @@ PCS_DEV int xcd_remap(int bid, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
-PCS_DEV float round_bf16(float v) { return bf2f(pack2bf(v, 0.f) & 0xffffu); }
+PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4 *>(p);
+  const float4 b = *reinterpret_cast<const float4 *>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 
-template <int PRO, int EPI, bool POOL>
+// Pipeline (one LDS double buffer, one register stage, one barrier per 64-deep k-step):
+//   compute(ks) from LDS[ks&1]  ->  transform + write the registers (k-step ks+1) into
+//   LDS[(ks+1)&1]  ->  issue the global loads of k-step ks+2  ->  barrier.
+// Each load has a full MFMA block to land; the per-channel prologue coefficients come from
+// LDS (staged once per workgroup: a workgroup's row chunk never leaves its scene), and rows
+// past the end of a scene are clamped rather than branched around (their outputs are never
+// stored), so the k-loop carries no exec-mask branches and no early vmcnt(0).
+template <int PRO, int EPI, bool MASK>
 __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                            int tiles_per_chunk, int ncb) {
   constexpr int EPC = 8;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  float *sred = reinterpret_cast<float *>(lds + LDS_MAIN);
+  float *cf = reinterpret_cast<float *>(lds + LDS_MAIN);
+  uint32_t *tbits = reinterpret_cast<uint32_t *>(lds + LDS_MAIN + COEF);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -58,88 +71,118 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   const int t_begin = cis * tiles_per_chunk;
   const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
   const int nks = K / BK;
+  if (t_begin >= t_end) return;
 
   const bf16_t *__restrict__ Ag = reinterpret_cast<const bf16_t *>(a.A);
   const bf16_t *__restrict__ A2g = reinterpret_cast<const bf16_t *>(a.A2);
   const bf16_t *__restrict__ Wg = reinterpret_cast<const bf16_t *>(a.W);
   bf16_t *__restrict__ Cg = reinterpret_cast<bf16_t *>(a.C);
 
-  const int slot = tid & 7, srow = tid >> 3;  // staging: rows srow + 64*i, fixed k-slot
+  // per-channel prologue coefficients -> LDS: c0 | c1 | c2 | pool argmax rows
+  for (int k = tid; k < K; k += THREADS) {
+    if constexpr (PRO == PCS_PRO_BNRELU) {
+      cf[k] = a.pa[k]; cf[KMAX + k] = a.pb[k];
+    } else if constexpr (PRO == PCS_PRO_BWD) {
+      cf[k] = a.pa[k]; cf[KMAX + k] = a.pb[k]; cf[2 * KMAX + k] = a.pc[k];
+    } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+      cf[k] = a.pool_coef[(int64_t)scene * K + k]; cf[KMAX + k] = a.pb[k];
+      cf[2 * KMAX + k] = a.pc[k];
+      reinterpret_cast<int *>(cf)[3 * KMAX + k] = a.pool_idx[(int64_t)scene * K + k];
+    }
+  }
 
+  const int slot = tid & 7, srow = tid >> 3;  // staging: rows srow + 64*i, fixed k-slot
   const int ecc = tid % CPR, er0 = tid / CPR, ecol = n0 + ecc * EPC;
+  const int lrow = lane & 15, lcol = 4 * (lane >> 4);
+
+  u32x4 ra[4], ra2[4], rb[4];
+  uint32_t mk[4];
+  uint32_t hits = 0;   // POOL: bit i set if staging row srow + 64 i is an argmax row of the tile
+  auto load_stage = [&](int64_t row_base, int valid, int ks) {
+    const int k0 = ks * BK + slot * EPC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(srow + 64 * i, valid - 1);
+      const int64_t off = (row_base + r) * K + k0;
+      ra[i] = *reinterpret_cast<const u32x4 *>(Ag + off);
+      if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const u32x4 *>(A2g + off);
+      if constexpr (MASK) mk[i] = a.a_mask[off >> 3];
+      rb[i] = *reinterpret_cast<const u32x4 *>(Wg + (int64_t)(n0 + srow + 64 * i) * K + k0);
+    }
+  };
+  auto store_stage = [&](int64_t row_base, int ks, int buf) {
+    char *tA = lds + buf * STAGE;
+    char *tB = tA + BM * ROWB;
+    const int k0 = ks * BK + slot * EPC;
+    float c0[EPC], c1[EPC], c2[EPC];
+    if constexpr (PRO == PCS_PRO_BNRELU) {
+      lds_vec8(cf + k0, c0); lds_vec8(cf + KMAX + k0, c1);
+    } else if constexpr (PRO == PCS_PRO_BWD) {
+      lds_vec8(cf + k0, c0); lds_vec8(cf + KMAX + k0, c1); lds_vec8(cf + 2 * KMAX + k0, c2);
+    } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+      lds_vec8(cf + KMAX + k0, c1); lds_vec8(cf + 2 * KMAX + k0, c2);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow + 64 * i;
+      float v[EPC];
+      unpack_chunk(ra[i], v);
+      if constexpr (PRO == PCS_PRO_BNRELU) {
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+          if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
+          v[e] = x;
+        }
+      } else if constexpr (PRO == PCS_PRO_BWD) {
+        float y[EPC];
+        unpack_chunk(ra2[i], y);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v[e] = fmaf(c0[e], v[e], fmaf(c2[e], y[e], c1[e]));
+      } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v[e] = fmaf(c2[e], v[e], c1[e]);
+        if ((hits >> i) & 1u) {   // rare: this row is the max-pool argmax of some channel
+          const int grow = (int)(row_base + r);
+          const int *am = reinterpret_cast<const int *>(cf + 3 * KMAX);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) v[e] += am[k0 + e] == grow ? cf[k0 + e] : 0.f;
+        }
+      }
+      const u32x4 out = (PRO == PCS_PRO_RAW) ? ra[i] : pack_chunk(v);
+      *reinterpret_cast<u32x4 *>(tA + r * ROWB + swz8(r, slot) * 16) = out;
+      *reinterpret_cast<u32x4 *>(tB + r * ROWB + swz8(r, slot) * 16) = rb[i];
+    }
+  };
+
+  auto tile_rows = [&](int tile) { return (int)pcs_min64(BM, N - (int64_t)tile * BM); };
+
+  int64_t row_base = scene * N + (int64_t)t_begin * BM;
+  int valid = tile_rows(t_begin);
+  load_stage(row_base, valid, 0);
+  __syncthreads();   // coefficients visible
 
   for (int tile = t_begin; tile < t_end; ++tile) {
-    const int64_t row_base = scene * N + (int64_t)tile * BM;
-    const int valid = (int)pcs_min64(BM, N - (int64_t)tile * BM);
-
-    u32x4 ra[4], ra2[4], rb[4];
-    auto load_stage = [&](int ks) {
-      const int k0 = ks * BK + slot * EPC;
+    if constexpr (PRO == PCS_PRO_BWD_POOL) {   // bitmap of the tile's argmax rows
+      if (tid < BM / 32) tbits[tid] = 0u;
+      __syncthreads();
+      const int *am = reinterpret_cast<const int *>(cf + 3 * KMAX);
+      for (int c = tid; c < K; c += THREADS) {
+        const int64_t m = (int64_t)am[c] - row_base;
+        if (m >= 0 && m < valid) atomicOr(&tbits[m >> 5], 1u << (m & 31));
+      }
+      __syncthreads();
+      hits = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = srow + 64 * i;
-        if (r < valid) {
-          const int64_t off = (row_base + r) * K + k0;
-          ra[i] = *reinterpret_cast<const u32x4 *>(Ag + off);
-          if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const u32x4 *>(A2g + off);
-        }
-        rb[i] = *reinterpret_cast<const u32x4 *>(Wg + (int64_t)(n0 + r) * K + k0);
+        hits |= ((tbits[r >> 5] >> (r & 31)) & 1u) << i;
       }
-    };
-    auto store_stage = [&](int ks, int buf) {
-      char *tA = lds + buf * STAGE;
-      char *tB = tA + BM * ROWB;
-      const int k0 = ks * BK + slot * EPC;
-      float c0[EPC], c1[EPC], c2[EPC];
-      int am[EPC];
-      if constexpr (PRO == PCS_PRO_BNRELU) {
-        load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1);
-      } else if constexpr (PRO == PCS_PRO_BWD) {
-        load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
-      } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
-        load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
-        load_vec<EPC>(a.pool_coef + scene * K, k0, c0);
-        const int4 i0 = *reinterpret_cast<const int4 *>(a.pool_idx + scene * K + k0);
-        const int4 i1 = *reinterpret_cast<const int4 *>(a.pool_idx + scene * K + k0 + 4);
-        am[0] = i0.x; am[1] = i0.y; am[2] = i0.z; am[3] = i0.w;
-        am[4] = i1.x; am[5] = i1.y; am[6] = i1.z; am[7] = i1.w;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = srow + 64 * i;
-        u32x4 out = mk_u32x4(0, 0, 0, 0);
-        if (r < valid) {
-          float v[EPC];
-          unpack_chunk(ra[i], v);
-          if constexpr (PRO == PCS_PRO_BNRELU) {
-            uint32_t bits = 0xffu;
-            if (a.a_mask) bits = mask_bits(a.a_mask, row_base + r, K, k0, EPC);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-              float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
-              if (a.a_mask) x *= ((bits >> e) & 1u) ? a.a_keep_scale : 0.f;
-              v[e] = x;
-            }
-          } else if constexpr (PRO == PCS_PRO_BWD) {
-            float y[EPC];
-            unpack_chunk(ra2[i], y);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) v[e] = fmaf(c0[e], v[e], fmaf(c2[e], y[e], c1[e]));
-          } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
-            const int grow = (int)(row_base + r);
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) {
-              float x = fmaf(c2[e], v[e], c1[e]);
-              if (am[e] == grow) x += c0[e];
-              v[e] = x;
-            }
-          }
-          out = pack_chunk(v);
-        }
-        *reinterpret_cast<u32x4 *>(tA + r * ROWB + swz8(r, slot) * 16) = out;
-        *reinterpret_cast<u32x4 *>(tB + r * ROWB + swz8(r, slot) * 16) = rb[i];
-      }
-    };
+    }
+    store_stage(row_base, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_stage(row_base, valid, 1);   // nks >= 8 (K >= 512)
+    lds_barrier();
 
     f32x4 acc[8][4];
 #pragma unroll
@@ -147,12 +190,10 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    load_stage(0);
-    store_stage(0, 0);
-    __syncthreads();
+    const int64_t next_base = row_base + BM;
+    const int next_valid = (tile + 1 < t_end) ? tile_rows(tile + 1) : 0;
     for (int ks = 0; ks < nks; ++ks) {
       const int buf = ks & 1;
-      if (ks + 1 < nks) load_stage(ks + 1);
       const char *tA = lds + buf * STAGE;
       const char *tB = tA + BM * ROWB;
 #pragma unroll
@@ -173,12 +214,21 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
         }
       }
-      if (ks + 1 < nks) store_stage(ks + 1, buf ^ 1);
-      __syncthreads();
+      if (ks + 1 < nks) {
+        store_stage(row_base, ks + 1, buf ^ 1);
+        __builtin_amdgcn_sched_barrier(0);   // keep one staging register set live, not two
+        // ONE load site (two sites make the compiler merge their registers with copies that
+        // wait for the loads): k-step ks+2 of this tile, else step 0 of the next tile, else
+        // a harmless in-bounds reload that is never consumed.
+        const bool tail = ks + 2 >= nks;
+        const bool has_next = next_valid > 0;
+        load_stage(tail && has_next ? next_base : row_base, tail && has_next ? next_valid : valid,
+                   tail ? 0 : ks + 2);
+      }
+      lds_barrier();
     }
 
     // lane owns rows m = wm*128 + i*16 + (lane&15), cols n = wn*64 + j*16 + 4*(lane>>4) + r
-    const int lrow = lane & 15, lcol = 4 * (lane >> 4);
     if constexpr (EPI == PCS_EPI_FWD) {
       if (a.bias) {
 #pragma unroll
@@ -211,15 +261,16 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
             *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
     }
     __syncthreads();
+    row_base = next_base;
+    valid = next_valid;
   }
-
 }
 
-template <int PRO, int EPI, bool POOL>
+template <int PRO, int EPI, bool MASK>
 int launch(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
   const int ncb = a.Ncols / BN;
   const int nb = ncb * (int)(a.num_scenes * a.chunks_per_scene);
-  hipLaunchKernelGGL((gemm_big_kernel<PRO, EPI, POOL>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc, ncb);
+  hipLaunchKernelGGL((gemm_big_kernel<PRO, EPI, MASK>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc, ncb);
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -227,7 +278,8 @@ int launch(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
 }  // namespace
 
 bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
-  if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 512) return false;
+  if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 512 || a.K > KMAX) return false;
+  if (a.a_mask && a.prologue != PCS_PRO_BNRELU) return false;
   if (a.flags & PCS_FLAG_GENERIC) return false;
   if (a.epilogue == PCS_EPI_FWD)   // statistics / pool: pcs_colstats on the stored output
     return a.prologue == PCS_PRO_BNRELU && !a.stats && !a.pool && !a.scene_bias;
@@ -236,8 +288,12 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
 }
 
 int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s) {
-  if (g.epilogue == PCS_EPI_FWD) return launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
+  if (g.epilogue == PCS_EPI_FWD)
+    return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
+                    : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
   if (g.prologue == PCS_PRO_BWD_POOL) return launch<PCS_PRO_BWD_POOL, PCS_EPI_RAW, false>(g, tps, tpc, s);
-  if (g.prologue == PCS_PRO_BNRELU) return launch<PCS_PRO_BNRELU, PCS_EPI_RAW, false>(g, tps, tpc, s);
+  if (g.prologue == PCS_PRO_BNRELU)
+    return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_RAW, true>(g, tps, tpc, s)
+                    : launch<PCS_PRO_BNRELU, PCS_EPI_RAW, false>(g, tps, tpc, s);
   return launch<PCS_PRO_BWD, PCS_EPI_RAW, false>(g, tps, tpc, s);
 }

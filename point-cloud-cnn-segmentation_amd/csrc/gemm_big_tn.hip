@@ -18,6 +18,8 @@ constexpr int TM = 256, TN = 256, MS = 64;
 constexpr int ROWB = TM * 2 + 32;          // 544 B: padded LDS row
 constexpr int OPB = MS * ROWB;             // one operand tile (34 KB)
 constexpr int STAGE = 2 * OPB;
+constexpr int COEF = 6 * 256 * 4;          // alpha|beta|gamma|argmax (Cout cols), s|t (Cin cols)
+constexpr int LDS_BYTES = 2 * STAGE + COEF;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -37,39 +39,49 @@ PCS_DEV bf16x8 tr_frag(const char *tile, int r0, int r1, int col) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int DYMODE>
+template <int DYMODE, bool MASK>
 PCS_DEV void tn_load(const bf16_t *__restrict__ dZ, const bf16_t *__restrict__ Yg,
-                     const bf16_t *__restrict__ Xg, int64_t rbase, int64_t rlast, int Cout, int Cin,
-                     int an, int bk, int r0, u32x4 (&rz)[4], u32x4 (&ry)[4], u32x4 (&rx)[4]) {
+                     const bf16_t *__restrict__ Xg, const uint8_t *__restrict__ xmask, int64_t rbase,
+                     int64_t rlast, int Cout, int Cin, int an, int bk, int r0, u32x4 (&rz)[4],
+                     u32x4 (&ry)[4], u32x4 (&rx)[4], uint32_t (&mk)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t r = rbase + r0 + 16 * i < rlast ? rbase + r0 + 16 * i : rlast - 1;
     if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + r * Cout + an);
     ry[i] = *reinterpret_cast<const u32x4 *>(Yg + r * Cout + an);
     rx[i] = *reinterpret_cast<const u32x4 *>(Xg + r * Cin + bk);
+    if constexpr (MASK) mk[i] = xmask[(r * Cin + bk) >> 3];
   }
 }
 
-template <int DYMODE>
-PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, int scene, int64_t rbase, int64_t rlast,
-                      int an, int bk, int cc, int r0, const u32x4 (&rz)[4], const u32x4 (&ry)[4],
-                      const u32x4 (&rx)[4]) {
+PCS_DEV void lds8(const float *p, float (&v)[8]) {
+  const float4 x = *reinterpret_cast<const float4 *>(p);
+  const float4 y = *reinterpret_cast<const float4 *>(p + 4);
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
+
+// Transform one staged 64-row step (dy and x) and write it to LDS.  Coefficients come from
+// the workgroup's LDS copy (cf: [alpha|pool coef][beta][gamma][argmax] over its 256 Cout
+// columns, [s][t] over its 256 Cin columns); rows past the slice end are written as zeros.
+template <int DYMODE, bool MASK>
+PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_t rbase, int64_t rlast,
+                      int bk, int cc, int r0, const u32x4 (&rz)[4], const u32x4 (&ry)[4],
+                      const u32x4 (&rx)[4], const uint32_t (&mk)[4]) {
   char *tB = tA + OPB;
   float ca[8], cb[8], cg[8], xs[8], xt[8];
   int am[8];
-  load_vec<8>(a.beta, an, cb);
-  load_vec<8>(a.gamma, an, cg);
-  if constexpr (DYMODE == PCS_PRO_BWD) {
-    load_vec<8>(a.alpha, an, ca);
-  } else {
-    load_vec<8>(a.pool_coef + scene * a.Cout, an, ca);
-    const int4 i0 = *reinterpret_cast<const int4 *>(a.pool_idx + scene * a.Cout + an);
-    const int4 i1 = *reinterpret_cast<const int4 *>(a.pool_idx + scene * a.Cout + an + 4);
+  const int c8 = cc * 8;
+  lds8(cf + c8, ca);
+  lds8(cf + 256 + c8, cb);
+  lds8(cf + 512 + c8, cg);
+  if constexpr (DYMODE == PCS_PRO_BWD_POOL) {
+    const int4 i0 = *reinterpret_cast<const int4 *>(cf + 768 + c8);
+    const int4 i1 = *reinterpret_cast<const int4 *>(cf + 768 + c8 + 4);
     am[0] = i0.x; am[1] = i0.y; am[2] = i0.z; am[3] = i0.w;
     am[4] = i1.x; am[5] = i1.y; am[6] = i1.z; am[7] = i1.w;
   }
-  load_vec<8>(a.s, bk, xs);
-  load_vec<8>(a.t, bk, xt);
+  lds8(cf + 1024 + c8, xs);
+  lds8(cf + 1280 + c8, xt);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rl = r0 + 16 * i;
@@ -94,12 +106,10 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, int scene, int64_t rbas
     *reinterpret_cast<u32x4 *>(tA + prow(rl) * ROWB + cc * 16) = o;
     float w[8];
     unpack_chunk(rx[i], w);
-    uint32_t bits = 0xffu;
-    if (a.x_mask) bits = mask_bits(a.x_mask, ok ? r : rlast - 1, a.Cin, bk, 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float x = fmaxf(fmaf(w[e], xs[e], xt[e]), 0.f);
-      if (a.x_mask) x *= ((bits >> e) & 1u) ? a.x_keep_scale : 0.f;
+      if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.x_keep_scale : 0.f;
       w[e] = x;
     }
     u32x4 ox = pack_chunk(w);
@@ -108,10 +118,11 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, int scene, int64_t rbas
   }
 }
 
-template <int DYMODE>
+template <int DYMODE, bool MASK>
 __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, int64_t rows_per_split,
                                                             int ntn, int ntiles) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  float *cf = reinterpret_cast<float *>(lds + 2 * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -129,6 +140,19 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
   const bf16_t *Xg = reinterpret_cast<const bf16_t *>(a.X);
   const int cc = tid & 31, r0 = tid >> 5;   // staging: fixed 8-column chunk, rows r0 + 16 i
   const int an = n0 + cc * 8, bk = k0 + cc * 8;
+  for (int c = tid; c < 256; c += THREADS) {
+    if constexpr (DYMODE == PCS_PRO_BWD) {
+      cf[c] = a.alpha[n0 + c];
+    } else {
+      cf[c] = a.pool_coef[(int64_t)scene * Cout + n0 + c];
+      reinterpret_cast<int *>(cf)[768 + c] = a.pool_idx[(int64_t)scene * Cout + n0 + c];
+    }
+    cf[256 + c] = a.beta[n0 + c];
+    cf[512 + c] = a.gamma[n0 + c];
+    cf[1024 + c] = a.s[k0 + c];
+    cf[1280 + c] = a.t[k0 + c];
+  }
+  __syncthreads();
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -138,17 +162,19 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
 
   const int nsteps = (int)((hi - lo + MS - 1) / MS);
   u32x4 rz[4], ry[4], rx[4];
+  uint32_t mk[4] = {0xffu, 0xffu, 0xffu, 0xffu};
   if (nsteps > 0) {
     const int64_t rb = scene * N + lo;
-    tn_load<DYMODE>(dZ, Yg, Xg, rb, rlast, Cout, Cin, an, bk, r0, rz, ry, rx);
-    tn_store<DYMODE>(a, lds, scene, rb, rlast, an, bk, cc, r0, rz, ry, rx);
+    tn_load<DYMODE, MASK>(dZ, Yg, Xg, a.x_mask, rb, rlast, Cout, Cin, an, bk, r0, rz, ry, rx, mk);
+    tn_store<DYMODE, MASK>(a, lds, cf, rb, rlast, bk, cc, r0, rz, ry, rx, mk);
     __syncthreads();
   }
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   for (int st = 0; st < nsteps; ++st) {
     const int buf = st & 1;
     const int64_t rb = scene * N + lo + (int64_t)st * MS;
-    if (st + 1 < nsteps) tn_load<DYMODE>(dZ, Yg, Xg, rb + MS, rlast, Cout, Cin, an, bk, r0, rz, ry, rx);
+    if (st + 1 < nsteps)
+      tn_load<DYMODE, MASK>(dZ, Yg, Xg, a.x_mask, rb + MS, rlast, Cout, Cin, an, bk, r0, rz, ry, rx, mk);
     const char *tA = lds + buf * STAGE;
     const char *tB = tA + OPB;
 #pragma unroll
@@ -166,8 +192,8 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
       }
     }
     if (st + 1 < nsteps)
-      tn_store<DYMODE>(a, lds + (buf ^ 1) * STAGE, scene, rb + MS, rlast, an, bk, cc, r0, rz, ry, rx);
-    __syncthreads();
+      tn_store<DYMODE, MASK>(a, lds + (buf ^ 1) * STAGE, cf, rb + MS, rlast, bk, cc, r0, rz, ry, rx, mk);
+    lds_barrier();
   }
   // lane holds dW[n = n0 + wm*128 + i*16 + (lane&15)][k = k0 + wn*64 + j*16 + 4*(lane>>4) + r]
   float *out = a.partial + (int64_t)split * Cout * Cin;
@@ -204,10 +230,13 @@ int pcs_wgrad_big_launch(const pcs_wgrad_args &a, hipStream_t s) {
   rps = (rps + MS - 1) / MS * MS;
   const int ntn = a.Cin / TN, ntiles = (a.Cout / TM) * ntn;
   const int nb = ntiles * (int)(a.num_scenes * a.splits_per_scene);
-  if (a.dy_mode == PCS_PRO_BWD_POOL)
-    hipLaunchKernelGGL(wgrad_big_kernel<PCS_PRO_BWD_POOL>, dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
-  else
-    hipLaunchKernelGGL(wgrad_big_kernel<PCS_PRO_BWD>, dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  if (a.dy_mode == PCS_PRO_BWD_POOL) {
+    if (a.x_mask) hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD_POOL, true>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+    else hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD_POOL, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  } else {
+    if (a.x_mask) hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD, true>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+    else hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  }
   PCS_CHECK_LAUNCH();
   return 0;
 }
