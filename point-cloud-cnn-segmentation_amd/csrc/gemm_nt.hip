@@ -57,38 +57,57 @@ PCS_DEV int xcd_remap(int bid, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
-// Staging of one k-step: global -> registers (issued early) ...
-template <typename T, int BM, int BN, int PRO>
-PCS_DEV void nt_load(const T *__restrict__ Ag, const T *__restrict__ A2g, const T *__restrict__ Wg,
-                     int64_t row_base, int valid, int K, int n0, int k0, int srow,
-                     u32x4 (&ra)[BM / 64], u32x4 (&ra2)[BM / 64], u32x4 (&rb)[BN / 64]) {
+constexpr int KMAX = 1024;   // prologue coefficient arrays staged in LDS (K <= KMAX)
+
+template <int PRO> struct Coef {   // per-channel prologue arrays kept in LDS
+  static constexpr int N = PRO == PCS_PRO_BNRELU ? 2 : PRO == PCS_PRO_BWD ? 3 : PRO == PCS_PRO_BWD_POOL ? 4 : 0;
+};
+
+template <int EPC>
+PCS_DEV void lds_vec(const float *p, float (&v)[EPC]) {
+#pragma unroll
+  for (int e = 0; e < EPC; e += 4) {
+    const float4 q = *reinterpret_cast<const float4 *>(p + e);
+    v[e] = q.x; v[e + 1] = q.y; v[e + 2] = q.z; v[e + 3] = q.w;
+  }
+}
+
+// Staging of one k-step: global -> registers (issued one k-step ahead) ...
+template <typename T, int BM, int BN, int PRO, bool MASK>
+PCS_DEV void nt_load(const pcs_gemm_args &a, const T *__restrict__ Ag, const T *__restrict__ A2g,
+                     const T *__restrict__ Wg, int64_t row_base, int valid, int K, int n0, int k0,
+                     int srow, u32x4 (&ra)[BM / 64], u32x4 (&ra2)[BM / 64], u32x4 (&rb)[BN / 64],
+                     uint32_t (&mk)[BM / 64]) {
+  constexpr int EPC = Elem<T>::EPC;
 #pragma unroll
   for (int i = 0; i < BM / 64; ++i) {
     const int r = min(srow + 64 * i, valid - 1);   // clamped: rows >= valid are zeroed later
     const int64_t off = (row_base + r) * K + k0;
     ra[i] = *reinterpret_cast<const u32x4 *>(Ag + off);
     if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const u32x4 *>(A2g + off);
+    if constexpr (MASK) {
+      const uint32_t byte = a.a_mask[off >> 3];
+      mk[i] = EPC == 8 ? byte : (byte >> (k0 & 7)) & 0xFu;
+    }
   }
 #pragma unroll
   for (int i = 0; i < BN / 64; ++i)
     rb[i] = *reinterpret_cast<const u32x4 *>(Wg + (int64_t)(n0 + srow + 64 * i) * K + k0);
 }
 
-// ... then prologue transform and registers -> LDS (after the current k-step's MFMAs)
-template <typename T, int BM, int BN, int PRO>
-PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, int scene, int64_t row_base, int valid, int K,
+// ... then prologue transform (coefficients from LDS) and registers -> LDS
+template <typename T, int BM, int BN, int PRO, bool MASK>
+PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, const float *cf, int64_t row_base, int valid,
                       int k0, int slot, int srow, const u32x4 (&ra)[BM / 64],
-                      const u32x4 (&ra2)[BM / 64], const u32x4 (&rb)[BN / 64]) {
+                      const u32x4 (&ra2)[BM / 64], const u32x4 (&rb)[BN / 64],
+                      const uint32_t (&mk)[BM / 64]) {
   constexpr int EPC = Elem<T>::EPC;
   char *tB = tA + BM * ROWB;
   float c0[EPC], c1[EPC], c2[EPC];
   if constexpr (PRO == PCS_PRO_BNRELU) {
-    load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1);
-  } else if constexpr (PRO == PCS_PRO_BWD) {
-    load_vec<EPC>(a.pa, k0, c0); load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
-  } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
-    load_vec<EPC>(a.pb, k0, c1); load_vec<EPC>(a.pc, k0, c2);
-    load_vec<EPC>(a.pool_coef + scene * K, k0, c0);
+    lds_vec<EPC>(cf + k0, c0); lds_vec<EPC>(cf + KMAX + k0, c1);
+  } else if constexpr (PRO == PCS_PRO_BWD || PRO == PCS_PRO_BWD_POOL) {
+    lds_vec<EPC>(cf + k0, c0); lds_vec<EPC>(cf + KMAX + k0, c1); lds_vec<EPC>(cf + 2 * KMAX + k0, c2);
   }
 #pragma unroll
   for (int i = 0; i < BM / 64; ++i) {
@@ -96,12 +115,10 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, int scene, int64_t row_b
     float v[EPC];
     unpack_chunk(ra[i], v);
     if constexpr (PRO == PCS_PRO_BNRELU) {
-      uint32_t bits = 0xffu;
-      if (a.a_mask) bits = mask_bits(a.a_mask, row_base + min(r, valid - 1), K, k0, EPC);
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
         float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
-        if (a.a_mask) x *= ((bits >> e) & 1u) ? a.a_keep_scale : 0.f;
+        if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
         v[e] = x;
       }
     } else if constexpr (PRO == PCS_PRO_BWD) {
@@ -111,15 +128,11 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, int scene, int64_t row_b
       for (int e = 0; e < EPC; ++e) v[e] = fmaf(c0[e], v[e], fmaf(c2[e], y[e], c1[e]));
     } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
       const int grow = (int)(row_base + r);
-      const int *am = a.pool_idx + scene * K + k0;
+      const int *am = reinterpret_cast<const int *>(cf + 3 * KMAX) + k0;
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) {
-        float x = fmaf(c2[e], v[e], c1[e]);
-        if (am[e] == grow) x += c0[e];
-        v[e] = x;
-      }
+      for (int e = 0; e < EPC; ++e) v[e] = fmaf(c2[e], v[e], c1[e]) + (am[e] == grow ? c0[e] : 0.f);
     }
-    u32x4 out = pack_chunk(v);
+    u32x4 out = PRO == PCS_PRO_RAW ? ra[i] : pack_chunk(v);
     if (r >= valid) out = mk_u32x4(0, 0, 0, 0);
     *reinterpret_cast<u32x4 *>(tA + r * ROWB + swz(r, slot) * 16) = out;
   }
@@ -130,8 +143,8 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, int scene, int64_t row_b
   }
 }
 
-template <typename T, int BM, int BN, int PRO, int EPI, bool POOL>
-__global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int tiles_per_scene,
+template <typename T, int BM, int BN, int PRO, int EPI, bool POOL, bool MASK>
+__global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                           int tiles_per_chunk, int ncb) {
   constexpr int EPC = Elem<T>::EPC;
   constexpr int SZ = Elem<T>::SIZE;
@@ -145,10 +158,15 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
   constexpr int CPR = BN * SZ / 16;            // chunks per output row
   constexpr int RPP = THREADS / CPR;           // rows per epilogue pass
   constexpr int RED_BYTES = RPP * BN * 16;
-  constexpr int LDS_BYTES = STAGE_BYTES > CTILE_BYTES
-                                ? (STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES)
-                                : (CTILE_BYTES > RED_BYTES ? CTILE_BYTES : RED_BYTES);
+  constexpr int MAIN_BYTES = STAGE_BYTES > CTILE_BYTES
+                                 ? (STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES)
+                                 : (CTILE_BYTES > RED_BYTES ? CTILE_BYTES : RED_BYTES);
+  constexpr int PCOEF = Coef<PRO>::N * KMAX;            // floats
+  constexpr int ECOEF = EPI == PCS_EPI_DGRAD ? 4 * BN : 0;
+  constexpr int LDS_BYTES = MAIN_BYTES + 4 * (PCOEF + ECOEF);
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  float *cf = reinterpret_cast<float *>(lds + MAIN_BYTES);
+  float *ecf = cf + PCOEF;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -162,11 +180,30 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
   const int t_begin = cis * tiles_per_chunk;
   const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
   const int nks = K / KSTEP;
+  if (t_begin >= t_end) return;  // uniform across the block
 
   const T *__restrict__ Ag = reinterpret_cast<const T *>(a.A);
   const T *__restrict__ A2g = reinterpret_cast<const T *>(a.A2);
   const T *__restrict__ Wg = reinterpret_cast<const T *>(a.W);
   T *__restrict__ Cg = reinterpret_cast<T *>(a.C);
+
+  // per-channel coefficients -> LDS (a workgroup's rows never leave its scene)
+  for (int k = tid; k < K; k += THREADS) {
+    if constexpr (PRO == PCS_PRO_BNRELU) {
+      cf[k] = a.pa[k]; cf[KMAX + k] = a.pb[k];
+    } else if constexpr (PRO == PCS_PRO_BWD) {
+      cf[k] = a.pa[k]; cf[KMAX + k] = a.pb[k]; cf[2 * KMAX + k] = a.pc[k];
+    } else if constexpr (PRO == PCS_PRO_BWD_POOL) {
+      cf[k] = a.pool_coef[(int64_t)scene * K + k]; cf[KMAX + k] = a.pb[k]; cf[2 * KMAX + k] = a.pc[k];
+      reinterpret_cast<int *>(cf)[3 * KMAX + k] = a.pool_idx[(int64_t)scene * K + k];
+    }
+  }
+  if constexpr (EPI == PCS_EPI_DGRAD) {
+    for (int c = tid; c < BN; c += THREADS) {
+      ecf[c] = a.es[n0 + c]; ecf[BN + c] = a.et[n0 + c];
+      ecf[2 * BN + c] = a.emean[n0 + c]; ecf[3 * BN + c] = a.erstd[n0 + c];
+    }
+  }
 
   const int slot = tid & 3;           // staging: fixed k-slot per thread
   const int srow = tid >> 2;          // staging: row (+64*i)
@@ -186,25 +223,38 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
     pmaxi[e] = 0x7fffffff; pmini[e] = 0x7fffffff;
   }
 
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int64_t row_base = scene * N + (int64_t)tile * BM;
-    const int valid = (int)pcs_min64(BM, N - (int64_t)tile * BM);
+  auto tile_rows = [&](int tile) { return (int)pcs_min64(BM, N - (int64_t)tile * BM); };
+  u32x4 ra[ACH], ra2[ACH], rb[BCH];
+  uint32_t mk[ACH];
+  int64_t row_base = scene * N + (int64_t)t_begin * BM;
+  int valid = tile_rows(t_begin);
+  nt_load<T, BM, BN, PRO, MASK>(a, Ag, A2g, Wg, row_base, valid, K, n0, slot * EPC, srow, ra, ra2, rb, mk);
+  __syncthreads();   // coefficients visible
 
-    u32x4 ra[ACH], ra2[ACH], rb[BCH];
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int64_t next_base = row_base + BM;
+    const int next_valid = tile + 1 < t_end ? tile_rows(tile + 1) : 0;
+    // ONE load site per k-step (see gemm_big.hip): step ks+1 of this tile, else step 0 of
+    // the next tile, else an in-bounds reload that is never consumed
+    auto prefetch = [&](int ks_next) {
+      const bool tail = ks_next >= nks;
+      const bool nxt = tail && next_valid > 0;
+      nt_load<T, BM, BN, PRO, MASK>(a, Ag, A2g, Wg, nxt ? next_base : row_base, nxt ? next_valid : valid,
+                                    K, n0, (tail ? 0 : ks_next) * KSTEP + slot * EPC, srow, ra, ra2, rb, mk);
+    };
+
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    nt_load<T, BM, BN, PRO>(Ag, A2g, Wg, row_base, valid, K, n0, slot * EPC, srow, ra, ra2, rb);
-    nt_store<T, BM, BN, PRO>(a, lds, scene, row_base, valid, K, slot * EPC, slot, srow, ra, ra2, rb);
-    __syncthreads();
+    nt_store<T, BM, BN, PRO, MASK>(a, lds, cf, row_base, valid, slot * EPC, slot, srow, ra, ra2, rb, mk);
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch(1);
+    lds_barrier();
     for (int ks = 0; ks < nks; ++ks) {
       const int buf = ks & 1;
-      if (ks + 1 < nks)
-        nt_load<T, BM, BN, PRO>(Ag, A2g, Wg, row_base, valid, K, n0, (ks + 1) * KSTEP + slot * EPC,
-                                srow, ra, ra2, rb);
       const char *tA = lds + buf * (BM + BN) * ROWB;
       const char *tB = tA + BM * ROWB;
 #pragma unroll
@@ -219,10 +269,13 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
 #pragma unroll
           for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::mma(bf[j], af[i], acc[i][j]);
       }
-      if (ks + 1 < nks)
-        nt_store<T, BM, BN, PRO>(a, lds + (buf ^ 1) * (BM + BN) * ROWB, scene, row_base, valid, K,
-                                 (ks + 1) * KSTEP + slot * EPC, slot, srow, ra, ra2, rb);
-      __syncthreads();
+      if (ks + 1 < nks) {
+        nt_store<T, BM, BN, PRO, MASK>(a, lds + (buf ^ 1) * (BM + BN) * ROWB, cf, row_base, valid,
+                                       (ks + 1) * KSTEP + slot * EPC, slot, srow, ra, ra2, rb, mk);
+        __builtin_amdgcn_sched_barrier(0);
+        prefetch(ks + 2);
+      }
+      lds_barrier();
     }
 
     // ---- epilogue phase 1: accumulators (+bias) -> LDS tile [BM][BN] in T ----
@@ -255,8 +308,9 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
     {
       float es[EPC], et[EPC], em[EPC], er[EPC];
       if constexpr (EPI == PCS_EPI_DGRAD) {
-        load_vec<EPC>(a.es, ecol, es); load_vec<EPC>(a.et, ecol, et);
-        load_vec<EPC>(a.emean, ecol, em); load_vec<EPC>(a.erstd, ecol, er);
+        const int lc = ecc * EPC;
+        lds_vec<EPC>(ecf + lc, es); lds_vec<EPC>(ecf + BN + lc, et);
+        lds_vec<EPC>(ecf + 2 * BN + lc, em); lds_vec<EPC>(ecf + 3 * BN + lc, er);
       }
       const T *Ypg = reinterpret_cast<const T *>(a.Yp);
       const T *Addg = reinterpret_cast<const T *>(a.addend);
@@ -335,10 +389,11 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_kernel(pcs_gemm_args a, int t
       }
     }
     __syncthreads();
+    row_base = next_base;
+    valid = next_valid;
   }
 
   // ---- chunk end: cross-thread reduction of the per-thread partials ----
-  if (t_begin >= t_end) return;  // uniform across the block
   const int64_t chunk_id = (int64_t)scene * cps + cis;
   if constexpr (EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD) {
     if (a.stats) {
@@ -388,8 +443,12 @@ template <typename T, int BM, int BN, int PRO, int EPI, bool POOL>
 int launch_t(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
   const int ncb = a.Ncols / BN;
   const int nb = ncb * (int)(a.num_scenes * a.chunks_per_scene);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL>), dim3(nb), dim3(THREADS), 0, s,
-                     a, tps, tpc, ncb);
+  if (PRO == PCS_PRO_BNRELU && a.a_mask)
+    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL, PRO == PCS_PRO_BNRELU>), dim3(nb),
+                       dim3(THREADS), 0, s, a, tps, tpc, ncb);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL, false>), dim3(nb), dim3(THREADS), 0, s,
+                       a, tps, tpc, ncb);
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -463,6 +522,9 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (a.pool && a.epilogue != PCS_EPI_FWD) return pcs_set_einval("pcs_gemm", "pool needs EPI_FWD");
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31)
     return pcs_set_einval("pcs_gemm", "M must be < 2^31 rows");
+  if (a.K > KMAX) return pcs_set_einval("pcs_gemm", "K must be <= 1024");
+  if (a.a_mask && a.prologue != PCS_PRO_BNRELU)
+    return pcs_set_einval("pcs_gemm", "a_mask applies to the BNRELU prologue only");
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
