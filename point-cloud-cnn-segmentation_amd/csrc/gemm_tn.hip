@@ -29,7 +29,7 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 template <typename T> struct TnCfg;
 template <> struct TnCfg<bf16_t> {
-  static constexpr int MS = 32;    // rows (reduction) per step
+  static constexpr int MS = 64;    // rows (reduction) per step: 2 MFMA k-iterations
   static constexpr int PADB = 32;  // row padding in bytes
   static PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 };
@@ -51,9 +51,9 @@ struct Operand {
   static constexpr int BYTES = MS * ROWB;
 };
 
-template <typename T, int TM, int TN, int DYMODE, int XMODE>
-__global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_t rows_per_split,
-                                                        int ntn, int ntiles) {
+template <typename T, int TM, int TN, int DYMODE, int XMODE, bool MASK>
+__global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int64_t rows_per_split,
+                                                           int ntn, int ntiles) {
   constexpr int EPC = Elem<T>::EPC;
   constexpr int MS = TnCfg<T>::MS;
   typedef Operand<T, TM, DYMODE> OA;  // dy tile [MS][TM]
@@ -98,21 +98,26 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
     load_vec<EPC>(a.t, bk, xt);
   }
 
+  // Rows past the slice end are loaded clamped (no branches) and written to LDS as zeros.
   u32x4 rz[OA::NCH], ry[OA::NCH], rx[OB::NCH];
+  uint32_t mk[OB::NCH];
   auto load_stage = [&](int64_t m0) {
 #pragma unroll
     for (int i = 0; i < OA::NCH; ++i) {
-      const int64_t r = m0 + ar0 + OA::RP * i;
-      if (r < hi) {
-        const int64_t off = (scene * N + r) * Cout + an;
-        if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
-        ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
-      }
+      const int64_t r = pcs_min64(m0 + ar0 + OA::RP * i, hi - 1);
+      const int64_t off = (scene * N + r) * Cout + an;
+      if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
+      ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
     }
 #pragma unroll
     for (int i = 0; i < OB::NCH; ++i) {
-      const int64_t r = m0 + br0 + OB::RP * i;
-      if (r < hi) rx[i] = *reinterpret_cast<const u32x4 *>(Xg + (scene * N + r) * Cin + bk);
+      const int64_t r = pcs_min64(m0 + br0 + OB::RP * i, hi - 1);
+      const int64_t off = (scene * N + r) * Cin + bk;
+      rx[i] = *reinterpret_cast<const u32x4 *>(Xg + off);
+      if constexpr (MASK) {
+        const uint32_t byte = a.x_mask[off >> 3];
+        mk[i] = EPC == 8 ? byte : (byte >> (bk & 7)) & 0xFu;
+      }
     }
   };
   auto store_stage = [&](int64_t m0, int buf) {
@@ -122,49 +127,38 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
     for (int i = 0; i < OA::NCH; ++i) {
       const int rl = ar0 + OA::RP * i;
       const int64_t r = m0 + rl;
-      u32x4 out = mk_u32x4(0, 0, 0, 0);
-      if (r < hi) {
-        float y[EPC], v[EPC];
-        unpack_chunk(ry[i], y);
-        if constexpr (DYMODE == PCS_PRO_BWD) {
-          unpack_chunk(rz[i], v);
+      float y[EPC], v[EPC];
+      unpack_chunk(ry[i], y);
+      if constexpr (DYMODE == PCS_PRO_BWD) {
+        unpack_chunk(rz[i], v);
 #pragma unroll
-          for (int e = 0; e < EPC; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
-        } else {
-          const int grow = (int)(scene * N + r);
+        for (int e = 0; e < EPC; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+      } else {
+        const int grow = (int)(scene * N + r);
 #pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            float x = fmaf(cg[e], y[e], cb[e]);
-            if (am[e] == grow) x += ca[e];
-            v[e] = x;
-          }
-        }
-        out = pack_chunk(v);
+        for (int e = 0; e < EPC; ++e) v[e] = fmaf(cg[e], y[e], cb[e]) + (am[e] == grow ? ca[e] : 0.f);
       }
+      u32x4 out = pack_chunk(v);
+      if (r >= hi) out = mk_u32x4(0, 0, 0, 0);
       *reinterpret_cast<u32x4 *>(tA + TnCfg<T>::prow(rl) * OA::ROWB + acc_c * 16) = out;
     }
 #pragma unroll
     for (int i = 0; i < OB::NCH; ++i) {
       const int rl = br0 + OB::RP * i;
       const int64_t r = m0 + rl;
-      u32x4 out = mk_u32x4(0, 0, 0, 0);
-      if (r < hi) {
-        if constexpr (XMODE == PCS_PRO_BNRELU) {
-          float v[EPC];
-          unpack_chunk(rx[i], v);
-          uint32_t bits = 0xffu;
-          if (a.x_mask) bits = mask_bits(a.x_mask, scene * N + r, Cin, bk, EPC);
+      u32x4 out = rx[i];
+      if constexpr (XMODE == PCS_PRO_BNRELU) {
+        float v[EPC];
+        unpack_chunk(rx[i], v);
 #pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            float x = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
-            if (a.x_mask) x *= ((bits >> e) & 1u) ? a.x_keep_scale : 0.f;
-            v[e] = x;
-          }
-          out = pack_chunk(v);
-        } else {
-          out = rx[i];
+        for (int e = 0; e < EPC; ++e) {
+          float x = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+          if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.x_keep_scale : 0.f;
+          v[e] = x;
         }
+        out = pack_chunk(v);
       }
+      if (r >= hi) out = mk_u32x4(0, 0, 0, 0);
       *reinterpret_cast<u32x4 *>(tB + TnCfg<T>::prow(rl) * OB::ROWB + bcc * 16) = out;
     }
   };
@@ -175,46 +169,52 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Pipeline: compute(st) -> write registers (step st+1) to the other LDS buffer -> issue
+  // the loads of step st+2 -> barrier; each load has a full step of MFMAs to land.
   const int nsteps = (int)((hi - lo + MS - 1) / MS);
   if (nsteps > 0) {
     load_stage(lo);
     store_stage(lo, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_stage(lo + MS);   // clamped: harmless when nsteps == 1
     __syncthreads();
   }
   for (int st = 0; st < nsteps; ++st) {
     const int buf = st & 1;
     const int64_t m0 = lo + (int64_t)st * MS;
-    if (st + 1 < nsteps) load_stage(m0 + MS);
     const char *tA = lds + buf * STAGE;
     const char *tB = tA + OA::BYTES;
     if constexpr (sizeof(T) == 2) {
-      // lane group g = lane>>4 holds k = 8g..8g+7 of the MFMA reduction (= m rows)
-      const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-      const int r0 = TnCfg<T>::prow(8 * g + q), r1 = TnCfg<T>::prow(8 * g + 4 + q);
-      bf16x8 xf[FN], yf[FM];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = wn * (TN / 2) + j * 16 + 4 * p;
-        s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tB + r0 * OB::ROWB + c * 2));
-        s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tB + r1 * OB::ROWB + c * 2));
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-        xf[j] = __builtin_bit_cast(bf16x8, v);
+      for (int kk = 0; kk < MS / 32; ++kk) {
+        // lane group g = lane>>4 holds k = 8g..8g+7 of the MFMA reduction (= m rows)
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int r0 = TnCfg<T>::prow(32 * kk + 8 * g + q), r1 = TnCfg<T>::prow(32 * kk + 8 * g + 4 + q);
+        bf16x8 xf[FN], yf[FM];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = wn * (TN / 2) + j * 16 + 4 * p;
+          s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tB + r0 * OB::ROWB + c * 2));
+          s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tB + r1 * OB::ROWB + c * 2));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+          xf[j] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int c = wm * (TM / 2) + i * 16 + 4 * p;
+          s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tA + r0 * OA::ROWB + c * 2));
+          s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tA + r1 * OA::ROWB + c * 2));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+          yf[i] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], yf[i], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int c = wm * (TM / 2) + i * 16 + 4 * p;
-        s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tA + r0 * OA::ROWB + c * 2));
-        s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(tA + r1 * OA::ROWB + c * 2));
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        s16x8 v = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-        yf[i] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], yf[i], acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
       for (int kk = 0; kk < MS / 4; ++kk) {
@@ -233,8 +233,12 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(pcs_wgrad_args a, int64_
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(xf[j], yf[i], acc[i][j], 0, 0, 0);
       }
     }
-    if (st + 1 < nsteps) store_stage(m0 + MS, buf ^ 1);
-    __syncthreads();
+    if (st + 1 < nsteps) {
+      store_stage(m0 + MS, buf ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+      load_stage(m0 + 2 * MS);   // clamped past the end: never consumed
+    }
+    lds_barrier();
   }
 
   // partial tile: lane holds dW[n][k..k+3]
@@ -255,7 +259,11 @@ template <typename T, int TM, int TN, int DY, int XM>
 int launch(const pcs_wgrad_args &a, int64_t rps, hipStream_t s) {
   const int ntn = a.Cin / TN, ntiles = (a.Cout / TM) * ntn;
   const int nb = ntiles * (int)(a.num_scenes * a.splits_per_scene);
-  hipLaunchKernelGGL((wgrad_kernel<T, TM, TN, DY, XM>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  if (XM == PCS_PRO_BNRELU && a.x_mask)
+    hipLaunchKernelGGL((wgrad_kernel<T, TM, TN, DY, XM, XM == PCS_PRO_BNRELU>), dim3(nb), dim3(THREADS), 0, s,
+                       a, rps, ntn, ntiles);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<T, TM, TN, DY, XM, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -290,7 +298,7 @@ int64_t rows_per_split_of(const pcs_wgrad_args &a, int ms) {
 extern "C" int64_t pcs_wgrad_workspace(pcs_wgrad_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Cout <= 0 || a->Cin <= 0)
     return pcs_set_einval("pcs_wgrad_workspace", "bad geometry");
-  const int ms = a->dtype == PCS_BF16 ? 32 : 16;
+  const int ms = a->dtype == PCS_BF16 ? TnCfg<bf16_t>::MS : TnCfg<float>::MS;
   if (a->splits_per_scene <= 0 && pcs_wgrad_big_applicable(*a)) a->splits_per_scene = pcs_wgrad_big_splits(*a);
   if (a->splits_per_scene <= 0) {
     const int tm = a->Cout % 128 == 0 ? 128 : 64, tn = a->Cin % 128 == 0 ? 128 : 64;
@@ -316,7 +324,7 @@ extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
     return pcs_set_einval("pcs_wgrad", "PRO_BWD_POOL needs pool_idx, pool_coef");
   if (a.x_mode == PCS_PRO_BNRELU && (!a.s || !a.t)) return pcs_set_einval("pcs_wgrad", "x BNRELU needs s, t");
   if (pcs_wgrad_workspace(&a) < 0) return PCS_EINVAL;
-  const int ms = a.dtype == PCS_BF16 ? 32 : 16;
+  const int ms = a.dtype == PCS_BF16 ? TnCfg<bf16_t>::MS : TnCfg<float>::MS;
   const int64_t rps = rows_per_split_of(a, ms);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc;
