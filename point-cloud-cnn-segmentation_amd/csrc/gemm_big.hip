@@ -1,19 +1,21 @@
-// bf16 256x256x64 points-major GEMM for the wide layers (global_feat forward and dgrad:
-// M x 1024 x 1024, 75 % of the model's MACs; P:113 and its autograd at P:254).
+// bf16 256x256x64 points-major GEMM (pcs_gemm for bf16 with Ncols % 256 == 0, K >= 128):
+// the wide layers' forward and input-gradient GEMMs (global_feat M x 1024 x 1024 is 75 % of
+// the model's MACs; conv5, seg_conv1/2/3; P:106-128 and their autograd at P:254).
 //
 // Same contract as gemm_nt.hip (pcs_gemm_args, scene-aligned row chunks, prologue and
 // epilogue fusion) with a tile sized for MFMA throughput instead of generality:
 // * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 outputs =
 //   8 x 4 v_mfma_f32_16x16x32_bf16 accumulators; 64 MFMAs per wave per 64-deep k-step.
-// * operands staged global -> VGPR (BN+ReLU / BN-backward prologue) -> LDS, 128-B rows,
-//   16-B slots XOR-swizzled with (row>>1)&7 so the ds_read_b128 fragment reads are
-//   bank-conflict free; two LDS stages, one barrier per k-step; the next k-step's global
-//   loads are issued before the current MFMAs.
-// * forward epilogue: bias, tile staged through LDS for 16-B coalesced stores (BN
-//   statistics and max-pool partials come from one streaming pass, pcs_colstats: fused
-//   here as cross-lane reductions they cost ~1/3 of the kernel).
-// * dgrad: raw store (PCS_EPI_RAW); the ReLU / BN-backward stage of the previous layer runs
-//   as one streaming pass (pcs_bnrelu_bwd).
+// * operands staged global -> VGPR (BN+ReLU / BN-backward prologue, coefficients from LDS)
+//   -> LDS, 128-B rows, 16-B slots XOR-swizzled with (row>>1)&7 so the ds_read_b128
+//   fragment reads are bank-conflict free; two LDS stages, one raw barrier per k-step; the
+//   loads of step ks+2 are issued right after step ks+1 is written (one load site).
+// * epilogue: the tile goes through LDS (phase 1) and is walked in coalesced row chunks
+//   (phase 2): bias / per-scene bias + store, or the previous layer's ReLU / dropout /
+//   addend backward (EPI_DGRAD).  Column statistics (Welford; or the BN-backward sums
+//   S1/S2) and max-pool max/min+argmax are per-thread over 16 rows, merged per tile
+//   through LDS into running per-column accumulators and written once per chunk in the
+//   generic kernel's partial layout.
 #include "common.h"
 
 namespace {
@@ -27,9 +29,20 @@ constexpr int CROW = BN * 2 + 16;            // epilogue tile row stride
 constexpr int CTILE = BM * CROW;             // 132 KB
 constexpr int CPR = BN * 2 / 16;             // 32 chunks per output row
 constexpr int RPP = THREADS / CPR;           // 16 rows per pass
+constexpr int NPASS = BM / RPP;              // 16 rows per thread in phase 2
 constexpr int LDS_MAIN = (2 * STAGE > CTILE) ? 2 * STAGE : CTILE;
-constexpr int COEF = 4 * KMAX * 4;           // up to 4 per-channel arrays (16 KB)
-constexpr int LDS_BYTES = LDS_MAIN + COEF + 32;   // + per-tile argmax-row bitmap (256 bits)
+
+// LDS layout after the main area: prologue coefficients | argmax bitmap | epilogue
+// coefficients (DGRAD) | running per-column accumulators
+template <int PRO, int EPI> struct Lay {
+  static constexpr int NC = PRO == PCS_PRO_BNRELU ? 2 : PRO == PCS_PRO_BWD ? 3 : PRO == PCS_PRO_BWD_POOL ? 4 : 0;
+  static constexpr int COEF = LDS_MAIN;
+  static constexpr int BITS = COEF + NC * KMAX * 4;
+  static constexpr int ECOEF = BITS + (PRO == PCS_PRO_BWD_POOL ? 32 : 0);
+  static constexpr int RUN = ECOEF + (EPI == PCS_EPI_DGRAD ? 4 * BN * 4 : 0);
+  static constexpr int BYTES = RUN + (EPI == PCS_EPI_FWD ? 6 * BN * 4 : EPI == PCS_EPI_DGRAD ? 2 * BN * 4 : 0);
+  static_assert(BYTES <= 160 * 1024, "LDS budget");
+};
 
 PCS_DEV int swz8(int row, int slot) { return slot ^ ((row >> 1) & 7); }
 
@@ -55,9 +68,12 @@ template <int PRO, int EPI, bool MASK>
 __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                            int tiles_per_chunk, int ncb) {
   constexpr int EPC = 8;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  float *cf = reinterpret_cast<float *>(lds + LDS_MAIN);
-  uint32_t *tbits = reinterpret_cast<uint32_t *>(lds + LDS_MAIN + COEF);
+  typedef Lay<PRO, EPI> LY;
+  __shared__ __attribute__((aligned(16))) char lds[LY::BYTES];
+  float *cf = reinterpret_cast<float *>(lds + LY::COEF);
+  uint32_t *tbits = reinterpret_cast<uint32_t *>(lds + LY::BITS);
+  float *ecf = reinterpret_cast<float *>(lds + LY::ECOEF);   // DGRAD: es | et | emean | erstd
+  float *run = reinterpret_cast<float *>(lds + LY::RUN);     // mean|m2|max|maxi|min|mini or S1|S2
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -90,6 +106,19 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       reinterpret_cast<int *>(cf)[3 * KMAX + k] = a.pool_idx[(int64_t)scene * K + k];
     }
   }
+  const bool do_stats = a.stats != nullptr, do_pool = EPI == PCS_EPI_FWD && a.pool != nullptr;
+  if (tid < BN) {
+    if constexpr (EPI == PCS_EPI_DGRAD) {
+      ecf[tid] = a.es[n0 + tid]; ecf[BN + tid] = a.et[n0 + tid];
+      ecf[2 * BN + tid] = a.emean[n0 + tid]; ecf[3 * BN + tid] = a.erstd[n0 + tid];
+      run[tid] = 0.f; run[BN + tid] = 0.f;
+    } else if constexpr (EPI == PCS_EPI_FWD) {
+      run[tid] = 0.f; run[BN + tid] = 0.f;
+      run[2 * BN + tid] = -__builtin_huge_valf(); run[3 * BN + tid] = __int_as_float(0x7fffffff);
+      run[4 * BN + tid] = __builtin_huge_valf(); run[5 * BN + tid] = __int_as_float(0x7fffffff);
+    }
+  }
+  float run_n = 0.f;   // rows merged into the running statistics so far (uniform)
 
   const int slot = tid & 7, srow = tid >> 3;  // staging: rows srow + 64*i, fixed k-slot
   const int ecc = tid % CPR, er0 = tid / CPR, ecol = n0 + ecc * EPC;
@@ -163,6 +192,16 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   __syncthreads();   // coefficients visible
 
   for (int tile = t_begin; tile < t_end; ++tile) {
+    const int64_t next_base = row_base + BM;
+    const int next_valid = (tile + 1 < t_end) ? tile_rows(tile + 1) : 0;
+    // ONE load site per k-step (two sites make the compiler merge their registers with
+    // copies that wait for the loads): step ks_next of this tile, else step 0 of the next
+    // tile, else a harmless in-bounds reload that is never consumed.
+    auto prefetch = [&](int ks_next) {
+      const bool tail = ks_next >= nks;
+      const bool nxt = tail && next_valid > 0;
+      load_stage(nxt ? next_base : row_base, nxt ? next_valid : valid, tail ? 0 : ks_next);
+    };
     if constexpr (PRO == PCS_PRO_BWD_POOL) {   // bitmap of the tile's argmax rows
       if (tid < BM / 32) tbits[tid] = 0u;
       __syncthreads();
@@ -181,7 +220,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     }
     store_stage(row_base, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
-    load_stage(row_base, valid, 1);   // nks >= 8 (K >= 512)
+    prefetch(1);
     lds_barrier();
 
     f32x4 acc[8][4];
@@ -190,8 +229,6 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int64_t next_base = row_base + BM;
-    const int next_valid = (tile + 1 < t_end) ? tile_rows(tile + 1) : 0;
     for (int ks = 0; ks < nks; ++ks) {
       const int buf = ks & 1;
       const char *tA = lds + buf * STAGE;
@@ -217,23 +254,18 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       if (ks + 1 < nks) {
         store_stage(row_base, ks + 1, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);   // keep one staging register set live, not two
-        // ONE load site (two sites make the compiler merge their registers with copies that
-        // wait for the loads): k-step ks+2 of this tile, else step 0 of the next tile, else
-        // a harmless in-bounds reload that is never consumed.
-        const bool tail = ks + 2 >= nks;
-        const bool has_next = next_valid > 0;
-        load_stage(tail && has_next ? next_base : row_base, tail && has_next ? next_valid : valid,
-                   tail ? 0 : ks + 2);
+        prefetch(ks + 2);
       }
       lds_barrier();
     }
 
     // lane owns rows m = wm*128 + i*16 + (lane&15), cols n = wn*64 + j*16 + 4*(lane>>4) + r
     if constexpr (EPI == PCS_EPI_FWD) {
-      if (a.bias) {
+      const float *bias = a.scene_bias ? a.scene_bias + (int64_t)scene * Ncols : a.bias;
+      if (bias) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float4 bb = *reinterpret_cast<const float4 *>(a.bias + n0 + wn * 64 + j * 16 + lcol);
+          const float4 bb = *reinterpret_cast<const float4 *>(bias + n0 + wn * 64 + j * 16 + lcol);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
@@ -242,7 +274,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       }
     }
 
-    // phase 1: tile -> LDS (bf16), phase 2: coalesced row chunks
+    // phase 1: tile -> LDS (bf16)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = wm * 128 + i * 16 + lrow;
@@ -254,15 +286,161 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       }
     }
     __syncthreads();
-    if (Cg) {
-#pragma unroll 4
-      for (int rr = er0; rr < valid; rr += RPP)
-        *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) =
-            *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+
+    // phase 2: coalesced row chunks (thread: 8 columns ecc*8.., rows er0 + 16 p)
+    float sa[EPC], sb[EPC];                      // Welford mean/M2, or S1/S2
+    float pmx[EPC], pmn[EPC];
+    int pmxi[EPC], pmni[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      sa[e] = 0.f; sb[e] = 0.f;
+      pmx[e] = -__builtin_huge_valf(); pmn[e] = __builtin_huge_valf();
+      pmxi[e] = 0x7fffffff; pmni[e] = 0x7fffffff;
     }
-    __syncthreads();
+    float cnt = 0.f;
+    if constexpr (EPI == PCS_EPI_FWD) {
+#pragma unroll 4
+      for (int p = 0; p < NPASS; ++p) {
+        const int rr = er0 + RPP * p;
+        if (rr < valid) {
+          const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+          if (Cg) *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) = raw;
+          if (do_stats || do_pool) {
+            float v[EPC];
+            unpack_chunk(raw, v);
+            if (do_stats) {
+              cnt += 1.f;
+              const float rn = 1.f / cnt;
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) {
+                const float d = v[e] - sa[e];
+                sa[e] = fmaf(d, rn, sa[e]);
+                sb[e] = fmaf(d, v[e] - sa[e], sb[e]);
+              }
+            }
+            if (do_pool) {
+              const int grow = (int)(row_base + rr);
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) {
+                if (v[e] > pmx[e]) { pmx[e] = v[e]; pmxi[e] = grow; }
+                if (v[e] < pmn[e]) { pmn[e] = v[e]; pmni[e] = grow; }
+              }
+            }
+          }
+        }
+      }
+    } else if constexpr (EPI == PCS_EPI_DGRAD) {
+      const bf16_t *Ypg = reinterpret_cast<const bf16_t *>(a.Yp);
+      const bf16_t *Addg = reinterpret_cast<const bf16_t *>(a.addend);
+      float es[EPC], et[EPC], em[EPC], er[EPC];
+      const int lc = ecc * EPC;
+      lds_vec8(ecf + lc, es); lds_vec8(ecf + BN + lc, et);
+      lds_vec8(ecf + 2 * BN + lc, em); lds_vec8(ecf + 3 * BN + lc, er);
+      const float ks = a.c_mask ? a.c_keep_scale : 1.f;
+      constexpr int BATCH = 4;
+#pragma unroll
+      for (int p0 = 0; p0 < NPASS; p0 += BATCH) {
+        u32x4 yv[BATCH], adv[BATCH];
+        uint32_t mb[BATCH];
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {   // clamped loads, issued together
+          const int rr = min(er0 + RPP * (p0 + q), valid - 1);
+          const int64_t goff = (row_base + rr) * Ncols + ecol;
+          yv[q] = *reinterpret_cast<const u32x4 *>(Ypg + goff);
+          adv[q] = Addg ? *reinterpret_cast<const u32x4 *>(Addg + goff) : mk_u32x4(0, 0, 0, 0);
+          mb[q] = a.c_mask ? a.c_mask[goff >> 3] : 0xffu;
+        }
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {
+          const int rr = er0 + RPP * (p0 + q);
+          if (rr < valid) {
+            const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+            float v[EPC], y[EPC], ad[EPC];
+            unpack_chunk(raw, v);
+            unpack_chunk(yv[q], y);
+            unpack_chunk(adv[q], ad);
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+              float g = v[e] + ad[e];
+              g *= ((mb[q] >> e) & 1u) ? ks : 0.f;
+              const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? g : 0.f;
+              v[e] = dz;
+              sa[e] += dz;                                       // S1
+              sb[e] = fmaf(dz, (y[e] - em[e]) * er[e], sb[e]);   // S2
+            }
+            *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) = pack_chunk(v);
+          }
+        }
+      }
+    } else {  // RAW
+#pragma unroll 4
+      for (int p = 0; p < NPASS; ++p) {
+        const int rr = er0 + RPP * p;
+        if (rr < valid)
+          *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) =
+              *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+      }
+    }
+    __syncthreads();   // the C tile has been consumed
+
+    // per-tile merge of the per-thread partials into the running per-column accumulators
+    if (EPI != PCS_EPI_RAW && (do_stats || do_pool)) {
+      float2 *ps = reinterpret_cast<float2 *>(lds);                 // [RPP][BN] stats / S1,S2
+      float4 *pp = reinterpret_cast<float4 *>(lds + RPP * BN * 8);  // [RPP][BN] pool
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        const int c = ecc * EPC + e;
+        if (do_stats) ps[er0 * BN + c] = make_float2(sa[e], sb[e]);
+        if (do_pool) pp[er0 * BN + c] = make_float4(pmx[e], __int_as_float(pmxi[e]), pmn[e], __int_as_float(pmni[e]));
+      }
+      __syncthreads();
+      if (tid < BN) {
+        const int c = tid;
+        if (do_stats) {
+          if constexpr (EPI == PCS_EPI_FWD) {
+            float n = run_n, mean = run[c], m2 = run[BN + c];
+            for (int j = 0; j < RPP; ++j) {
+              const float nj = valid > j ? (float)((valid - j + RPP - 1) / RPP) : 0.f;
+              const float2 q = ps[j * BN + c];
+              chan_merge(n, mean, m2, nj, q.x, q.y);
+            }
+            run[c] = mean; run[BN + c] = m2;
+          } else {
+            float s1 = run[c], s2 = run[BN + c];
+            for (int j = 0; j < RPP; ++j) {
+              const float2 q = ps[j * BN + c];
+              s1 += q.x; s2 += q.y;
+            }
+            run[c] = s1; run[BN + c] = s2;
+          }
+        }
+        if (do_pool) {
+          float mx = run[2 * BN + c], mn = run[4 * BN + c];
+          int mxi = __float_as_int(run[3 * BN + c]), mni = __float_as_int(run[5 * BN + c]);
+          for (int j = 0; j < RPP; ++j) {
+            const float4 q = pp[j * BN + c];
+            const int qi = __float_as_int(q.y), qj = __float_as_int(q.w);
+            if (q.x > mx || (q.x == mx && qi < mxi)) { mx = q.x; mxi = qi; }
+            if (q.z < mn || (q.z == mn && qj < mni)) { mn = q.z; mni = qj; }
+          }
+          run[2 * BN + c] = mx; run[3 * BN + c] = __int_as_float(mxi);
+          run[4 * BN + c] = mn; run[5 * BN + c] = __int_as_float(mni);
+        }
+      }
+      __syncthreads();   // partial area reused by the next tile's staging
+    }
+    run_n += (float)valid;
     row_base = next_base;
     valid = next_valid;
+  }
+
+  // chunk end: this workgroup's per-column partials (same layout as gemm_nt)
+  if (EPI != PCS_EPI_RAW && tid < BN) {
+    const int64_t o = (int64_t)chunk * Ncols + n0 + tid;
+    if (do_stats) *reinterpret_cast<float2 *>(a.stats + o * 2) = make_float2(run[tid], run[BN + tid]);
+    if (do_pool)
+      *reinterpret_cast<float4 *>(a.pool + o * 4) =
+          make_float4(run[2 * BN + tid], run[3 * BN + tid], run[4 * BN + tid], run[5 * BN + tid]);
   }
 }
 
@@ -278,22 +456,25 @@ int launch(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
 }  // namespace
 
 bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
-  if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 512 || a.K > KMAX) return false;
-  if (a.a_mask && a.prologue != PCS_PRO_BNRELU) return false;
+  if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 128 || a.K > KMAX) return false;
   if (a.flags & PCS_FLAG_GENERIC) return false;
-  if (a.epilogue == PCS_EPI_FWD)   // statistics / pool: pcs_colstats on the stored output
-    return a.prologue == PCS_PRO_BNRELU && !a.stats && !a.pool && !a.scene_bias;
-  if (a.epilogue == PCS_EPI_RAW) return a.prologue != PCS_PRO_RAW;   // dgrad: pcs_bnrelu_bwd after
+  if (a.a_mask && a.prologue != PCS_PRO_BNRELU) return false;
+  if (a.epilogue == PCS_EPI_FWD) return a.prologue == PCS_PRO_BNRELU;
+  if (a.epilogue == PCS_EPI_DGRAD) return a.prologue == PCS_PRO_BWD || a.prologue == PCS_PRO_BWD_POOL;
+  if (a.epilogue == PCS_EPI_RAW) return a.prologue == PCS_PRO_BWD || a.prologue == PCS_PRO_BWD_POOL;
   return false;
 }
 
 int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s) {
-  if (g.epilogue == PCS_EPI_FWD)
-    return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
-                    : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
-  if (g.prologue == PCS_PRO_BWD_POOL) return launch<PCS_PRO_BWD_POOL, PCS_EPI_RAW, false>(g, tps, tpc, s);
-  if (g.prologue == PCS_PRO_BNRELU)
-    return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_RAW, true>(g, tps, tpc, s)
-                    : launch<PCS_PRO_BNRELU, PCS_EPI_RAW, false>(g, tps, tpc, s);
-  return launch<PCS_PRO_BWD, PCS_EPI_RAW, false>(g, tps, tpc, s);
+  switch (g.epilogue) {
+    case PCS_EPI_FWD:
+      return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
+                      : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
+    case PCS_EPI_DGRAD:
+      return g.prologue == PCS_PRO_BWD_POOL ? launch<PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(g, tps, tpc, s)
+                                            : launch<PCS_PRO_BWD, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
+    default:
+      return g.prologue == PCS_PRO_BWD_POOL ? launch<PCS_PRO_BWD_POOL, PCS_EPI_RAW, false>(g, tps, tpc, s)
+                                            : launch<PCS_PRO_BWD, PCS_EPI_RAW, false>(g, tps, tpc, s);
+  }
 }

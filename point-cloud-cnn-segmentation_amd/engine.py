@@ -271,19 +271,14 @@ class Engine:
         layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"])
         layer("conv5", "conv4", "bn4", 128, 1024, "bn5", P["conv5.bias"])
 
-        # global_feat: plain GEMM + store, then one streaming pass for BN stats + max-pool
-        # partials (cheaper than reducing 1024 columns inside the GEMM epilogue)
+        # global_feat: GEMM + store with BN statistics and max-pool partials in the epilogue
         yg = self._empty(M, 1024, device=dev)
-        self._gemm(B, N, 1024, 1024, L.PRO_BNRELU, L.EPI_FWD, sv.ys["conv5"], wc["global_feat"][0], yg,
-                   tag="fwd:global_feat", **bnrelu("bn5"))
-        sv.ys["global_feat"] = yg
-        cps_g = ct.c_int32(0)
-        rpc_g = L.load().pcs_colstats_geometry(B, N, 1024, ct.byref(cps_g))
-        cps_g = cps_g.value
+        cps_g, rpc_g = self.geometry(B, N, 1024, 1024)
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
         st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
-        self._launch("stats:global_feat", "pcs_colstats", L.ptr(yg), B, N, 1024, self.dt, cps_g, rpc_g,
-                     L.ptr(st), L.ptr(pool), s)
+        self._gemm(B, N, 1024, 1024, L.PRO_BNRELU, L.EPI_FWD, sv.ys["conv5"], wc["global_feat"][0], yg,
+                   stats=st, pool=pool, tag="fwd:global_feat", **bnrelu("bn5"))
+        sv.ys["global_feat"] = yg
         sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_g, rpc_g, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]
@@ -466,19 +461,15 @@ class Engine:
                    A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
         wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
 
-        # global_feat (dy from the sparse max-pool gradient): raw dgrad GEMM, then the
-        # ReLU/BN5-backward input stage as one streaming pass
+        # global_feat (dy from the sparse max-pool gradient); the epilogue applies the
+        # ReLU/BN5-backward input stage and sums S1/S2 for bn5
         pc5 = sv.bn["bn5"]
-        self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_RAW, ys["global_feat"],
-                   wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
-                   tag="dgrad:global_feat")
-        cps5 = ct.c_int32(0)
-        rpc5 = L.load().pcs_colstats_geometry(B, N, 1024, ct.byref(cps5))
-        cps5 = cps5.value
+        cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD)
         st = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
-        self._launch("bnrelu_bwd:global_feat", "pcs_bnrelu_bwd", L.ptr(bufB), L.ptr(ys["conv5"]), None, None,
-                     1.0, L.ptr(pc5.scale), L.ptr(pc5.shift), L.ptr(pc5.mean), L.ptr(pc5.rstd), B, N, 1024,
-                     self.dt, cps5, rpc5, L.ptr(st), s)
+        self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD, ys["global_feat"],
+                   wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
+                   Yp=ys["conv5"], es=pc5.scale, et=pc5.shift, emean=pc5.mean, erstd=pc5.rstd,
+                   stats=st, tag="dgrad:global_feat")
         keepalive.append(self._wgrad(
             B, N, 1024, 1024, L.PRO_BWD_POOL, L.PRO_BNRELU, G("global_feat.weight"),
             tag="wgrad:global_feat", Y=ys["global_feat"], beta=bg, gamma=gg, pool_idx=sv.am, pool_coef=sp,
