@@ -64,10 +64,13 @@ PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
 // LDS (staged once per workgroup: a workgroup's row chunk never leaves its scene), and rows
 // past the end of a scene are clamped rather than branched around (their outputs are never
 // stored), so the k-loop carries no exec-mask branches and no early vmcnt(0).
-template <int PRO, int EPI, bool MASK>
+// MASK: dropout keep bits of A (FWD prologue) or of C (DGRAD epilogue); ADD: DGRAD addend
+template <int PRO, int EPI, bool MASK, bool ADD>
 __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                            int tiles_per_chunk, int ncb) {
   constexpr int EPC = 8;
+  constexpr bool AMASK = MASK && PRO == PCS_PRO_BNRELU;   // dropout bits of the A operand
+  constexpr bool CMASK = MASK && EPI == PCS_EPI_DGRAD;    // dropout bits of the dgrad output
   typedef Lay<PRO, EPI> LY;
   __shared__ __attribute__((aligned(16))) char lds[LY::BYTES];
   float *cf = reinterpret_cast<float *>(lds + LY::COEF);
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       const int64_t off = (row_base + r) * K + k0;
       ra[i] = *reinterpret_cast<const u32x4 *>(Ag + off);
       if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const u32x4 *>(A2g + off);
-      if constexpr (MASK) mk[i] = a.a_mask[off >> 3];
+      if constexpr (AMASK) mk[i] = a.a_mask[off >> 3];
       rb[i] = *reinterpret_cast<const u32x4 *>(Wg + (int64_t)(n0 + srow + 64 * i) * K + k0);
     }
   };
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
           float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
-          if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
+          if constexpr (AMASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
           v[e] = x;
         }
       } else if constexpr (PRO == PCS_PRO_BWD) {
@@ -297,7 +300,6 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       pmx[e] = -__builtin_huge_valf(); pmn[e] = __builtin_huge_valf();
       pmxi[e] = 0x7fffffff; pmni[e] = 0x7fffffff;
     }
-    float cnt = 0.f;
     if constexpr (EPI == PCS_EPI_FWD) {
 #pragma unroll 4
       for (int p = 0; p < NPASS; ++p) {
@@ -308,14 +310,11 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
           if (do_stats || do_pool) {
             float v[EPC];
             unpack_chunk(raw, v);
-            if (do_stats) {
-              cnt += 1.f;
-              const float rn = 1.f / cnt;
+            if (do_stats) {   // plain sums over this thread's <= 16 rows (bf16 data)
 #pragma unroll
               for (int e = 0; e < EPC; ++e) {
-                const float d = v[e] - sa[e];
-                sa[e] = fmaf(d, rn, sa[e]);
-                sb[e] = fmaf(d, v[e] - sa[e], sb[e]);
+                sa[e] += v[e];
+                sb[e] = fmaf(v[e], v[e], sb[e]);
               }
             }
             if (do_pool) {
@@ -332,11 +331,10 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     } else if constexpr (EPI == PCS_EPI_DGRAD) {
       const bf16_t *Ypg = reinterpret_cast<const bf16_t *>(a.Yp);
       const bf16_t *Addg = reinterpret_cast<const bf16_t *>(a.addend);
-      float es[EPC], et[EPC], em[EPC], er[EPC];
+      float es[EPC], et[EPC];
       const int lc = ecc * EPC;
       lds_vec8(ecf + lc, es); lds_vec8(ecf + BN + lc, et);
-      lds_vec8(ecf + 2 * BN + lc, em); lds_vec8(ecf + 3 * BN + lc, er);
-      const float ks = a.c_mask ? a.c_keep_scale : 1.f;
+      const float ks = a.c_keep_scale;
       constexpr int BATCH = 4;
 #pragma unroll
       for (int p0 = 0; p0 < NPASS; p0 += BATCH) {
@@ -347,26 +345,31 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
           const int rr = min(er0 + RPP * (p0 + q), valid - 1);
           const int64_t goff = (row_base + rr) * Ncols + ecol;
           yv[q] = *reinterpret_cast<const u32x4 *>(Ypg + goff);
-          adv[q] = Addg ? *reinterpret_cast<const u32x4 *>(Addg + goff) : mk_u32x4(0, 0, 0, 0);
-          mb[q] = a.c_mask ? a.c_mask[goff >> 3] : 0xffu;
+          if constexpr (ADD) adv[q] = *reinterpret_cast<const u32x4 *>(Addg + goff);
+          if constexpr (CMASK) mb[q] = a.c_mask[goff >> 3];
         }
 #pragma unroll
         for (int q = 0; q < BATCH; ++q) {
           const int rr = er0 + RPP * (p0 + q);
           if (rr < valid) {
             const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
-            float v[EPC], y[EPC], ad[EPC];
+            float v[EPC], y[EPC];
             unpack_chunk(raw, v);
             unpack_chunk(yv[q], y);
-            unpack_chunk(adv[q], ad);
+            if constexpr (ADD) {
+              float ad[EPC];
+              unpack_chunk(adv[q], ad);
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) v[e] += ad[e];
+            }
 #pragma unroll
             for (int e = 0; e < EPC; ++e) {
-              float g = v[e] + ad[e];
-              g *= ((mb[q] >> e) & 1u) ? ks : 0.f;
+              float g = v[e];
+              if constexpr (CMASK) g = ((mb[q] >> e) & 1u) ? g * ks : 0.f;
               const float dz = fmaf(y[e], es[e], et[e]) > 0.f ? g : 0.f;
               v[e] = dz;
-              sa[e] += dz;                                       // S1
-              sb[e] = fmaf(dz, (y[e] - em[e]) * er[e], sb[e]);   // S2
+              sa[e] += dz;                  // S1
+              sb[e] = fmaf(dz, y[e], sb[e]);  // sum dz*y; S2 = rstd*(sum dz*y - mean*S1)
             }
             *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) = pack_chunk(v);
           }
@@ -401,8 +404,9 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
             float n = run_n, mean = run[c], m2 = run[BN + c];
             for (int j = 0; j < RPP; ++j) {
               const float nj = valid > j ? (float)((valid - j + RPP - 1) / RPP) : 0.f;
-              const float2 q = ps[j * BN + c];
-              chan_merge(n, mean, m2, nj, q.x, q.y);
+              const float2 q = ps[j * BN + c];   // (sum, sum of squares) of nj rows
+              const float mj = nj > 0.f ? q.x / nj : 0.f;
+              chan_merge(n, mean, m2, nj, mj, fmaxf(q.y - q.x * mj, 0.f));
             }
             run[c] = mean; run[BN + c] = m2;
           } else {
@@ -437,18 +441,22 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   // chunk end: this workgroup's per-column partials (same layout as gemm_nt)
   if (EPI != PCS_EPI_RAW && tid < BN) {
     const int64_t o = (int64_t)chunk * Ncols + n0 + tid;
-    if (do_stats) *reinterpret_cast<float2 *>(a.stats + o * 2) = make_float2(run[tid], run[BN + tid]);
+    if (do_stats) {
+      float s2 = run[BN + tid];
+      if constexpr (EPI == PCS_EPI_DGRAD) s2 = ecf[3 * BN + tid] * (s2 - ecf[2 * BN + tid] * run[tid]);
+      *reinterpret_cast<float2 *>(a.stats + o * 2) = make_float2(run[tid], s2);
+    }
     if (do_pool)
       *reinterpret_cast<float4 *>(a.pool + o * 4) =
           make_float4(run[2 * BN + tid], run[3 * BN + tid], run[4 * BN + tid], run[5 * BN + tid]);
   }
 }
 
-template <int PRO, int EPI, bool MASK>
+template <int PRO, int EPI, bool MASK, bool ADD = false>
 int launch(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
   const int ncb = a.Ncols / BN;
   const int nb = ncb * (int)(a.num_scenes * a.chunks_per_scene);
-  hipLaunchKernelGGL((gemm_big_kernel<PRO, EPI, MASK>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc, ncb);
+  hipLaunchKernelGGL((gemm_big_kernel<PRO, EPI, MASK, ADD>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc, ncb);
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -460,7 +468,9 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
   if (a.flags & PCS_FLAG_GENERIC) return false;
   if (a.a_mask && a.prologue != PCS_PRO_BNRELU) return false;
   if (a.epilogue == PCS_EPI_FWD) return a.prologue == PCS_PRO_BNRELU;
-  if (a.epilogue == PCS_EPI_DGRAD) return a.prologue == PCS_PRO_BWD || a.prologue == PCS_PRO_BWD_POOL;
+  if (a.epilogue == PCS_EPI_DGRAD)   // BWD_POOL (global_feat) has neither a mask nor an addend
+    return a.prologue == PCS_PRO_BWD ? !(a.c_mask && a.addend)
+                                     : a.prologue == PCS_PRO_BWD_POOL && !a.c_mask && !a.addend;
   if (a.epilogue == PCS_EPI_RAW) return a.prologue == PCS_PRO_BWD || a.prologue == PCS_PRO_BWD_POOL;
   return false;
 }
@@ -471,8 +481,10 @@ int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s)
       return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
     case PCS_EPI_DGRAD:
-      return g.prologue == PCS_PRO_BWD_POOL ? launch<PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(g, tps, tpc, s)
-                                            : launch<PCS_PRO_BWD, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
+      if (g.prologue == PCS_PRO_BWD_POOL) return launch<PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
+      if (g.c_mask) return launch<PCS_PRO_BWD, PCS_EPI_DGRAD, true>(g, tps, tpc, s);
+      if (g.addend) return launch<PCS_PRO_BWD, PCS_EPI_DGRAD, false, true>(g, tps, tpc, s);
+      return launch<PCS_PRO_BWD, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
     default:
       return g.prologue == PCS_PRO_BWD_POOL ? launch<PCS_PRO_BWD_POOL, PCS_EPI_RAW, false>(g, tps, tpc, s)
                                             : launch<PCS_PRO_BWD, PCS_EPI_RAW, false>(g, tps, tpc, s);
