@@ -273,6 +273,32 @@ int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weigh
 int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
                      uint8_t *bits, pcs_stream_t stream);
 
+/*
+ * Gram of the BN+ReLU activations a = relu(Y * s + t) (Y [M, C] scene-major rows, the
+ * stored pre-BN input of global_feat): G = a^T a (fp32 [C, C], symmetric, filled) and
+ * colsum[k] = sum_m a[m, k].  Used by pcs_gram_wgrad in place of the M x C x C weight-
+ * gradient GEMM of global_feat (autograd of P:113 at P:254).  pcs_gram_workspace returns
+ * the fp32 workspace bytes and the row splits per scene to pass to pcs_gram.
+ */
+int64_t pcs_gram_workspace(int64_t num_scenes, int64_t scene_rows, int32_t C, int32_t dtype,
+                           int32_t *splits_per_scene);
+int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, int64_t scene_rows,
+             int32_t C, int32_t dtype, int32_t splits_per_scene, float *workspace, float *G,
+             float *colsum, pcs_stream_t stream);
+
+/*
+ * global_feat weight gradient from the Gram (dy = beta + gamma*y + max-pool rows, y = a W^T):
+ *   dW[c, k] = beta[c] S[k] + gamma[c] sum_j W[c, j] G[j, k] + sum_b sp[b, c] a[am[b, c], k]
+ * W: fp32 [Cout, Cin] (row stride ldw_in), beta/gamma: bn_global backward coefficients,
+ * sp/am: [B, Cout] max-pool gradient and argmax rows (pcs_pool_bwd / pcs_pool_finalize),
+ * Y/s/t: the stored conv5 output and bn5 scale/shift (a recomputed at the argmax rows).
+ */
+int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_in,
+                   const float *beta, const float *gamma, const float *sp, const int32_t *am,
+                   const void *Y, const float *s, const float *t, int64_t num_scenes,
+                   int32_t Cout, int32_t Cin, int32_t dtype, float *dW, int64_t ldw,
+                   pcs_stream_t stream);
+
 /* out[i] = scale * sum_s partial[s*len + i]  (fixed order) */
 int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale,
                         float *out, int64_t out_stride_rows, int64_t row_len,

@@ -119,7 +119,8 @@ struct ChunkGeo {
   int chunks_per_scene;
 };
 
-PCS_DEV int64_t pcs_min64(int64_t a, int64_t b) { return a < b ? a : b; }
+__host__ __device__ inline int64_t pcs_min64(int64_t a, int64_t b) { return a < b ? a : b; }
+__host__ __device__ inline int64_t pcs_max64(int64_t a, int64_t b) { return a > b ? a : b; }
 
 // Scene-aligned chunk geometry: fills a->chunks_per_scene (auto when <= 0, aiming at
 // ~target workgroups over ncb column blocks) and returns rows per chunk.

@@ -9,6 +9,9 @@
 //   padded: the 8 rows one transposed read touches hit 8 distinct bank groups).
 // * the M reduction is split into scene-aligned row slices; each workgroup writes one
 //   fp32 partial tile and pcs_reduce_partials sums them in a fixed order.
+// * Gram mode (DYMODE = PCS_PRO_BNRELU, pcs_gram): both operands are a = relu(Y*s + t) of
+//   the same activations, only the upper 256-tiles of the symmetric a^T a are computed,
+//   and the diagonal tiles also sum their x columns (sum_m a[m, k]).
 #include "common.h"
 
 namespace {
@@ -66,7 +69,7 @@ PCS_DEV void lds8(const float *p, float (&v)[8]) {
 template <int DYMODE, bool MASK>
 PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_t rbase, int64_t rlast,
                       int bk, int cc, int r0, const u32x4 (&rz)[4], const u32x4 (&ry)[4],
-                      const u32x4 (&rx)[4], const uint32_t (&mk)[4]) {
+                      const u32x4 (&rx)[4], const uint32_t (&mk)[4], bool diag, float (&csum)[8]) {
   char *tB = tA + OPB;
   float ca[8], cb[8], cg[8], xs[8], xt[8];
   int am[8];
@@ -93,6 +96,9 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_
       unpack_chunk(rz[i], v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+    } else if constexpr (DYMODE == PCS_PRO_BNRELU) {   // Gram: (beta, gamma) slots hold (s, t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(y[e], cb[e], cg[e]), 0.f);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -112,6 +118,12 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_
       if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.x_keep_scale : 0.f;
       w[e] = x;
     }
+    if constexpr (DYMODE == PCS_PRO_BNRELU) {
+      if (diag && ok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += w[e];
+      }
+    }
     u32x4 ox = pack_chunk(w);
     if (!ok) ox = mk_u32x4(0, 0, 0, 0);
     *reinterpret_cast<u32x4 *>(tB + prow(rl) * ROWB + cc * 16) = ox;
@@ -127,7 +139,15 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
   const int wm = wid >> 2, wn = wid & 3;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L / ntiles, tile = L % ntiles;
-  const int n0 = (tile / ntn) * TM, k0 = (tile % ntn) * TN;
+  int nt = tile / ntn, kt = tile % ntn;
+  if constexpr (DYMODE == PCS_PRO_BNRELU) {   // upper triangle: tile -> (nt <= kt)
+    int t = tile;
+    nt = 0;
+    while (t >= ntn - nt) { t -= ntn - nt; ++nt; }
+    kt = nt + t;
+  }
+  const int n0 = nt * TM, k0 = kt * TN;
+  const bool diag = nt == kt;
   const int sps = a.splits_per_scene;
   const int scene = split / sps, sis = split % sps;
   const int64_t N = a.scene_rows;
@@ -143,12 +163,17 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
   for (int c = tid; c < 256; c += THREADS) {
     if constexpr (DYMODE == PCS_PRO_BWD) {
       cf[c] = a.alpha[n0 + c];
-    } else {
+    } else if constexpr (DYMODE == PCS_PRO_BWD_POOL) {
       cf[c] = a.pool_coef[(int64_t)scene * Cout + n0 + c];
       reinterpret_cast<int *>(cf)[768 + c] = a.pool_idx[(int64_t)scene * Cout + n0 + c];
     }
-    cf[256 + c] = a.beta[n0 + c];
-    cf[512 + c] = a.gamma[n0 + c];
+    if constexpr (DYMODE == PCS_PRO_BNRELU) {
+      cf[256 + c] = a.s[n0 + c];
+      cf[512 + c] = a.t[n0 + c];
+    } else {
+      cf[256 + c] = a.beta[n0 + c];
+      cf[512 + c] = a.gamma[n0 + c];
+    }
     cf[1024 + c] = a.s[k0 + c];
     cf[1280 + c] = a.t[k0 + c];
   }
@@ -163,10 +188,11 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
   const int nsteps = (int)((hi - lo + MS - 1) / MS);
   u32x4 rz[4], ry[4], rx[4];
   uint32_t mk[4] = {0xffu, 0xffu, 0xffu, 0xffu};
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (nsteps > 0) {
     const int64_t rb = scene * N + lo;
     tn_load<DYMODE, MASK>(dZ, Yg, Xg, a.x_mask, rb, rlast, Cout, Cin, an, bk, r0, rz, ry, rx, mk);
-    tn_store<DYMODE, MASK>(a, lds, cf, rb, rlast, bk, cc, r0, rz, ry, rx, mk);
+    tn_store<DYMODE, MASK>(a, lds, cf, rb, rlast, bk, cc, r0, rz, ry, rx, mk, diag, csum);
     __syncthreads();
   }
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -192,7 +218,8 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
       }
     }
     if (st + 1 < nsteps)
-      tn_store<DYMODE, MASK>(a, lds + (buf ^ 1) * STAGE, cf, rb + MS, rlast, bk, cc, r0, rz, ry, rx, mk);
+      tn_store<DYMODE, MASK>(a, lds + (buf ^ 1) * STAGE, cf, rb + MS, rlast, bk, cc, r0, rz, ry, rx, mk,
+                             diag, csum);
     lds_barrier();
   }
   // lane holds dW[n = n0 + wm*128 + i*16 + (lane&15)][k = k0 + wn*64 + j*16 + 4*(lane>>4) + r]
@@ -207,30 +234,63 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
           make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
     }
   }
+  if constexpr (DYMODE == PCS_PRO_BNRELU) {   // column sums of a over this slice (diagonal tiles)
+    if (diag) {
+      __syncthreads();
+      float *red = reinterpret_cast<float *>(lds);   // [16 row groups][256 columns]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[r0 * 256 + cc * 8 + e] = csum[e];
+      __syncthreads();
+      if (tid < 256) {
+        float v = 0.f;
+        for (int j = 0; j < THREADS / 32; ++j) v += red[j * 256 + tid];
+        const int nsplit = gridDim.x / ntiles;
+        a.partial[(int64_t)nsplit * Cout * Cin + (int64_t)split * Cin + k0 + tid] = v;
+      }
+    }
+  }
 }
 
 }  // namespace
 
 bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a) {
-  return !(a.flags & PCS_FLAG_GENERIC) && a.dtype == PCS_BF16 && a.Cout % TM == 0 && a.Cin % TN == 0 && a.x_mode == PCS_PRO_BNRELU &&
-         (a.dy_mode == PCS_PRO_BWD || a.dy_mode == PCS_PRO_BWD_POOL);
+  if (a.dy_mode == PCS_PRO_BNRELU && (a.Cout != a.Cin || a.x_mask)) return false;   // Gram: square
+  return !(a.flags & PCS_FLAG_GENERIC) && a.dtype == PCS_BF16 && a.Cout % TM == 0 && a.Cin % TN == 0 &&
+         a.x_mode == PCS_PRO_BNRELU &&
+         (a.dy_mode == PCS_PRO_BWD || a.dy_mode == PCS_PRO_BWD_POOL || a.dy_mode == PCS_PRO_BNRELU);
+}
+
+int pcs_wgrad_big_tiles(const pcs_wgrad_args &a) {
+  const int ntm = a.Cout / TM, ntn = a.Cin / TN;
+  return a.dy_mode == PCS_PRO_BNRELU ? ntm * (ntm + 1) / 2 : ntm * ntn;
 }
 
 int pcs_wgrad_big_splits(const pcs_wgrad_args &a) {
-  const int64_t ntiles = (int64_t)(a.Cout / TM) * (a.Cin / TN);
-  int64_t sps = (256 + a.num_scenes * ntiles - 1) / (a.num_scenes * ntiles);  // 1 WG per CU
-  const int64_t max_sps = (a.scene_rows + 8 * MS - 1) / (8 * MS);
-  if (sps > max_sps) sps = max_sps;
-  if (sps < 1) sps = 1;
-  return (int)sps;
+  // one 512-thread workgroup per CU: pick the row splits per scene that minimise
+  // (waves of 256 workgroups) / splits, i.e. the time of the slowest CU, with the fp32
+  // partial slabs kept below 256 MB
+  const int64_t per_split = a.num_scenes * pcs_wgrad_big_tiles(a);
+  const int64_t slab = (int64_t)a.Cout * a.Cin * 4;
+  const int64_t max_sps = pcs_max64(1, pcs_min64((a.scene_rows + 8 * MS - 1) / (8 * MS),
+                                                 ((int64_t)256 << 20) / slab / a.num_scenes));
+  int64_t best = 1;
+  double best_cost = 1e30;
+  for (int64_t sps = 1; sps <= max_sps; ++sps) {
+    const double waves = (double)((per_split * sps + 255) / 256);
+    const double cost = waves / (double)sps * (1.0 + 1e-3 * sps);   // tie-break: fewer slabs
+    if (cost < best_cost) { best_cost = cost; best = sps; }
+  }
+  return (int)best;
 }
 
 int pcs_wgrad_big_launch(const pcs_wgrad_args &a, hipStream_t s) {
   int64_t rps = (a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene;
   rps = (rps + MS - 1) / MS * MS;
-  const int ntn = a.Cin / TN, ntiles = (a.Cout / TM) * ntn;
+  const int ntn = a.Cin / TN, ntiles = pcs_wgrad_big_tiles(a);
   const int nb = ntiles * (int)(a.num_scenes * a.splits_per_scene);
-  if (a.dy_mode == PCS_PRO_BWD_POOL) {
+  if (a.dy_mode == PCS_PRO_BNRELU) {
+    hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BNRELU, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+  } else if (a.dy_mode == PCS_PRO_BWD_POOL) {
     if (a.x_mask) hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD_POOL, true>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
     else hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD_POOL, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
   } else {

@@ -86,13 +86,22 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
   int am[EPC];
   if constexpr (DYMODE == PCS_PRO_BWD) {
     load_vec<EPC>(a.alpha, an, ca);
-  } else {
+  } else if constexpr (DYMODE == PCS_PRO_BWD_POOL) {
     load_vec<EPC>(a.pool_coef + scene * Cout, an, ca);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) am[e] = a.pool_idx[scene * Cout + an + e];
   }
-  load_vec<EPC>(a.beta, an, cb);
-  load_vec<EPC>(a.gamma, an, cg);
+  if constexpr (DYMODE == PCS_PRO_BNRELU) {   // Gram: dy = relu(y*s + t) of the same activations
+    load_vec<EPC>(a.s, an, cb);
+    load_vec<EPC>(a.t, an, cg);
+  } else {
+    load_vec<EPC>(a.beta, an, cb);
+    load_vec<EPC>(a.gamma, an, cg);
+  }
+  const bool diag = DYMODE == PCS_PRO_BNRELU && n0 == k0 && TM == TN;
+  float csum[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) csum[e] = 0.f;
   if constexpr (XMODE == PCS_PRO_BNRELU) {
     load_vec<EPC>(a.s, bk, xs);
     load_vec<EPC>(a.t, bk, xt);
@@ -133,6 +142,9 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
         unpack_chunk(rz[i], v);
 #pragma unroll
         for (int e = 0; e < EPC; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+      } else if constexpr (DYMODE == PCS_PRO_BNRELU) {
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v[e] = fmaxf(fmaf(y[e], cb[e], cg[e]), 0.f);
       } else {
         const int grow = (int)(scene * N + r);
 #pragma unroll
@@ -155,6 +167,10 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
           float x = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
           if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.x_keep_scale : 0.f;
           v[e] = x;
+        }
+        if (diag && r < hi) {
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) csum[e] += v[e];
         }
         out = pack_chunk(v);
       }
@@ -253,6 +269,19 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
           make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
     }
   }
+  if (diag) {   // Gram: column sums of the x operand over this slice
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(lds);   // [RP row groups][TN columns]
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) red[br0 * TN + bcc * EPC + e] = csum[e];
+    __syncthreads();
+    for (int c = tid; c < TN; c += THREADS) {
+      float v = 0.f;
+      for (int j = 0; j < OB::RP; ++j) v += red[j * TN + c];
+      const int nsplit = gridDim.x / ntiles;
+      a.partial[(int64_t)nsplit * Cout * Cin + (int64_t)split * Cin + k0 + c] = v;
+    }
+  }
 }
 
 template <typename T, int TM, int TN, int DY, int XM>
@@ -275,6 +304,8 @@ int dispatch_modes(const pcs_wgrad_args &a, int64_t rps, hipStream_t s) {
     if (a.x_mode == PCS_PRO_RAW) return launch<T, TM, TN, PCS_PRO_BWD, PCS_PRO_RAW>(a, rps, s);
   } else if (a.dy_mode == PCS_PRO_BWD_POOL) {
     if (a.x_mode == PCS_PRO_BNRELU) return launch<T, TM, TN, PCS_PRO_BWD_POOL, PCS_PRO_BNRELU>(a, rps, s);
+  } else if (a.dy_mode == PCS_PRO_BNRELU && a.x_mode == PCS_PRO_BNRELU && !a.x_mask) {
+    return launch<T, TM, TN, PCS_PRO_BNRELU, PCS_PRO_BNRELU>(a, rps, s);
   }
   return pcs_set_einval("pcs_wgrad", "unsupported dy_mode/x_mode");
 }
@@ -336,4 +367,77 @@ extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   const int64_t nslabs = a.num_scenes * a.splits_per_scene;
   return pcs_reduce_partials(a.partial, nslabs, (int64_t)a.Cout * a.Cin, 1.0f, a.dW,
                              a.ldw ? a.ldw : a.Cin, a.Cin, stream);
+}
+
+// ---------------------------------------------------------------------------------------
+// Gram of the BN+ReLU activations (global_feat weight gradient, see gram.hip)
+// ---------------------------------------------------------------------------------------
+namespace {
+
+pcs_wgrad_args gram_args(const void *Y, const float *s, const float *t, int64_t num_scenes,
+                         int64_t scene_rows, int32_t C, int32_t dtype, int32_t sps) {
+  pcs_wgrad_args a = {};
+  a.num_scenes = num_scenes; a.scene_rows = scene_rows; a.Cout = C; a.Cin = C; a.dtype = dtype;
+  a.splits_per_scene = sps; a.dy_mode = PCS_PRO_BNRELU; a.x_mode = PCS_PRO_BNRELU;
+  a.Y = Y; a.X = Y; a.s = s; a.t = t; a.x_keep_scale = 1.f;
+  return a;
+}
+
+// G[j][k] = sum over slices of the (j, k) partial, taken from the upper 256-tile of the pair
+// (the 256x256 kernel computes only those); colsum[k] = sum of the slices' column sums.
+__global__ void gram_reduce_kernel(const float *__restrict__ part, int nsplit, int C,
+                                   float *__restrict__ G, float *__restrict__ colsum) {
+  const int64_t n = (int64_t)C * C;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(idx / C), k = (int)(idx % C);
+    const int64_t src = (j >> 8) <= (k >> 8) ? idx : (int64_t)k * C + j;
+    float v = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) v += part[sp * n + src];
+    G[idx] = v;
+    if (idx < C) {
+      float c = 0.f;
+      for (int sp = 0; sp < nsplit; ++sp) c += part[nsplit * n + (int64_t)sp * C + idx];
+      colsum[idx] = c;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t pcs_gram_workspace(int64_t num_scenes, int64_t scene_rows, int32_t C, int32_t dtype,
+                                      int32_t *splits_per_scene) {
+  if (num_scenes <= 0 || scene_rows <= 0 || C <= 0 || C % 64 || !splits_per_scene)
+    return pcs_set_einval("pcs_gram_workspace", "bad geometry");
+  pcs_wgrad_args a = gram_args(nullptr, nullptr, nullptr, num_scenes, scene_rows, C, dtype, 0);
+  const int64_t g = pcs_wgrad_workspace(&a);
+  if (g < 0) return g;
+  *splits_per_scene = a.splits_per_scene;
+  return g + num_scenes * a.splits_per_scene * (int64_t)C * 4;
+}
+
+extern "C" int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, int64_t scene_rows,
+                        int32_t C, int32_t dtype, int32_t splits_per_scene, float *workspace, float *G,
+                        float *colsum, pcs_stream_t stream) {
+  if (!Y || !s || !t || !workspace || !G || !colsum || splits_per_scene <= 0)
+    return pcs_set_einval("pcs_gram", "missing operand or splits");
+  if (C % 64) return pcs_set_einval("pcs_gram", "C must be a multiple of 64");
+  pcs_wgrad_args a = gram_args(Y, s, t, num_scenes, scene_rows, C, dtype, splits_per_scene);
+  a.partial = workspace;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int rc;
+  if (pcs_wgrad_big_applicable(a)) {
+    rc = pcs_wgrad_big_launch(a, st);
+  } else {
+    const int ms = dtype == PCS_BF16 ? TnCfg<bf16_t>::MS : TnCfg<float>::MS;
+    const int64_t rps = rows_per_split_of(a, ms);
+    if (dtype == PCS_BF16) rc = dispatch_tiles<bf16_t>(a, rps, st);
+    else if (dtype == PCS_F32) rc = dispatch_tiles<float>(a, rps, st);
+    else return pcs_set_einval("pcs_gram", "bad dtype");
+  }
+  if (rc) return rc;
+  const int nsplit = (int)(num_scenes * splits_per_scene);
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(1024), dim3(256), 0, st, workspace, nsplit, C, G, colsum);
+  PCS_CHECK_LAUNCH();
+  return 0;
 }

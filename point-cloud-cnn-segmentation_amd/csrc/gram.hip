@@ -1,0 +1,94 @@
+// Weight gradient of global_feat (P:113, autograd at P:254) from the Gram of its input.
+//
+// The max-pool feeds bn_global's backward a dy of the form (see pcs_pool_bwd)
+//     dy[m, c] = beta[c] + gamma[c] * y[m, c] + [m == am[b, c]] * sp[b, c],
+// and y = a W^T with a = relu(bn5(Y5)) (bias-free centred storage), so
+//     dW = dy^T a = beta (x) S + diag(gamma) W G + sum_b sp[b, c] a[am[b, c], :]
+// with G = a^T a and S = column sums of a (pcs_gram).  This replaces the M x 1024 x 1024
+// weight-gradient GEMM by the symmetric Gram (upper tiles only) plus this O(C^3) assemble.
+#include "common.h"
+
+namespace {
+
+constexpr int TILE = 64, KC = 32, THREADS = 256;
+
+template <typename T>
+__global__ __launch_bounds__(THREADS) void gram_wgrad_kernel(
+    const float *__restrict__ G, const float *__restrict__ S, const float *__restrict__ W, int64_t ldwin,
+    const float *__restrict__ beta, const float *__restrict__ gamma, const float *__restrict__ sp,
+    const int *__restrict__ am, const T *__restrict__ Y, const float *__restrict__ s,
+    const float *__restrict__ t, int B, int Cout, int Cin, float *__restrict__ dW, int64_t ldw) {
+  __shared__ float Ws[TILE][KC + 1];
+  __shared__ float Gs[KC][TILE];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int c0 = blockIdx.y * TILE, k0 = blockIdx.x * TILE;
+  float acc[4][4] = {};
+  for (int j0 = 0; j0 < Cin; j0 += KC) {
+    for (int e = tid; e < TILE * KC; e += THREADS) {
+      const int r = e / KC, q = e % KC;
+      Ws[r][q] = W[(int64_t)(c0 + r) * ldwin + j0 + q];
+      const int gr = e / TILE, gq = e % TILE;
+      Gs[gr][gq] = G[(int64_t)(j0 + gr) * Cin + k0 + gq];
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int q = 0; q < KC; ++q) {
+      float wv[4], gv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wv[i] = Ws[ty * 4 + i][q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gv[j] = Gs[q][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(wv[i], gv[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = c0 + ty * 4 + i;
+    const float gc = gamma[c], bc = beta[c];
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + tx * 4 + j;
+      o[j] = fmaf(gc, acc[i][j], bc * S[k]);
+    }
+    for (int b = 0; b < B; ++b) {   // the max-pool rows: a recomputed from the stored Y
+      const float w = sp[(int64_t)b * Cout + c];
+      const int64_t m = am[(int64_t)b * Cout + c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + tx * 4 + j;
+        o[j] = fmaf(w, fmaxf(fmaf(load_elem(Y, m * Cin + k), s[k], t[k]), 0.f), o[j]);
+      }
+    }
+    *reinterpret_cast<float4 *>(dW + (int64_t)c * ldw + k0 + tx * 4) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+}  // namespace
+
+extern "C" int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_in,
+                              const float *beta, const float *gamma, const float *sp, const int32_t *am,
+                              const void *Y, const float *s, const float *t, int64_t num_scenes,
+                              int32_t Cout, int32_t Cin, int32_t dtype, float *dW, int64_t ldw,
+                              pcs_stream_t stream) {
+  if (!G || !S || !W || !beta || !gamma || !sp || !am || !Y || !s || !t || !dW)
+    return pcs_set_einval("pcs_gram_wgrad", "missing operand");
+  if (Cout % TILE || Cin % TILE || num_scenes <= 0 || ldw % 4 || ldw < Cin || ldw_in < Cin)
+    return pcs_set_einval("pcs_gram_wgrad", "Cout/Cin must be multiples of 64, ldw >= Cin (multiple of 4)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid(Cin / TILE, Cout / TILE);
+  if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(gram_wgrad_kernel<bf16_t>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
+                       sp, am, reinterpret_cast<const bf16_t *>(Y), s, t, (int)num_scenes, Cout, Cin, dW, ldw);
+  else if (dtype == PCS_F32)
+    hipLaunchKernelGGL(gram_wgrad_kernel<float>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
+                       sp, am, reinterpret_cast<const float *>(Y), s, t, (int)num_scenes, Cout, Cin, dW, ldw);
+  else
+    return pcs_set_einval("pcs_gram_wgrad", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

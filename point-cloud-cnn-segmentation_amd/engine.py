@@ -470,10 +470,22 @@ class Engine:
                    wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
                    Yp=ys["conv5"], es=pc5.scale, et=pc5.shift, emean=pc5.mean, erstd=pc5.rstd,
                    stats=st, tag="dgrad:global_feat")
-        keepalive.append(self._wgrad(
-            B, N, 1024, 1024, L.PRO_BWD_POOL, L.PRO_BNRELU, G("global_feat.weight"),
-            tag="wgrad:global_feat", Y=ys["global_feat"], beta=bg, gamma=gg, pool_idx=sv.am, pool_coef=sp,
-            X=ys["conv5"], s=pc5.scale, t=pc5.shift))
+        # global_feat weight gradient from the Gram of a5 = relu(bn5(y5)): the symmetric
+        # a5^T a5 (upper tiles) + an O(C^3) assemble instead of the M x 1024 x 1024 GEMM
+        gram = torch.empty(1024, 1024, dtype=torch.float32, device=dev)
+        colsum = torch.empty(1024, dtype=torch.float32, device=dev)
+        sps = ct.c_int32(0)
+        nbytes = L.load().pcs_gram_workspace(B, N, 1024, self.dt, ct.byref(sps))
+        ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
+        keepalive.append(ws)
+        self._launch("wgrad:global_feat", "pcs_gram", L.ptr(ys["conv5"]), L.ptr(pc5.scale), L.ptr(pc5.shift),
+                     B, N, 1024, self.dt, sps.value, L.ptr(ws), L.ptr(gram), L.ptr(colsum), s)
+        Wg = P["global_feat.weight"]
+        self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg),
+                     Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(ys["conv5"]),
+                     L.ptr(pc5.scale), L.ptr(pc5.shift), B, 1024, 1024, self.dt,
+                     L.ptr(G("global_feat.weight")), 1024, s)
+        keepalive.append((gram, colsum))
         bn_bwd("bn5", "conv5", st, cps5)
         dz5 = bufB
 

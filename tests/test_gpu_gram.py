@@ -1,0 +1,71 @@
+"""pcs_gram / pcs_gram_wgrad (global_feat weight gradient from the Gram of its input)
+against torch fp32 on the same operands: G = a^T a, colsum = sum_m a, and
+dW = beta S^T... + diag(gamma) W G + the max-pool rows (see csrc/gram.hip)."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _case(B, N, C, dtype, seed=0):
+    import pcs_amd._lib as L
+    g = torch.Generator().manual_seed(seed)
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    Y = (torch.randn(B * N, C, generator=g) * 0.7).to(tdt).to(DEV)
+    s = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    t = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    a = torch.relu(Y.float() * s + t)
+    dt = L.BF16 if dtype == "bf16" else L.F32
+    sps = ct.c_int32(0)
+    nbytes = L.load().pcs_gram_workspace(B, N, C, dt, ct.byref(sps))
+    assert nbytes > 0 and sps.value > 0
+    ws = torch.empty(nbytes // 4, device=DEV)
+    G = torch.empty(C, C, device=DEV)
+    S = torch.empty(C, device=DEV)
+    L.call("pcs_gram", L.ptr(Y), L.ptr(s), L.ptr(t), B, N, C, dt, sps.value, L.ptr(ws), L.ptr(G), L.ptr(S),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    return L, dt, Y, s, t, a, G, S
+
+
+@pytest.mark.parametrize("B,N,C,dtype", [(2, 700, 256, "bf16"),   # 256x256 kernel (upper tiles)
+                                         (3, 333, 128, "bf16"),   # generic bf16 kernel
+                                         (2, 257, 128, "fp32")])
+def test_gram_matches_torch(B, N, C, dtype):
+    L, dt, Y, s, t, a, G, S = _case(B, N, C, dtype)
+    ab = a.to(torch.bfloat16).float() if dtype == "bf16" else a   # MFMA operands are rounded
+    ref = (ab.double().T @ ab.double()).float()
+    err = (G - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (2e-5 if dtype == "fp32" else 1e-4), err
+    assert torch.equal(G, G.T)
+    serr = (S.double() - a.double().sum(0)).abs().max().item() / a.sum(0).abs().max().item()
+    assert serr < 1e-5, serr
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_gram_wgrad_matches_direct(dtype):
+    B, N, C = 2, 500, 256
+    L, dt, Y, s, t, a, G, S = _case(B, N, C, dtype, seed=1)
+    g = torch.Generator().manual_seed(7)
+    W = (torch.randn(C, C, generator=g) * 0.05).to(DEV)
+    beta = (torch.randn(C, generator=g) * 1e-2).to(DEV)
+    gamma = (torch.randn(C, generator=g) * 1e-2).to(DEV)
+    sp = torch.randn(B, C, generator=g).to(DEV)
+    am = (torch.randint(0, N, (B, C), generator=g) + torch.arange(B)[:, None] * N).int().to(DEV)
+    dW = torch.empty(C, C, device=DEV)
+    L.call("pcs_gram_wgrad", L.ptr(G), L.ptr(S), L.ptr(W), C, L.ptr(beta), L.ptr(gamma), L.ptr(sp), L.ptr(am),
+           L.ptr(Y), L.ptr(s), L.ptr(t), B, C, C, dt, L.ptr(dW), C, L.stream_ptr())
+    torch.cuda.synchronize()
+    # direct: dy = beta + gamma * (a W^T) + max-pool rows, dW = dy^T a  (float64)
+    ad, Wd = a.double(), W.double()
+    dy = beta.double() + gamma.double() * (ad @ Wd.T)
+    rows = am.long()
+    for b in range(B):
+        dy[rows[b], torch.arange(C, device=DEV)] += sp[b].double()
+    ref = dy.T @ ad
+    err = (dW.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (1e-5 if dtype == "fp32" else 5e-3), err
