@@ -38,13 +38,12 @@ LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (
 
 # bench tag -> HIP kernel symbol (as summarised from rocprofv3 in profiles/pmc_<round>.json)
 TAG_KERNEL = {
-    "wgrad:global_feat": "wgrad_big_kernel<3>",
-    "fwd:global_feat": "gemm_big_kernel<1, 0, false>",
-    "dgrad:global_feat": "gemm_big_kernel<3, 2, false>",
-    "bnrelu_bwd:global_feat": "bnrelu_bwd_kernel<unsigned short>",
-    "stats:global_feat": "colstats_kernel<unsigned short, true>",
+    "wgrad:global_feat": "wgrad_big_kernel<1, false>",          # Gram a5^T a5 (upper tiles)
+    "fwd:global_feat": "gemm_big_kernel<1, 0, false, false>",   # + BN stats + max-pool epilogue
+    "dgrad:global_feat": "gemm_big_kernel<3, 1, false, false>",  # + ReLU/BN5-backward epilogue
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_r01.json")
+GRAM_TILE_FRACTION = 10.0 / 16.0   # upper 256-tiles of the symmetric 1024 x 1024 Gram
 
 
 def pmc_traffic(tag, dtype):
@@ -64,11 +63,15 @@ def kernel_model(tag, M, ab):
         return None
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
+    if kind == "wgrad" and conv == "global_feat":   # Gram of a5: upper tiles, reads y5 once
+        return flops * GRAM_TILE_FRACTION, M * cin * ab
+    if conv == "conv5" and kind in ("dgrad", "wgrad"):   # folded form: dz5 + y4/128-wide out
+        return flops, M * (cout + cin) * ab
     if kind == "fwd":
         nbytes = M * (cin + cout) * ab
     elif kind == "dgrad":
         extra = 0 if conv == "global_feat" else cout      # pool path reads no dZ
-        nbytes = M * (cout + extra + 2 * cin) * ab
+        nbytes = M * (cout + extra + 2 * cin) * ab        # A (+dZ), Y_{l-1} in, dZ_{l-1} out
         if conv == "seg_conv1":
             nbytes = M * (2 * cout + cin) * ab
     else:  # wgrad

@@ -287,17 +287,31 @@ int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, 
              float *colsum, pcs_stream_t stream);
 
 /*
- * global_feat weight gradient from the Gram (dy = beta + gamma*y + max-pool rows, y = a W^T):
- *   dW[c, k] = beta[c] S[k] + gamma[c] sum_j W[c, j] G[j, k] + sum_b sp[b, c] a[am[b, c], k]
- * W: fp32 [Cout, Cin] (row stride ldw_in), beta/gamma: bn_global backward coefficients,
- * sp/am: [B, Cout] max-pool gradient and argmax rows (pcs_pool_bwd / pcs_pool_finalize),
- * Y/s/t: the stored conv5 output and bn5 scale/shift (a recomputed at the argmax rows).
+ * Weight gradient of a BN-fed layer from the Gram of its input a (G, S from pcs_gram):
+ *   dW[c, k] = alpha[c] R[c, k] + beta[c] S[k] + gamma[c] sum_j W[c, j] G[j, k]
+ *              + sum_b sp[b, c] a[am[b, c], k]
+ * i.e. dy^T a for dy = alpha*dz + beta + gamma*y (+ max-pool rows) and y = a W^T, without
+ * reading y.  global_feat (P:113): R = NULL, dy from the max-pool (sp/am: pcs_pool_bwd /
+ * pcs_pool_finalize; Y/s/t: stored conv5 output and bn5 scale/shift, a recomputed at the
+ * argmax rows).  conv5 (P:110): R = dz^T a (pcs_wgrad with dy_mode RAW), sp = NULL.
+ * W: fp32 [Cout, Cin] with row stride ldw_in; dW row stride ldw (multiple of 4).
  */
 int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_in,
                    const float *beta, const float *gamma, const float *sp, const int32_t *am,
                    const void *Y, const float *s, const float *t, int64_t num_scenes,
-                   int32_t Cout, int32_t Cin, int32_t dtype, float *dW, int64_t ldw,
-                   pcs_stream_t stream);
+                   int32_t Cout, int32_t Cin, int32_t dtype, const float *R, const float *alpha,
+                   float *dW, int64_t ldw, pcs_stream_t stream);
+
+/*
+ * Folded operands of the input gradient of a BN-fed layer y = a W^T (W fp32 [Cout, Cin],
+ * row stride ldw) with BN-backward coefficients (alpha, beta, gamma) over Cout:
+ *   dA = dz (diag(alpha) W) + a H + 1 c^T,  WsT = (diag(alpha) W)^T [Cin, Cout] (dtype),
+ *   c = W^T beta [Cin] (fp32),  H = W^T diag(gamma) W [Cin, Cin] (dtype).
+ * Two pcs_gemm launches then give dA without reading y (conv5 backward, P:110 at P:254).
+ */
+int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const float *alpha,
+                const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
+                pcs_stream_t stream);
 
 /* out[i] = scale * sum_s partial[s*len + i]  (fixed order) */
 int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale,

@@ -473,6 +473,8 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
         case PCS_PRO_BWD: return launch_t<T, BM, BN, PCS_PRO_BWD, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
         case PCS_PRO_BWD_POOL:
           return launch_t<T, BM, BN, PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
+        case PCS_PRO_BNRELU:   // a_{l-1} H (folded BN backward of a wide layer, see pcs_bn_fold)
+          return launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
         default: break;
       }
       break;

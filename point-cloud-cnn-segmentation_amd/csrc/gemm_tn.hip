@@ -94,7 +94,7 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
   if constexpr (DYMODE == PCS_PRO_BNRELU) {   // Gram: dy = relu(y*s + t) of the same activations
     load_vec<EPC>(a.s, an, cb);
     load_vec<EPC>(a.t, an, cg);
-  } else {
+  } else if constexpr (DYMODE != PCS_PRO_RAW) {
     load_vec<EPC>(a.beta, an, cb);
     load_vec<EPC>(a.gamma, an, cg);
   }
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
     for (int i = 0; i < OA::NCH; ++i) {
       const int64_t r = pcs_min64(m0 + ar0 + OA::RP * i, hi - 1);
       const int64_t off = (scene * N + r) * Cout + an;
-      if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
-      ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
+      if constexpr (DYMODE == PCS_PRO_BWD || DYMODE == PCS_PRO_RAW) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
+      if constexpr (DYMODE != PCS_PRO_RAW) ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
     }
 #pragma unroll
     for (int i = 0; i < OB::NCH; ++i) {
@@ -137,8 +137,10 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
       const int rl = ar0 + OA::RP * i;
       const int64_t r = m0 + rl;
       float y[EPC], v[EPC];
-      unpack_chunk(ry[i], y);
-      if constexpr (DYMODE == PCS_PRO_BWD) {
+      if constexpr (DYMODE != PCS_PRO_RAW) unpack_chunk(ry[i], y);
+      if constexpr (DYMODE == PCS_PRO_RAW) {   // dy = dZ as stored (scaled later, pcs_gram_wgrad)
+        unpack_chunk(rz[i], v);
+      } else if constexpr (DYMODE == PCS_PRO_BWD) {
         unpack_chunk(rz[i], v);
 #pragma unroll
         for (int e = 0; e < EPC; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
@@ -304,6 +306,8 @@ int dispatch_modes(const pcs_wgrad_args &a, int64_t rps, hipStream_t s) {
     if (a.x_mode == PCS_PRO_RAW) return launch<T, TM, TN, PCS_PRO_BWD, PCS_PRO_RAW>(a, rps, s);
   } else if (a.dy_mode == PCS_PRO_BWD_POOL) {
     if (a.x_mode == PCS_PRO_BNRELU) return launch<T, TM, TN, PCS_PRO_BWD_POOL, PCS_PRO_BNRELU>(a, rps, s);
+  } else if (a.dy_mode == PCS_PRO_RAW) {
+    if (a.x_mode == PCS_PRO_BNRELU) return launch<T, TM, TN, PCS_PRO_RAW, PCS_PRO_BNRELU>(a, rps, s);
   } else if (a.dy_mode == PCS_PRO_BNRELU && a.x_mode == PCS_PRO_BNRELU && !a.x_mask) {
     return launch<T, TM, TN, PCS_PRO_BNRELU, PCS_PRO_BNRELU>(a, rps, s);
   }
@@ -348,8 +352,9 @@ extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   if (!ap) return pcs_set_einval("pcs_wgrad", "null args");
   pcs_wgrad_args a = *ap;
   if (a.Cout % 64 || a.Cin % 64) return pcs_set_einval("pcs_wgrad", "Cout/Cin must be multiples of 64");
-  if (!a.Y || !a.X || !a.partial || !a.dW || !a.beta || !a.gamma)
-    return pcs_set_einval("pcs_wgrad", "missing operand");
+  if (!a.X || !a.partial || !a.dW) return pcs_set_einval("pcs_wgrad", "missing operand");
+  if (a.dy_mode == PCS_PRO_RAW ? !a.dZ : (!a.Y || !a.beta || !a.gamma))
+    return pcs_set_einval("pcs_wgrad", "dy operands missing (RAW: dZ; BWD/BWD_POOL: Y, beta, gamma)");
   if (a.dy_mode == PCS_PRO_BWD && (!a.dZ || !a.alpha)) return pcs_set_einval("pcs_wgrad", "PRO_BWD needs dZ, alpha");
   if (a.dy_mode == PCS_PRO_BWD_POOL && (!a.pool_idx || !a.pool_coef))
     return pcs_set_einval("pcs_wgrad", "PRO_BWD_POOL needs pool_idx, pool_coef");

@@ -483,15 +483,45 @@ class Engine:
         Wg = P["global_feat.weight"]
         self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg),
                      Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(ys["conv5"]),
-                     L.ptr(pc5.scale), L.ptr(pc5.shift), B, 1024, 1024, self.dt,
+                     L.ptr(pc5.scale), L.ptr(pc5.shift), B, 1024, 1024, self.dt, None, None,
                      L.ptr(G("global_feat.weight")), 1024, s)
         keepalive.append((gram, colsum))
         bn_bwd("bn5", "conv5", st, cps5)
         dz5 = bufB
 
-        st, cps = dgrad("conv5", "bn5", 128, 1024, dz5, ys["conv5"], "conv4", "bn4", bufA)
-        wgrad("conv5", "bn5", 128, 1024, dz5, ys["conv5"], "conv4", "bn4")
-        bn_bwd("bn4", "conv4", st, cps)
+        # conv5 (128 -> 1024) in folded form: neither gradient reads the wide y5 (gram.hip)
+        #   dA4 = dz5 (diag(alpha5) W5) + a4 (W5^T diag(gamma5) W5) + W5^T beta5
+        #   dW5 = diag(alpha5) dz5^T a4 + beta5 (x) colsum(a4) + diag(gamma5) W5 (a4^T a4)
+        al5, be5, ga5 = coefs["bn5"]
+        pc4 = sv.bn["bn4"]
+        W5 = P["conv5.weight"]
+        ws_t = self._empty(128, 1024, device=dev)
+        c5 = torch.empty(128, dtype=torch.float32, device=dev)
+        h4 = self._empty(128, 128, device=dev)
+        L.call("pcs_bn_fold", L.ptr(W5), 1024, 128, 128, L.ptr(al5), L.ptr(be5), L.ptr(ga5), self.dt,
+               L.ptr(ws_t), L.ptr(c5), L.ptr(h4), s)
+        pbuf = self._empty(M, 128, device=dev)
+        self._gemm(B, N, 1024, 128, L.PRO_RAW, L.EPI_FWD, dz5, ws_t, pbuf, bias=c5, tag="dgrad:conv5")
+        cps4, _ = self.geometry(B, N, 128, 128, L.PRO_BNRELU, L.EPI_DGRAD)
+        st = torch.empty(B * cps4, 128, 2, dtype=torch.float32, device=dev)
+        self._gemm(B, N, 128, 128, L.PRO_BNRELU, L.EPI_DGRAD, ys["conv4"], h4, bufA, pa=pc4.scale,
+                   pb=pc4.shift, Yp=ys["conv4"], es=pc4.scale, et=pc4.shift, emean=pc4.mean,
+                   erstd=pc4.rstd, addend=pbuf, stats=st, tag="dgrad2:conv5")
+        r5 = torch.empty(1024, 128, dtype=torch.float32, device=dev)
+        keepalive.append(self._wgrad(B, N, 1024, 128, L.PRO_RAW, L.PRO_BNRELU, r5, tag="wgrad:conv5",
+                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift))
+        g4 = torch.empty(128, 128, dtype=torch.float32, device=dev)
+        s4 = torch.empty(128, dtype=torch.float32, device=dev)
+        sps4 = ct.c_int32(0)
+        nbytes = L.load().pcs_gram_workspace(B, N, 128, self.dt, ct.byref(sps4))
+        ws4 = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
+        self._launch("gram:conv4", "pcs_gram", L.ptr(ys["conv4"]), L.ptr(pc4.scale), L.ptr(pc4.shift), B, N,
+                     128, self.dt, sps4.value, L.ptr(ws4), L.ptr(g4), L.ptr(s4), s)
+        self._launch("wgrad_asm:conv5", "pcs_gram_wgrad", L.ptr(g4), L.ptr(s4), L.ptr(W5), 128, L.ptr(be5),
+                     L.ptr(ga5), None, None, None, None, None, B, 1024, 128, self.dt, L.ptr(r5), L.ptr(al5),
+                     L.ptr(G("conv5.weight")), 128, s)
+        keepalive.append((ws_t, c5, h4, pbuf, r5, g4, s4, ws4))
+        bn_bwd("bn4", "conv4", st, cps4)
         dz4 = bufA
         st, cps = dgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3", bufB)
         wgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3")

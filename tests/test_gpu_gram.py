@@ -58,7 +58,7 @@ def test_gram_wgrad_matches_direct(dtype):
     am = (torch.randint(0, N, (B, C), generator=g) + torch.arange(B)[:, None] * N).int().to(DEV)
     dW = torch.empty(C, C, device=DEV)
     L.call("pcs_gram_wgrad", L.ptr(G), L.ptr(S), L.ptr(W), C, L.ptr(beta), L.ptr(gamma), L.ptr(sp), L.ptr(am),
-           L.ptr(Y), L.ptr(s), L.ptr(t), B, C, C, dt, L.ptr(dW), C, L.stream_ptr())
+           L.ptr(Y), L.ptr(s), L.ptr(t), B, C, C, dt, None, None, L.ptr(dW), C, L.stream_ptr())
     torch.cuda.synchronize()
     # direct: dy = beta + gamma * (a W^T) + max-pool rows, dW = dy^T a  (float64)
     ad, Wd = a.double(), W.double()
