@@ -313,6 +313,18 @@ int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const fl
                 const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
                 pcs_stream_t stream);
 
+/*
+ * Confusion matrix of argmax predictions (P:261-266 accuracy, P:314-346 F1 / mIoU inputs):
+ * cm[y, argmax_c logits[m, c]] += 1 for every point m with 0 <= labels[m] < C (labels -1 =
+ * padding are skipped).  logits: fp32 rows of stride ld; cm: int64 [C, C], accumulated
+ * (zero it once per epoch).  C <= 32.
+ */
+int pcs_confusion(const float *logits, int64_t ld, const int64_t *labels, int64_t M, int32_t C,
+                  int64_t *cm, pcs_stream_t stream);
+
+/* out[m] = argmax_c logits[m, c] (first maximum; int64), the inference path of P:448-452 */
+int pcs_argmax(const float *logits, int64_t ld, int64_t M, int32_t C, int64_t *out, pcs_stream_t stream);
+
 /* out[i] = scale * sum_s partial[s*len + i]  (fixed order) */
 int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale,
                         float *out, int64_t out_stride_rows, int64_t row_len,

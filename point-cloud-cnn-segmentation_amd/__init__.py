@@ -17,6 +17,10 @@ _LAZY = {
     "FusedAdam": ("optim", "FusedAdam"),
     "collate_fn": ("data", "collate_fn"),
     "load_reference_checkpoint": ("model", "load_reference_checkpoint"),
+    "save_checkpoint": ("checkpoint", "save_checkpoint"),
+    "load_checkpoint": ("checkpoint", "load_checkpoint"),
+    "predict": ("checkpoint", "predict"),
+    "ConfusionMeter": ("metrics", "ConfusionMeter"),
 }
 
 
@@ -25,7 +29,7 @@ def __getattr__(name):
         import importlib
         mod, attr = _LAZY[name]
         return getattr(importlib.import_module(f"{__name__}.{mod}"), attr)
-    if name in ("data", "model", "optim", "train", "engine"):
+    if name in ("data", "model", "optim", "train", "engine", "metrics", "checkpoint"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
     raise AttributeError(name)

@@ -117,6 +117,8 @@ SIGNATURES = [
     ("pcs_gram_wgrad", ct.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
                                   _i32, _vp, _vp, _vp, _i64, _vp]),
     ("pcs_bn_fold", ct.c_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    ("pcs_confusion", ct.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),
+    ("pcs_argmax", ct.c_int, [_vp, _i64, _i64, _i32, _vp, _vp]),
     ("pcs_last_error", ct.c_char_p, []),
 ]
 

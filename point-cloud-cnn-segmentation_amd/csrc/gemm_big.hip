@@ -130,16 +130,28 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   u32x4 ra[4], ra2[4], rb[4];
   uint32_t mk[4];
   uint32_t hits = 0;   // POOL: bit i set if staging row srow + 64 i is an argmax row of the tile
-  auto load_stage = [&](int64_t row_base, int valid, int ks) {
-    const int k0 = ks * BK + slot * EPC;
+  // Staging addresses: a uniform (SGPR) base per tile and k-step plus per-thread 32-bit byte
+  // offsets computed once per tile (rows clamped to the tile's valid rows), so the loads use
+  // the saddr + voffset form instead of 64-bit VALU address arithmetic every k-step.
+  uint32_t woff[4], aoff[4], aoff_next[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) woff[i] = (uint32_t)(((srow + 64 * i) * K + slot * EPC) * 2);
+  const char *wbase0 = reinterpret_cast<const char *>(Wg + (int64_t)n0 * K);
+  auto row_offs = [&](int valid_rows, uint32_t (&o)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (uint32_t)((min(srow + 64 * i, valid_rows - 1) * K + slot * EPC) * 2);
+  };
+  auto load_stage = [&](int64_t row_base, const uint32_t (&o)[4], int ks) {
+    const int64_t e0 = row_base * K + (int64_t)ks * BK;   // element offset of (row_base, k-step)
+    const char *ab = reinterpret_cast<const char *>(Ag + e0);
+    const char *wb = wbase0 + ks * BK * 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = min(srow + 64 * i, valid - 1);
-      const int64_t off = (row_base + r) * K + k0;
-      ra[i] = *reinterpret_cast<const u32x4 *>(Ag + off);
-      if constexpr (PRO == PCS_PRO_BWD) ra2[i] = *reinterpret_cast<const u32x4 *>(A2g + off);
-      if constexpr (AMASK) mk[i] = a.a_mask[off >> 3];
-      rb[i] = *reinterpret_cast<const u32x4 *>(Wg + (int64_t)(n0 + srow + 64 * i) * K + k0);
+      ra[i] = *reinterpret_cast<const u32x4 *>(ab + o[i]);
+      if constexpr (PRO == PCS_PRO_BWD)
+        ra2[i] = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(A2g + e0) + o[i]);
+      if constexpr (AMASK) mk[i] = (a.a_mask + (e0 >> 3))[o[i] >> 4];
+      rb[i] = *reinterpret_cast<const u32x4 *>(wb + woff[i]);
     }
   };
   auto store_stage = [&](int64_t row_base, int ks, int buf) {
@@ -191,7 +203,8 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
 
   int64_t row_base = scene * N + (int64_t)t_begin * BM;
   int valid = tile_rows(t_begin);
-  load_stage(row_base, valid, 0);
+  row_offs(valid, aoff);
+  load_stage(row_base, aoff, 0);
   __syncthreads();   // coefficients visible
 
   for (int tile = t_begin; tile < t_end; ++tile) {
@@ -200,10 +213,14 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     // ONE load site per k-step (two sites make the compiler merge their registers with
     // copies that wait for the loads): step ks_next of this tile, else step 0 of the next
     // tile, else a harmless in-bounds reload that is never consumed.
+    row_offs(next_valid > 0 ? next_valid : 1, aoff_next);
     auto prefetch = [&](int ks_next) {
       const bool tail = ks_next >= nks;
       const bool nxt = tail && next_valid > 0;
-      load_stage(nxt ? next_base : row_base, nxt ? next_valid : valid, tail ? 0 : ks_next);
+      uint32_t o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = nxt ? aoff_next[i] : aoff[i];
+      load_stage(nxt ? next_base : row_base, o, tail ? 0 : ks_next);
     };
     if constexpr (PRO == PCS_PRO_BWD_POOL) {   // bitmap of the tile's argmax rows
       if (tid < BM / 32) tbits[tid] = 0u;
@@ -436,6 +453,8 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     run_n += (float)valid;
     row_base = next_base;
     valid = next_valid;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i] = aoff_next[i];
   }
 
   // chunk end: this workgroup's per-column partials (same layout as gemm_nt)
@@ -467,7 +486,7 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 128 || a.K > KMAX) return false;
   if (a.flags & PCS_FLAG_GENERIC) return false;
   if (a.a_mask && a.prologue != PCS_PRO_BNRELU) return false;
-  if (a.epilogue == PCS_EPI_FWD) return a.prologue == PCS_PRO_BNRELU;
+  if (a.epilogue == PCS_EPI_FWD) return a.prologue == PCS_PRO_BNRELU || a.prologue == PCS_PRO_RAW;
   if (a.epilogue == PCS_EPI_DGRAD)   // BWD_POOL (global_feat) has neither a mask nor an addend
     return a.prologue == PCS_PRO_BWD ? !(a.c_mask && a.addend)
                                      : a.prologue == PCS_PRO_BWD_POOL && !a.c_mask && !a.addend;
@@ -478,6 +497,7 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
 int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s) {
   switch (g.epilogue) {
     case PCS_EPI_FWD:
+      if (g.prologue == PCS_PRO_RAW) return launch<PCS_PRO_RAW, PCS_EPI_FWD, false>(g, tps, tpc, s);
       return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
     case PCS_EPI_DGRAD:
