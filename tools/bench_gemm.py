@@ -64,6 +64,7 @@ def main():
 
     fwd = dict(pa=s, pb=t)
     run("fwd store", L.PRO_BNRELU, L.EPI_FWD, **fwd)
+    run("fwd store, RAW prologue (no BN+ReLU)", L.PRO_RAW, L.EPI_FWD)
     run("fwd store+stats", L.PRO_BNRELU, L.EPI_FWD, stats=True, **fwd)
     run("fwd store+stats+pool", L.PRO_BNRELU, L.EPI_FWD, stats=True, pool=True, **fwd)
     run("fwd stats+pool (no store)", L.PRO_BNRELU, L.EPI_FWD, stats=True, pool=True, C=None, **fwd)
