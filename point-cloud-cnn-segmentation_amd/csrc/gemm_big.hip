@@ -317,7 +317,14 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       pmx[e] = -__builtin_huge_valf(); pmn[e] = __builtin_huge_valf();
       pmxi[e] = 0x7fffffff; pmni[e] = 0x7fffffff;
     }
+    // tile statistics are shifted by the tile's first row (same shift for every thread of a
+    // column): per-thread sums of d = v - K, plain adds across threads, one Chan merge per
+    // column per tile
+    float ksh[EPC];
+    float kc = 0.f;   // merge thread tid < BN: the shift of column tid
     if constexpr (EPI == PCS_EPI_FWD) {
+      unpack_chunk(*reinterpret_cast<const u32x4 *>(lds + ecc * 16), ksh);
+      if (tid < BN) kc = bf2f(*reinterpret_cast<const unsigned short *>(lds + tid * 2));
 #pragma unroll 4
       for (int p = 0; p < NPASS; ++p) {
         const int rr = er0 + RPP * p;
@@ -327,11 +334,12 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
           if (do_stats || do_pool) {
             float v[EPC];
             unpack_chunk(raw, v);
-            if (do_stats) {   // plain sums over this thread's <= 16 rows (bf16 data)
+            if (do_stats) {
 #pragma unroll
               for (int e = 0; e < EPC; ++e) {
-                sa[e] += v[e];
-                sb[e] = fmaf(v[e], v[e], sb[e]);
+                const float d = v[e] - ksh[e];
+                sa[e] += d;
+                sb[e] = fmaf(d, d, sb[e]);
               }
             }
             if (do_pool) {
@@ -418,13 +426,15 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
         const int c = tid;
         if (do_stats) {
           if constexpr (EPI == PCS_EPI_FWD) {
-            float n = run_n, mean = run[c], m2 = run[BN + c];
+            float s1 = 0.f, s2 = 0.f;   // shifted sums of the tile's valid rows
+#pragma unroll
             for (int j = 0; j < RPP; ++j) {
-              const float nj = valid > j ? (float)((valid - j + RPP - 1) / RPP) : 0.f;
-              const float2 q = ps[j * BN + c];   // (sum, sum of squares) of nj rows
-              const float mj = nj > 0.f ? q.x / nj : 0.f;
-              chan_merge(n, mean, m2, nj, mj, fmaxf(q.y - q.x * mj, 0.f));
+              const float2 q = ps[j * BN + c];
+              s1 += q.x; s2 += q.y;
             }
+            const float nt = (float)valid, d1 = s1 / nt;
+            float n = run_n, mean = run[c], m2 = run[BN + c];
+            chan_merge(n, mean, m2, nt, kc + d1, fmaxf(s2 - s1 * d1, 0.f));
             run[c] = mean; run[BN + c] = m2;
           } else {
             float s1 = run[c], s2 = run[BN + c];
