@@ -388,24 +388,18 @@ pcs_wgrad_args gram_args(const void *Y, const float *s, const float *t, int64_t 
   return a;
 }
 
-// G[j][k] = sum over slices of the (j, k) partial, taken from the upper 256-tile of the pair
-// (the 256x256 kernel computes only those); colsum[k] = sum of the slices' column sums.
-__global__ void gram_reduce_kernel(const float *__restrict__ part, int nsplit, int C,
-                                   float *__restrict__ G, float *__restrict__ colsum) {
-  const int64_t n = (int64_t)C * C;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int j = (int)(idx / C), k = (int)(idx % C);
-    const int64_t src = (j >> 8) <= (k >> 8) ? idx : (int64_t)k * C + j;
-    float v = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) v += part[sp * n + src];
-    G[idx] = v;
-    if (idx < C) {
-      float c = 0.f;
-      for (int sp = 0; sp < nsplit; ++sp) c += part[nsplit * n + (int64_t)sp * C + idx];
-      colsum[idx] = c;
-    }
-  }
+// Mirror the upper 64x64 tiles of the summed Gram into the lower ones (the 256x256 kernel
+// computes only upper tiles; a transposed copy through LDS keeps both sides coalesced).
+__global__ __launch_bounds__(256) void gram_mirror_kernel(float *__restrict__ G, int C) {
+  __shared__ float tile[64][65];
+  const int nt = C / 64;
+  int t = blockIdx.x, tj = 0;
+  while (t >= nt - 1 - tj) { t -= nt - 1 - tj; ++tj; }   // strictly upper pairs (tj < tk)
+  const int tk = tj + 1 + t;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) tile[r][tx] = G[(int64_t)(tj * 64 + r) * C + tk * 64 + tx];
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) G[(int64_t)(tk * 64 + r) * C + tj * 64 + tx] = tile[tx][r];
 }
 
 }  // namespace
@@ -442,7 +436,13 @@ extern "C" int pcs_gram(const void *Y, const float *s, const float *t, int64_t n
   }
   if (rc) return rc;
   const int nsplit = (int)(num_scenes * splits_per_scene);
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(1024), dim3(256), 0, st, workspace, nsplit, C, G, colsum);
-  PCS_CHECK_LAUNCH();
+  const int64_t n = (int64_t)C * C;
+  if ((rc = pcs_reduce_partials(workspace, nsplit, n, 1.f, G, C, C, stream))) return rc;
+  if ((rc = pcs_reduce_partials(workspace + nsplit * n, nsplit, C, 1.f, colsum, C, C, stream))) return rc;
+  const int nt = C / 64;
+  if (nt > 1) {
+    hipLaunchKernelGGL(gram_mirror_kernel, dim3(nt * (nt - 1) / 2), dim3(256), 0, st, G, C);
+    PCS_CHECK_LAUNCH();
+  }
   return 0;
 }

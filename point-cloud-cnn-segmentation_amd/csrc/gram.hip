@@ -130,16 +130,26 @@ __global__ void fold_wt_kernel(const float *__restrict__ W, int64_t ldw, int Cou
   }
 }
 
-// H[i][j] = sum_k W[k][i] gamma[k] W[k][j]   (one block per row i)
+// H[i][j] = sum_k W[k][i] gamma[k] W[k][j]: block = row i, 4 parts of k (fixed-order combine)
 template <typename T>
-__global__ void fold_h_kernel(const float *__restrict__ W, int64_t ldw, int Cout, int Cin,
-                              const float *__restrict__ gamma, T *__restrict__ H) {
-  const int i = blockIdx.x;
-  for (int j = threadIdx.x; j < Cin; j += blockDim.x) {
+__global__ __launch_bounds__(256) void fold_h_kernel(const float *__restrict__ W, int64_t ldw, int Cout, int Cin,
+                                                     const float *__restrict__ gamma, T *__restrict__ H) {
+  __shared__ float red[4][64];
+  const int i = blockIdx.x, jj = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int k0 = (int)((int64_t)Cout * pr / 4), k1 = (int)((int64_t)Cout * (pr + 1) / 4);
+  for (int j0 = 0; j0 < Cin; j0 += 64) {
+    const int j = j0 + jj;
     float acc = 0.f;
-    for (int k = 0; k < Cout; ++k) acc = fmaf(W[(int64_t)k * ldw + i] * gamma[k], W[(int64_t)k * ldw + j], acc);
-    if constexpr (sizeof(T) == 2) H[(int64_t)i * Cin + j] = (T)(pack2bf(acc, 0.f) & 0xffffu);
-    else H[(int64_t)i * Cin + j] = acc;
+    if (j < Cin)
+      for (int k = k0; k < k1; ++k) acc = fmaf(W[(int64_t)k * ldw + i] * gamma[k], W[(int64_t)k * ldw + j], acc);
+    red[pr][jj] = acc;
+    __syncthreads();
+    if (pr == 0 && j < Cin) {
+      const float v = ((red[0][jj] + red[1][jj]) + red[2][jj]) + red[3][jj];
+      if constexpr (sizeof(T) == 2) H[(int64_t)i * Cin + j] = (T)(pack2bf(v, 0.f) & 0xffffu);
+      else H[(int64_t)i * Cin + j] = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -155,12 +165,12 @@ extern "C" int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ld
   if (dtype == PCS_BF16) {
     hipLaunchKernelGGL(fold_wt_kernel<bf16_t>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, beta,
                        reinterpret_cast<bf16_t *>(WsT), c);
-    hipLaunchKernelGGL(fold_h_kernel<bf16_t>, dim3(Cin), dim3(128), 0, st, W, ldw, Cout, Cin, gamma,
+    hipLaunchKernelGGL(fold_h_kernel<bf16_t>, dim3(Cin), dim3(256), 0, st, W, ldw, Cout, Cin, gamma,
                        reinterpret_cast<bf16_t *>(H));
   } else if (dtype == PCS_F32) {
     hipLaunchKernelGGL(fold_wt_kernel<float>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, beta,
                        reinterpret_cast<float *>(WsT), c);
-    hipLaunchKernelGGL(fold_h_kernel<float>, dim3(Cin), dim3(128), 0, st, W, ldw, Cout, Cin, gamma,
+    hipLaunchKernelGGL(fold_h_kernel<float>, dim3(Cin), dim3(256), 0, st, W, ldw, Cout, Cin, gamma,
                        reinterpret_cast<float *>(H));
   } else {
     return pcs_set_einval("pcs_bn_fold", "bad dtype");

@@ -316,27 +316,40 @@ __global__ void pool_bwd_dw_kernel(pcs_pool_bwd_args a) {
   a.dW_s1_global[(int64_t)n * a.ldw + a.col_off + k] = acc;
 }
 
-// dg = W_g^T csum; dz_g = dg*(g>0); bn_global backward from the B sparse entries
-__global__ void pool_bwd_coef_kernel(pcs_pool_bwd_args a) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.Cg) return;
+// dg = W_g^T csum; dz_g = dg*(g>0); bn_global backward from the B sparse entries.
+// Block: 64 channels k x 4 parts of the n reduction (fixed-order combine through LDS).
+constexpr int PBC_MAXB = 64;
+__global__ __launch_bounds__(256) void pool_bwd_coef_kernel(pcs_pool_bwd_args a) {
+  __shared__ float part[4][PBC_MAXB][64];
+  const int kk = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + kk;
+  const int B = (int)a.num_scenes;
+  const int n0 = (int)((int64_t)a.Cs * pr / 4), n1 = (int)((int64_t)a.Cs * (pr + 1) / 4);
+  if (k < a.Cg) {
+    for (int b = 0; b < B; ++b) {
+      float dg = 0.f;
+      for (int n = n0; n < n1; ++n)
+        dg = fmaf(a.W_s1[(int64_t)n * a.ldw + a.col_off + k], a.csum[(int64_t)b * a.Cs + n], dg);
+      part[pr][b][kk] = dg;
+    }
+  }
+  __syncthreads();
+  if (pr != 0 || k >= a.Cg) return;
   const double M = (double)(a.num_scenes * a.scene_rows);
   const double r = a.g_rstd[k], gm = a.g_gamma[k], mu = a.g_mean[k];
   double S1 = 0, S2 = 0, Sy = 0;
-  for (int64_t b = 0; b < a.num_scenes; ++b) {
-    float dg = 0.f;
-    for (int n = 0; n < a.Cs; ++n)
-      dg = fmaf(a.W_s1[(int64_t)n * a.ldw + a.col_off + k], a.csum[b * a.Cs + n], dg);
-    const float dz = a.g[b * a.Cg + k] > 0.f ? dg : 0.f;
-    a.sp[b * a.Cg + k] = dz;  // scaled by alpha below
+  for (int b = 0; b < B; ++b) {
+    const float dg = ((part[0][b][kk] + part[1][b][kk]) + part[2][b][kk]) + part[3][b][kk];
+    const float dz = a.g[(int64_t)b * a.Cg + k] > 0.f ? dg : 0.f;
+    a.sp[(int64_t)b * a.Cg + k] = dz;  // scaled by alpha below
     S1 += dz;
-    S2 += (double)dz * ((double)a.ysel[b * a.Cg + k] - mu) * r;
-    Sy += a.g_scene_sum[b * a.Cg + k];
+    S2 += (double)dz * ((double)a.ysel[(int64_t)b * a.Cg + k] - mu) * r;
+    Sy += a.g_scene_sum[(int64_t)b * a.Cg + k];
   }
   const double al = gm * r;
   const double ga = -gm * r * r * S2 / M;
   const double be = -gm * r * S1 / M - ga * mu;
-  for (int64_t b = 0; b < a.num_scenes; ++b) a.sp[b * a.Cg + k] = (float)(al * a.sp[b * a.Cg + k]);
+  for (int b = 0; b < B; ++b) a.sp[(int64_t)b * a.Cg + k] = (float)(al * a.sp[(int64_t)b * a.Cg + k]);
   a.alpha[k] = (float)al; a.beta_c[k] = (float)be; a.gamma_c[k] = (float)ga;
   a.dgamma[k] = (float)S2; a.dbeta[k] = (float)S1;
   a.dbias[k] = (float)(al * S1 + M * be + ga * Sy);
@@ -723,39 +736,66 @@ PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
 
 __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbytes, uint32_t thr,
                                     uint8_t *bits) {
-  // byte j covers elements 8j..8j+7; one Philox call gives 8 16-bit uniforms
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nbytes) return;
-  uint32_t ctr[4] = {(uint32_t)j, (uint32_t)((uint64_t)j >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
-  philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-  uint32_t b = 0;
+  // byte j covers elements 8j..8j+7; one Philox call gives 8 16-bit uniforms.  A thread makes
+  // 4 consecutive bytes and stores them as one word (byte stores are issue-bound).
+  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (j0 >= nbytes) return;
+  uint32_t word = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t lo = ctr[i] & 0xffffu, hi = ctr[i] >> 16;
-    b |= (lo >= thr ? 1u : 0u) << (2 * i);
-    b |= (hi >= thr ? 1u : 0u) << (2 * i + 1);
+  for (int q = 0; q < 4; ++q) {
+    const int64_t j = j0 + q;
+    uint32_t ctr[4] = {(uint32_t)j, (uint32_t)((uint64_t)j >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
+    philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t lo = ctr[i] & 0xffffu, hi = ctr[i] >> 16;
+      b |= (lo >= thr ? 1u : 0u) << (2 * i);
+      b |= (hi >= thr ? 1u : 0u) << (2 * i + 1);
+    }
+    word |= b << (8 * q);
   }
-  bits[j] = (uint8_t)b;
+  if (j0 + 4 <= nbytes && ((reinterpret_cast<uintptr_t>(bits) & 3) == 0)) {
+    *reinterpret_cast<uint32_t *>(bits + j0) = word;
+  } else {
+    for (int q = 0; q < 4 && j0 + q < nbytes; ++q) bits[j0 + q] = (uint8_t)(word >> (8 * q));
+  }
 }
 
+// out = scale * sum over slabs.  TPO threads share one 4-float output (slabs k = sub,
+// sub + TPO, ...) and combine with a fixed xor-shuffle tree: deterministic, and wide enough
+// for the thousand-slab reductions of the small layers' weight gradients.
+template <int TPO>
 __global__ void reduce_partials_kernel(const float *partial, int64_t nslabs, int64_t len, float scale,
                                        float *out, int64_t ldo, int64_t row_len) {
-  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i4 >= len) return;
-  if (i4 + 4 <= len && (row_len & 3) == 0) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t k = 0; k < nslabs; ++k) {
-      const float4 p = *reinterpret_cast<const float4 *>(partial + k * len + i4);
-      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+  const int sub = threadIdx.x % TPO;
+  const int64_t i4 = ((int64_t)blockIdx.x * (blockDim.x / TPO) + threadIdx.x / TPO) * 4;
+  const bool vec = (row_len & 3) == 0 && i4 + 4 <= len;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (i4 < len) {
+    if (vec) {
+      for (int64_t k = sub; k < nslabs; k += TPO) {
+        const float4 p = *reinterpret_cast<const float4 *>(partial + k * len + i4);
+        v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+      }
+    } else {
+      for (int64_t k = sub; k < nslabs; k += TPO)
+        for (int e = 0; e < 4 && i4 + e < len; ++e) v[e] += partial[k * len + i4 + e];
     }
+  }
+#pragma unroll
+  for (int off = TPO / 2; off > 0; off >>= 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += __shfl_xor(v[e], off);
+  if (sub != 0 || i4 >= len) return;
+  if (vec) {
     const int64_t row = i4 / row_len, col = i4 % row_len;
     *reinterpret_cast<float4 *>(out + row * ldo + col) =
-        make_float4(s.x * scale, s.y * scale, s.z * scale, s.w * scale);
+        make_float4(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale);
   } else {
-    for (int64_t i = i4; i < len && i < i4 + 4; ++i) {
-      float s = 0.f;
-      for (int64_t k = 0; k < nslabs; ++k) s += partial[k * len + i];
-      out[(i / row_len) * ldo + i % row_len] = s * scale;
+    for (int e = 0; e < 4 && i4 + e < len; ++e) {
+      const int64_t i = i4 + e;
+      out[(i / row_len) * ldo + i % row_len] = v[e] * scale;
     }
   }
 }
@@ -919,10 +959,11 @@ extern "C" int pcs_pool_bwd(const pcs_pool_bwd_args *ap, pcs_stream_t stream) {
       !a.dW_s1_global || !a.csum || !a.alpha || !a.beta_c || !a.gamma_c || !a.dgamma || !a.dbeta ||
       !a.dbias || !a.sp)
     return pcs_set_einval("pcs_pool_bwd", "null argument");
+  if (a.num_scenes < 1 || a.num_scenes > PBC_MAXB) return pcs_set_einval("pcs_pool_bwd", "1 <= scenes <= 64 per call");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(pool_bwd_csum_kernel, dim3(blocks_for(a.num_scenes * a.Cs, 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(pool_bwd_dw_kernel, dim3(blocks_for((int64_t)a.Cs * a.Cg, 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(pool_bwd_coef_kernel, dim3(blocks_for(a.Cg, 64)), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(pool_bwd_coef_kernel, dim3(blocks_for(a.Cg, 64)), dim3(256), 0, s, a);
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -1018,7 +1059,7 @@ extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32
   if (!bits || C % 8 != 0 || p < 0.f || p >= 1.f) return pcs_set_einval("pcs_dropout_bits", "bad arguments");
   const int64_t nbytes = M * (C / 8);
   const uint32_t thr = (uint32_t)(p * 65536.0f + 0.5f);
-  hipLaunchKernelGGL(dropout_bits_kernel, dim3(blocks_for(nbytes, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(dropout_bits_kernel, dim3(blocks_for((nbytes + 3) / 4, 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), seed, offset, nbytes, thr, bits);
   PCS_CHECK_LAUNCH();
   return 0;
@@ -1027,8 +1068,17 @@ extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32
 extern "C" int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale, float *out,
                                    int64_t ldo, int64_t row_len, pcs_stream_t stream) {
   if (!partial || !out || len <= 0 || nslabs <= 0 || row_len <= 0) return pcs_set_einval("pcs_reduce_partials", "bad arguments");
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks_for((len + 3) / 4, 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), partial, nslabs, len, scale, out, ldo, row_len);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n4 = (len + 3) / 4;
+  if (nslabs >= 64)
+    hipLaunchKernelGGL(reduce_partials_kernel<32>, dim3(blocks_for(n4, 256 / 32)), dim3(256), 0, st, partial, nslabs,
+                       len, scale, out, ldo, row_len);
+  else if (nslabs >= 8)
+    hipLaunchKernelGGL(reduce_partials_kernel<8>, dim3(blocks_for(n4, 256 / 8)), dim3(256), 0, st, partial, nslabs,
+                       len, scale, out, ldo, row_len);
+  else
+    hipLaunchKernelGGL(reduce_partials_kernel<1>, dim3(blocks_for(n4, 256)), dim3(256), 0, st, partial, nslabs, len,
+                       scale, out, ldo, row_len);
   PCS_CHECK_LAUNCH();
   return 0;
 }
