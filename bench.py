@@ -80,6 +80,34 @@ def kernel_model(tag, M, ab):
     return flops, nbytes
 
 
+def step_roofline(M, C, ab, measured_ms):
+    """t_roof = sum over layers of max(F_l / P_mfma, Bytes_l / 8 TB/s) for
+    the whole fwd+bwd step (decomposed seg_conv1: local 64->512 GEMM; conv1 has no dgrad;
+    every activation read or written once per pass)."""
+    layers = [(4, 64, 2), (64, 64, 3), (64, 64, 3), (64, 128, 3), (128, 1024, 3), (1024, 1024, 3),
+              (64, 512, 3), (512, 256, 3), (256, 128, 3), (128, C, 3)]
+    peak = PEAK["bf16" if ab == 2 else "fp32"]
+    t = 0.0
+    for cin, cout, passes in layers:
+        f = 2.0 * M * cin * cout * passes
+        b = 3.0 * M * (cin + cout) * ab
+        t += max(f / (peak["mfma"] * 1e12), b / (peak["hbm"] * 1e9))
+    return {"t_roof_ms": round(t * 1e3, 3), "frac": round(t * 1e3 / measured_ms, 4),
+            "model": "sum_l max(F_l/P_mfma, B_l/8TB/s), SURVEY 8(d)"}
+
+
+def northstar_64(kernels, M, ab):
+    """HBM-only fraction of the 64->64 conv fwd+bwd (conv2: fwd, dgrad, wgrad)
+    against t_HBM = 6 x 64 ch x M x bytes / 8 TB/s."""
+    tags = ("fwd:conv2", "dgrad:conv2", "wgrad:conv2")
+    if not all(t in kernels for t in tags):
+        return None
+    ms = sum(kernels[t][0] / kernels[t][1] for t in tags)
+    t_hbm = 6 * 64 * M * ab / (PEAK["bf16"]["hbm"] * 1e9) * 1e3
+    return {"layer": "conv2 (64->64) fwd+dgrad+wgrad", "ms": round(ms, 4), "t_hbm_ms": round(t_hbm, 4),
+            "hbm_frac": round(t_hbm / ms, 4)}
+
+
 def cpu_baseline(max_seconds=12.0):
     """Numpy oracle (fp32) fwd+bwd on the reference's CPU-runnable case (B=4, N=4096, C=2)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -231,6 +259,8 @@ def main():
                        "points_per_scene": N, "parallelism": f"dp{world}"},
             "loss": round(loss_v, 6),
             "roofline": roof,
+            "step_roofline": step_roofline(M, C, ab, el / args.steps * 1e3),
+            "northstar_64x64": northstar_64(kernels, M, ab) if kernels else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec))
