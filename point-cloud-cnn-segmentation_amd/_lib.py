@@ -134,12 +134,13 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("PCS_LIB", LIB_PATH)   # an alternative build, for A/B timing
+    if not os.path.exists(path):
         raise ImportError(
-            f"pcs_amd HIP library not built: {LIB_PATH} is missing. Build it with "
+            f"pcs_amd HIP library not built: {path} is missing. Build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` or "
             "`make -C point-cloud-cnn-segmentation_amd/csrc`.")
-    lib = ct.CDLL(LIB_PATH)
+    lib = ct.CDLL(path)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res
