@@ -33,7 +33,10 @@ typedef struct ihipStream_t *pcs_stream_t; /* == hipStream_t */
 enum { PCS_F32 = 0, PCS_BF16 = 1 };
 enum { PCS_OK = 0, PCS_EINVAL = -1000 };
 /* pcs_gemm_args.flags */
-enum { PCS_FLAG_GENERIC = 1 /* force the generic 128x{64,128} kernel (cross-checks) */ };
+enum {
+  PCS_FLAG_GENERIC = 1, /* force the generic 128x{64,128} kernel (cross-checks)            */
+  PCS_FLAG_NO_GLDS = 2  /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
+};
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
 enum {
@@ -46,11 +49,15 @@ enum {
 
 /* epilogue of the points-major GEMM */
 enum {
-  PCS_EPI_FWD = 0,   /* y = acc + bias; store y; per-chunk BN statistics (mean, M2);
-                        optional per-chunk max/min + arg for the global max-pool          */
-  PCS_EPI_DGRAD = 1, /* v = acc (+addend) (*keep*keep_scale); dz = (Yp*s+t > 0) ? v : 0;
-                        store dz; per-chunk S1 = sum dz, S2 = sum dz*xhat                 */
-  PCS_EPI_RAW = 2    /* store acc                                                        */
+  PCS_EPI_FWD = 0,   /* y = acc + bias; store y (C may be NULL: statistics only); per-chunk
+                        BN statistics (mean, M2); optional per-chunk max/min + arg for the
+                        global max-pool                                                    */
+  PCS_EPI_DGRAD = 1, /* v = acc (+bias) (+addend) (+sparse rows) (*keep*keep_scale);
+                        dz = (Yp*s+t > 0) ? v : 0 (es/et NULL: Yp > 0); store dz; per-chunk
+                        S1 = sum dz, S2 = sum dz*(Yp-mean)*rstd (0 when erstd is NULL)      */
+  PCS_EPI_RAW = 2,   /* store acc                                                          */
+  PCS_EPI_BNRELU = 3 /* y = acc + bias; store relu(y*es + et): the BN+ReLU of this layer
+                        applied on the way out, from a finished statistics pass (P:106-110) */
 };
 
 /*
@@ -90,6 +97,12 @@ typedef struct {
   float *stats;         /* [B*chunks_per_scene, Ncols, 2] partials (FWD, DGRAD) or NULL */
   float *pool;          /* [B*chunks_per_scene, Ncols, 4] (maxv, argmax, minv, argmin) or NULL */
   int32_t flags;        /* PCS_FLAG_* */
+  /* EPI_DGRAD with PRO_RAW: sparse rows of a folded max-pool gradient (global_feat, P:114):
+   *   v[m, n] += sum_{c < pool_c : pool_idx[b, c] == m} pool_coef[b, c] * pool_w[c*pool_ldw + n]
+   * with pool_idx / pool_coef [B, pool_c] (global row index, coefficient); NULL = none. */
+  const float *pool_w;
+  int64_t pool_ldw;
+  int32_t pool_c;
 } pcs_gemm_args;
 
 /* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error.  The
@@ -308,10 +321,24 @@ int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_i
  *   dA = dz (diag(alpha) W) + a H + 1 c^T,  WsT = (diag(alpha) W)^T [Cin, Cout] (dtype),
  *   c = W^T beta [Cin] (fp32),  H = W^T diag(gamma) W [Cin, Cin] (dtype).
  * Two pcs_gemm launches then give dA without reading y (conv5 backward, P:110 at P:254).
+ * WsT (and alpha) may be NULL: global_feat's dz is the sparse max-pool gradient, whose rows
+ * pcs_gemm adds in its EPI_DGRAD epilogue (pool_w).
  */
 int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const float *alpha,
                 const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
                 pcs_stream_t stream);
+
+/*
+ * S2 of a BN-fed layer's backward from R = dz^T a (pcs_wgrad with dy_mode RAW) instead of the
+ * stored output: y = a W^T (bias-free, W [C, Cin] in dtype, row stride ldw), so
+ *   S2[c] = sum_m dz[m,c] (y[m,c] - mean[c]) rstd[c] = rstd[c] (sum_k W[c,k] R[c,k] - mean[c] S1[c]).
+ * Rewrites the S2 slots of the per-chunk (S1, S2) partials [num_chunks, C, 2]: chunk 0 holds
+ * the total, the others 0 (pcs_bn_bwd_finalize sums them).  conv5 (P:110) when its output
+ * is kept only as relu(bn5(y)) for global_feat.
+ */
+int pcs_bn_s2_from_r(float *stats, int64_t num_chunks, int32_t C, const float *R, const void *W,
+                     int32_t dtype, int64_t ldw, int32_t Cin, const float *mean, const float *rstd,
+                     pcs_stream_t stream);
 
 /*
  * Confusion matrix of argmax predictions (P:261-266 accuracy, P:314-346 F1 / mIoU inputs):

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "csrc", "libpcs.so")
 
 F32, BF16 = 0, 1
 PRO_RAW, PRO_BNRELU, PRO_BWD, PRO_BWD_POOL = 0, 1, 2, 3
-EPI_FWD, EPI_DGRAD, EPI_RAW = 0, 1, 2
+EPI_FWD, EPI_DGRAD, EPI_RAW, EPI_BNRELU = 0, 1, 2, 3
 HEAD_FWD, HEAD_CE, HEAD_BWD = 0, 1, 2
 
 _vp = ct.c_void_p
@@ -37,10 +37,12 @@ class GemmArgs(ct.Structure):
         ("c_mask", _vp), ("c_keep_scale", _f),
         ("Yp", _vp), ("es", _vp), ("et", _vp), ("emean", _vp), ("erstd", _vp),
         ("stats", _vp), ("pool", _vp), ("flags", _i32),
+        ("pool_w", _vp), ("pool_ldw", _i64), ("pool_c", _i32),
     ]
 
 
 FLAG_GENERIC = 1
+FLAG_NO_GLDS = 2
 
 
 class WgradArgs(ct.Structure):
@@ -117,6 +119,7 @@ SIGNATURES = [
     ("pcs_gram_wgrad", ct.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
                                   _i32, _vp, _vp, _vp, _i64, _vp]),
     ("pcs_bn_fold", ct.c_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    ("pcs_bn_s2_from_r", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
     ("pcs_confusion", ct.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcs_argmax", ct.c_int, [_vp, _i64, _i64, _i32, _vp, _vp]),
     ("pcs_last_error", ct.c_char_p, []),

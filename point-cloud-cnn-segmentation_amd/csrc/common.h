@@ -141,6 +141,10 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a);
 int pcs_gemm_big_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                         hipStream_t s);
 constexpr int PCS_BIG_BM = 256;
+// LDS-DMA 256x256 kernel for the RAW-operand global_feat GEMMs (gemm_glds.hip)
+bool pcs_gemm_glds_applicable(const pcs_gemm_args &a);
+int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
+                         hipStream_t s);
 // wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)
 bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a);
 int pcs_wgrad_big_splits(const pcs_wgrad_args &a);

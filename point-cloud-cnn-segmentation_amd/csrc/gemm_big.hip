@@ -280,7 +280,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     }
 
     // lane owns rows m = wm*128 + i*16 + (lane&15), cols n = wn*64 + j*16 + 4*(lane>>4) + r
-    if constexpr (EPI == PCS_EPI_FWD) {
+    if constexpr (EPI == PCS_EPI_FWD || EPI == PCS_EPI_BNRELU) {
       const float *bias = a.scene_bias ? a.scene_bias + (int64_t)scene * Ncols : a.bias;
       if (bias) {
 #pragma unroll
@@ -290,6 +290,21 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
           for (int i = 0; i < 8; ++i) {
             acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
           }
+        }
+      }
+    }
+
+    if constexpr (EPI == PCS_EPI_BNRELU) {   // this layer's BN + ReLU on the way out
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 s4 = *reinterpret_cast<const float4 *>(a.es + n0 + wn * 64 + j * 16 + lcol);
+        const float4 t4 = *reinterpret_cast<const float4 *>(a.et + n0 + wn * 64 + j * 16 + lcol);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[i][j][0] = fmaxf(fmaf(acc[i][j][0], s4.x, t4.x), 0.f);
+          acc[i][j][1] = fmaxf(fmaf(acc[i][j][1], s4.y, t4.y), 0.f);
+          acc[i][j][2] = fmaxf(fmaf(acc[i][j][2], s4.z, t4.z), 0.f);
+          acc[i][j][3] = fmaxf(fmaf(acc[i][j][3], s4.w, t4.w), 0.f);
         }
       }
     }
@@ -412,7 +427,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
     __syncthreads();   // the C tile has been consumed
 
     // per-tile merge of the per-thread partials into the running per-column accumulators
-    if (EPI != PCS_EPI_RAW && (do_stats || do_pool)) {
+    if ((EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD) && (do_stats || do_pool)) {
       float2 *ps = reinterpret_cast<float2 *>(lds);                 // [RPP][BN] stats / S1,S2
       float4 *pp = reinterpret_cast<float4 *>(lds + RPP * BN * 8);  // [RPP][BN] pool
 #pragma unroll
@@ -468,7 +483,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   }
 
   // chunk end: this workgroup's per-column partials (same layout as gemm_nt)
-  if (EPI != PCS_EPI_RAW && tid < BN) {
+  if ((EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD) && tid < BN) {
     const int64_t o = (int64_t)chunk * Ncols + n0 + tid;
     if (do_stats) {
       float s2 = run[BN + tid];
@@ -496,7 +511,9 @@ bool pcs_gemm_big_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || a.K % BK != 0 || a.Ncols % BN != 0 || a.K < 128 || a.K > KMAX) return false;
   if (a.flags & PCS_FLAG_GENERIC) return false;
   if (a.a_mask && a.prologue != PCS_PRO_BNRELU) return false;
-  if (a.epilogue == PCS_EPI_FWD) return a.prologue == PCS_PRO_BNRELU || a.prologue == PCS_PRO_RAW;
+  if (a.epilogue == PCS_EPI_FWD || a.epilogue == PCS_EPI_BNRELU)
+    return a.prologue == PCS_PRO_BNRELU || a.prologue == PCS_PRO_RAW;
+  if (a.epilogue == PCS_EPI_DGRAD && (!a.es || !a.erstd || a.bias || a.pool_w)) return false;
   if (a.epilogue == PCS_EPI_DGRAD)   // BWD_POOL (global_feat) has neither a mask nor an addend
     return a.prologue == PCS_PRO_BWD ? !(a.c_mask && a.addend)
                                      : a.prologue == PCS_PRO_BWD_POOL && !a.c_mask && !a.addend;
@@ -510,6 +527,10 @@ int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s)
       if (g.prologue == PCS_PRO_RAW) return launch<PCS_PRO_RAW, PCS_EPI_FWD, false>(g, tps, tpc, s);
       return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
+    case PCS_EPI_BNRELU:
+      if (g.prologue == PCS_PRO_RAW) return launch<PCS_PRO_RAW, PCS_EPI_BNRELU, false>(g, tps, tpc, s);
+      return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, true>(g, tps, tpc, s)
+                      : launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, false>(g, tps, tpc, s);
     case PCS_EPI_DGRAD:
       if (g.prologue == PCS_PRO_BWD_POOL) return launch<PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(g, tps, tpc, s);
       if (g.c_mask) return launch<PCS_PRO_BWD, PCS_EPI_DGRAD, true>(g, tps, tpc, s);

@@ -1,0 +1,547 @@
+// bf16 256x256 points-major GEMM with LDS-DMA staging (global_load_lds_dwordx4) and an
+// 8-phase software pipeline, for the two 1024-deep GEMMs of global_feat, whose operand is
+// the materialised a5 = relu(bn5(y5)) (no prologue transform, so the operand goes
+// HBM -> LDS without passing through registers):
+//   forward   y_g = a5 Wg^T            epilogue: BN statistics + max-pool partials (P:113-114)
+//   backward  dA5 = a5 H + c + sparse  with H = Wg^T diag(gamma_g) Wg, c = Wg^T beta_g
+//             (pcs_bn_fold), the max-pool rows added sparsely, the ReLU mask of bn5 read
+//             from the operand itself, S1 = sum dz per column (autograd of P:110-114, P:254)
+//
+// Structure (cdna_hip_programming.md §5, "The 256² 8-phase template"):
+// * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 outputs = 8 x 4 accumulators of
+//   v_mfma_f32_16x16x32_bf16.  One K-tile (64 deep) is four phases of 16 MFMAs, one output
+//   quadrant each: (rows lo, cols lo), (lo, hi), (hi, lo), (hi, hi).
+// * LDS holds two K-tiles, each as four 16 KB regions (A-lo, A-hi, B-lo, B-hi: the lower /
+//   upper halves of every wave's rows and columns), so a region is free as soon as its last
+//   quadrant has read it: A-lo and B-lo after phase 1, B-hi after phase 2, A-hi after
+//   phase 3.  One region is restaged per phase, about four phases ahead of its use, by two
+//   glds per thread; waits are counted (vmcnt(10): five regions stay in flight) and the
+//   barriers are raw s_barriers, so the loads stay in flight across them.  The 16-B chunks
+//   of a 128-B LDS row are XOR-swizzled by (row >> 1) & 7; glds writes LDS linearly, so the
+//   swizzle is applied to the SOURCE address and again on the ds_read_b128 side (rule 21).
+// * The pipeline runs across the row tiles of a workgroup's chunk without draining: the
+//   epilogue works on the accumulators (DPP row reductions, per-wave running statistics in
+//   LDS outside the staging area), so the next tile's first K-tiles load while it runs.
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 512;
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int REG = 128 * BK * 2;                  // one region: 128 rows x 128 B
+constexpr int KBUF = 4 * REG;                      // A-lo | A-hi | B-lo | B-hi
+constexpr int STAGE_BYTES = 2 * KBUF;              // 128 KB
+constexpr int OFF_RUN = STAGE_BYTES;               // [2 wm][256] float2: (mean, m2) | (S1, 0)
+constexpr int OFF_POOL = OFF_RUN + 2 * 256 * 8;    // [2][256] float4: max, argmax, min, argmin
+constexpr int OFF_BIAS = OFF_POOL + 2 * 256 * 16;  // [256] f32
+constexpr int OFF_RUNN = OFF_BIAS + 256 * 4;       // [2] f32: rows merged per wave half
+constexpr int OFF_SPI = OFF_RUNN + 16;             // [1024] i32: sparse rows (max-pool argmax)
+constexpr int OFF_SPC = OFF_SPI + 1024 * 4;        // [1024] f32: sparse coefficients
+constexpr int OFF_BITS = OFF_SPC + 1024 * 4;       // [8] u32: hit bitmap of the tile's rows
+constexpr int LDS_BYTES = OFF_BITS + 64;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+constexpr int SPMAX = 1024;
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+PCS_DEV int xcd_remap(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+PCS_DEV void sbar() { __builtin_amdgcn_sched_barrier(0); }
+// One LDS-DMA piece: 64 lanes x 16 B from sbase + voff (per lane) to lds_dst + 16*lane.  Inline
+// asm (the §5.7 recipe) so that the compiler's own wait insertion neither drains these loads
+// before unrelated LDS reads nor spills their 64-bit addresses: the kernel counts them itself.
+PCS_DEV void glds16(const char *sbase, uint32_t voff, char *lds_dst) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t *)lds_dst;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(m0v)
+               : "memory");
+}
+PCS_DEV void barrier_raw() {
+  sbar();
+  asm volatile("s_barrier" ::: "memory");
+  sbar();
+}
+template <int N> PCS_DEV void wait_vm() {
+  sbar();
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  sbar();
+}
+PCS_DEV void wait_lgkm0() {
+  sbar();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  sbar();
+}
+
+// Butterfly over the 16 lanes of a DPP row (quad xor 1, quad xor 2, half-row mirror, row
+// mirror): every lane of the row ends with the row's result.
+template <int CTRL> PCS_DEV float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL> PCS_DEV int dppi(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+PCS_DEV float row_sum(float v) {
+  v += dppf<0xB1>(v); v += dppf<0x4E>(v); v += dppf<0x141>(v);
+  return v + dppf<0x140>(v);
+}
+PCS_DEV float row_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v)); v = fmaxf(v, dppf<0x4E>(v)); v = fmaxf(v, dppf<0x141>(v));
+  return fmaxf(v, dppf<0x140>(v));
+}
+PCS_DEV float row_min(float v) {
+  v = fminf(v, dppf<0xB1>(v)); v = fminf(v, dppf<0x4E>(v)); v = fminf(v, dppf<0x141>(v));
+  return fminf(v, dppf<0x140>(v));
+}
+PCS_DEV int row_mini(int v) {
+  v = min(v, dppi<0xB1>(v)); v = min(v, dppi<0x4E>(v)); v = min(v, dppi<0x141>(v));
+  return min(v, dppi<0x140>(v));
+}
+
+// region row q (0..127) -> tile row (A regions) / weight row (B regions)
+PCS_DEV int a_row(int hi, int q) { return (q & 63) + ((q >> 6) << 7) + (hi ? 64 : 0); }
+PCS_DEV int b_row(int hi, int q) { return (q & 31) + ((q >> 5) << 6) + (hi ? 32 : 0); }
+PCS_DEV int swz(int q, int chunk) { return chunk ^ ((q >> 1) & 7); }
+
+template <int MODE>
+__global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int tiles_per_scene,
+                                                            int tiles_per_chunk, int ncb) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  float2 *run = reinterpret_cast<float2 *>(lds + OFF_RUN);
+  float4 *runp = reinterpret_cast<float4 *>(lds + OFF_POOL);
+  float *lbias = reinterpret_cast<float *>(lds + OFF_BIAS);
+  float *runn = reinterpret_cast<float *>(lds + OFF_RUNN);
+  int *spi = reinterpret_cast<int *>(lds + OFF_SPI);
+  float *spc = reinterpret_cast<float *>(lds + OFF_SPC);
+  uint32_t *bits = reinterpret_cast<uint32_t *>(lds + OFF_BITS);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = L / ncb, cb = L % ncb;
+  const int cps = a.chunks_per_scene;
+  const int scene = chunk / cps, cis = chunk % cps;
+  const int n0 = cb * BN;
+  const int K = a.K, Ncols = a.Ncols;
+  const int64_t N = a.scene_rows;
+  const int t_begin = cis * tiles_per_chunk;
+  const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
+  if (t_begin >= t_end) return;   // uniform across the workgroup
+  const int nks = K / BK;
+  const int total = (t_end - t_begin) * nks;
+  const int64_t row0 = (int64_t)scene * N + (int64_t)t_begin * BM;
+  const int64_t scene_end = (int64_t)(scene + 1) * N;
+  const char *Ab = reinterpret_cast<const char *>(a.A);
+  const char *Wb = reinterpret_cast<const char *>(a.W) + (int64_t)n0 * K * 2;
+  const int64_t rowbytes = (int64_t)K * 2;
+
+  // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first glds)
+  const bool do_stats = a.stats != nullptr;
+  const bool do_pool = MODE == MODE_FWD && a.pool != nullptr;
+  const bool sparse = MODE == MODE_DGRAD && a.pool_w != nullptr;
+  if (tid < BN) {
+    lbias[tid] = a.bias ? a.bias[n0 + tid] : 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      run[h * BN + tid] = make_float2(0.f, 0.f);
+      runp[h * BN + tid] = make_float4(-__builtin_huge_valf(), __int_as_float(0x7fffffff),
+                                       __builtin_huge_valf(), __int_as_float(0x7fffffff));
+    }
+  }
+  if (tid < 2) runn[tid] = 0.f;
+  if (sparse) {
+    for (int c = tid; c < a.pool_c; c += THREADS) {
+      spi[c] = a.pool_idx[(int64_t)scene * a.pool_c + c];
+      spc[c] = a.pool_coef[(int64_t)scene * a.pool_c + c];
+    }
+  }
+  __syncthreads();
+
+  // ---- glds: piece g of wave w covers region rows (2w+g)*8 .. +8; lane -> row +lane/8,
+  // LDS slot lane%8, which holds the logical 16-B chunk swz(row, lane%8) of the source row.
+  // Addresses are a uniform (SGPR) base per K-tile plus a 32-bit per-lane byte offset.
+  int qrow[2];
+  uint32_t cbyte[2], boff[2][2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    qrow[g] = (2 * wid + g) * 8 + (lane >> 3);
+    cbyte[g] = (uint32_t)swz(qrow[g], lane & 7) * 16u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) boff[h][g] = (uint32_t)b_row(h, qrow[g]) * (uint32_t)rowbytes + cbyte[g];
+  }
+  auto issue = [&](int qseq, int region) {
+    if (qseq >= total) return;   // nothing left to prefetch (the counted waits stay valid)
+    const int tl = qseq / nks, kt = qseq - tl * nks;
+    char *dst = lds + (qseq & 1) * KBUF + region * REG;
+    if (region < 2) {
+      const int64_t rb = row0 + (int64_t)tl * BM;
+      const int valid = (int)pcs_min64(BM, scene_end - rb);
+      const char *sb = Ab + rb * rowbytes + kt * 128;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const uint32_t tr = (uint32_t)min(a_row(region, qrow[g]), valid - 1);   // rows past the scene: clamped
+        glds16(sb, tr * (uint32_t)rowbytes + cbyte[g], dst + (2 * wid + g) * 1024);
+      }
+    } else {
+      const char *sb = Wb + kt * 128;
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        glds16(sb, boff[region - 2][g], dst + (2 * wid + g) * 1024);
+    }
+  };
+
+  // ---- fragment reads (ds_read_b128 of the swizzled 16-B chunks)
+  bf16x8 af[4][2], bfr[4][2];
+  auto read_a = [&](int buf, int region) {
+    const char *base = lds + buf * KBUF + region * REG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wm * 64 + i * 16 + lr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[i][kk] = *reinterpret_cast<const bf16x8 *>(base + q * 128 + swz(q, kk * 4 + lg) * 16);
+    }
+  };
+  auto read_b = [&](int buf, int region, int j0) {
+    const char *base = lds + buf * KBUF + region * REG;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = wn * 32 + j * 16 + lr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bfr[j0 + j][kk] = *reinterpret_cast<const bf16x8 *>(base + q * 128 + swz(q, kk * 4 + lg) * 16);
+    }
+  };
+  // DGRAD: the ReLU mask of bn5 comes from the operand (Yp == A, K == Ncols): the wave's
+  // output columns n0 + wn*64 .. +64 are the k-columns of K-tile (n0 >> 6) + wn.  Bit j*4+r
+  // of mbit(i) <-> (row wm*128 + i*16 + lr, column wn*64 + j*16 + 4*lg + r); two rows per word.
+  uint32_t mb[4];
+  auto read_mask = [&](int buf, int region, int i0) {
+    const char *base = lds + buf * KBUF + region * REG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wm * 64 + i * 16 + lr;
+      uint32_t m = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(base + q * 128 + swz(q, 2 * j + (lg >> 1)) * 16 +
+                                                         (lg & 1) * 8);
+        const uint32_t b0 = (int16_t)(v.x & 0xffffu) > 0, b1 = (int16_t)(v.x >> 16) > 0;
+        const uint32_t b2 = (int16_t)(v.y & 0xffffu) > 0, b3 = (int16_t)(v.y >> 16) > 0;
+        m |= (b0 | (b1 << 1) | (b2 << 2) | (b3 << 3)) << (4 * j);
+      }
+      if (i & 1) mb[(i0 + i) >> 1] |= m << 16;
+      else mb[(i0 + i) >> 1] = m;
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < 4) mb[i] = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  auto mfma_quad = [&](int i0, int j0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j0 + j][kk], af[i][kk],
+                                                                         acc[i0 + i][j0 + j], 0, 0, 0);
+  };
+
+  // ---- prologue: K-tile 0 landed; A-lo, B-lo, B-hi of K-tile 1 in flight
+  issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
+  issue(1, 0); issue(1, 2); issue(1, 3);
+  wait_vm<6>();
+  barrier_raw();
+
+  const int ktm = (n0 >> 6) + wn;   // DGRAD: the K-tile holding this wave's mask columns
+  float run_n = 0.f;                // rows of this wave's half merged so far (uniform)
+
+  for (int qs = 0; qs < total; ++qs) {
+    const int buf = qs & 1;
+    const int kt = qs % nks;
+    // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
+    read_a(buf, 0);
+    read_b(buf, 2, 0);
+    if (MODE == MODE_DGRAD && kt == ktm) read_mask(buf, 0, 0);
+    issue(qs + 1, 1);
+    wait_vm<10>();
+    barrier_raw();
+    wait_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quad(0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier_raw();
+    // phase 2: (lo, hi); restage A-lo of K-tile qs+2
+    read_b(buf, 3, 2);
+    issue(qs + 2, 0);
+    wait_vm<10>();
+    barrier_raw();
+    wait_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quad(0, 2);
+    __builtin_amdgcn_s_setprio(0);
+    barrier_raw();
+    // phase 3: (hi, lo); restage B-lo of K-tile qs+2
+    read_a(buf, 1);
+    if (MODE == MODE_DGRAD && kt == ktm) read_mask(buf, 1, 4);
+    issue(qs + 2, 2);
+    barrier_raw();
+    wait_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quad(4, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier_raw();
+    // phase 4: (hi, hi); restage B-hi of K-tile qs+2
+    issue(qs + 2, 3);
+    wait_vm<10>();
+    barrier_raw();
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quad(4, 2);
+    __builtin_amdgcn_s_setprio(0);
+    barrier_raw();
+
+    if (kt != nks - 1) continue;
+
+    // ===================== epilogue of row tile qs / nks =====================
+    const int64_t rb = row0 + (int64_t)(qs / nks) * BM;
+    const int valid = (int)pcs_min64(BM, scene_end - rb);
+    const int nvw = max(0, min(128, valid - wm * 128));   // valid rows of this wave's half
+    // lane's columns c(j, r) = wn*64 + j*16 + 4*lg + r; rows m(i) = wm*128 + i*16 + lr
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 bb = *reinterpret_cast<const float4 *>(lbias + wn * 64 + j * 16 + 4 * lg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
+      }
+    }
+    uint32_t rowok = 0;   // bit i: row m(i) is a row of the scene
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rowok |= (uint32_t)(wm * 128 + i * 16 + lr < valid) << i;
+
+    if constexpr (MODE == MODE_FWD) {
+      if (nvw > 0) {
+        if (do_stats) {
+          // sums shifted by the half's running column mean, one Chan merge per column
+          float sh[16], s1[16], s2[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            sh[e] = run[wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3)].x;
+            s1[e] = 0.f;
+            s2[e] = 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if ((rowok >> i) & 1u) {
+#pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                const float d = acc[i][e >> 2][e & 3] - sh[e];
+                s1[e] += d;
+                s2[e] = fmaf(d, d, s2[e]);
+              }
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            s1[e] = row_sum(s1[e]);
+            s2[e] = row_sum(s2[e]);
+          }
+          if (lr == 0) {
+            const float nt = (float)nvw;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int c = wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3);
+              const float d1 = s1[e] / nt;
+              float n = run_n, mean = run[c].x, m2 = run[c].y;
+              chan_merge(n, mean, m2, nt, sh[e] + d1, fmaxf(s2[e] - s1[e] * d1, 0.f));
+              run[c] = make_float2(mean, m2);
+            }
+          }
+        }
+        if (do_pool) {
+          float mx[16], mn[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            mx[e] = -__builtin_huge_valf();
+            mn[e] = __builtin_huge_valf();
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if ((rowok >> i) & 1u) {
+#pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                mx[e] = fmaxf(mx[e], acc[i][e >> 2][e & 3]);
+                mn[e] = fminf(mn[e], acc[i][e >> 2][e & 3]);
+              }
+            }
+          }
+          bool upd = false;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            mx[e] = row_max(mx[e]);
+            mn[e] = row_min(mn[e]);
+            const float4 q = runp[wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3)];
+            upd |= mx[e] > q.x || mn[e] < q.z;
+          }
+          // a tile beats a column's running max / min rarely: only then find its first row
+          if (__builtin_amdgcn_ballot_w64(upd)) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              int ix = 0x7fffffff, in = 0x7fffffff;
+#pragma unroll
+              for (int i = 7; i >= 0; --i) {
+                if ((rowok >> i) & 1u) {
+                  const float v = acc[i][e >> 2][e & 3];
+                  const int row = (int)(rb + wm * 128 + i * 16 + lr);
+                  if (v == mx[e]) ix = row;
+                  if (v == mn[e]) in = row;
+                }
+              }
+              ix = row_mini(ix);
+              in = row_mini(in);
+              if (lr == 0) {
+                const int c = wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3);
+                float4 q = runp[c];
+                if (mx[e] > q.x) { q.x = mx[e]; q.y = __int_as_float(ix); }
+                if (mn[e] < q.z) { q.z = mn[e]; q.w = __int_as_float(in); }
+                runp[c] = q;
+              }
+            }
+          }
+        }
+        run_n += (float)nvw;
+      }
+    } else {   // MODE_DGRAD
+      if (sparse) {   // the tile's max-pool rows: a bitmap, then the rare per-row sums
+        if (tid < 8) bits[tid] = 0u;
+        lds_barrier();
+        for (int c = tid; c < a.pool_c; c += THREADS) {
+          const int64_t m = (int64_t)spi[c] - rb;
+          if (m >= 0 && m < valid) atomicOr(&bits[m >> 5], 1u << (m & 31));
+        }
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = wm * 128 + i * 16 + lr;
+          if ((bits[m >> 5] >> (m & 31)) & 1u) {
+            const int grow = (int)(rb + m);
+            for (int c = 0; c < a.pool_c; ++c) {
+              if (spi[c] != grow) continue;
+              const float w = spc[c];
+              const float *wr = a.pool_w + (int64_t)c * a.pool_ldw + n0 + wn * 64 + 4 * lg;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const float4 q = *reinterpret_cast<const float4 *>(wr + j * 16);
+                acc[i][j][0] = fmaf(w, q.x, acc[i][j][0]);
+                acc[i][j][1] = fmaf(w, q.y, acc[i][j][1]);
+                acc[i][j][2] = fmaf(w, q.z, acc[i][j][2]);
+                acc[i][j][3] = fmaf(w, q.w, acc[i][j][3]);
+              }
+            }
+          }
+        }
+        lds_barrier();   // bitmap reads done before the next tile's reset
+      }
+      float s1[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s1[e] = 0.f;
+      bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bool ok = (rowok >> i) & 1u;
+        const int64_t grow = rb + wm * 128 + i * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = ((mb[i >> 1] >> ((i & 1) * 16 + j * 4 + r)) & 1u) ? acc[i][j][r] : 0.f;
+            s1[j * 4 + r] += ok ? v[r] : 0.f;
+          }
+          if (ok)
+            *reinterpret_cast<uint2 *>(Cg + grow * Ncols + n0 + wn * 64 + j * 16 + 4 * lg) =
+                make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s1[e] = row_sum(s1[e]);
+      if (lr == 0 && do_stats) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int c = wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3);
+          run[c].x += s1[e];
+        }
+      }
+      // stores count in vmcnt: retire them so the next tile's counted waits stay exact
+      wait_vm<0>();
+    }
+
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < 4) mb[i] = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  // ---- chunk end: merge the two wave halves and write this workgroup's partials
+  if (wn == 0 && lane == 0) runn[wm] = run_n;
+  __syncthreads();
+  if (tid < BN) {
+    const int64_t o = (int64_t)chunk * Ncols + n0 + tid;
+    if (do_stats) {
+      const float2 h0 = run[tid], h1 = run[BN + tid];
+      if constexpr (MODE == MODE_FWD) {
+        float n = runn[0], mean = h0.x, m2 = h0.y;
+        chan_merge(n, mean, m2, runn[1], h1.x, h1.y);
+        *reinterpret_cast<float2 *>(a.stats + o * 2) = make_float2(mean, m2);
+      } else {
+        *reinterpret_cast<float2 *>(a.stats + o * 2) = make_float2(h0.x + h1.x, 0.f);
+      }
+    }
+    if (do_pool) {
+      float4 p = runp[tid];
+      const float4 q = runp[BN + tid];
+      const int pi = __float_as_int(p.y), qi = __float_as_int(q.y);
+      const int pj = __float_as_int(p.w), qj = __float_as_int(q.w);
+      if (q.x > p.x || (q.x == p.x && qi < pi)) { p.x = q.x; p.y = q.y; }
+      if (q.z < p.z || (q.z == p.z && qj < pj)) { p.z = q.z; p.w = q.w; }
+      *reinterpret_cast<float4 *>(a.pool + o * 4) = p;
+    }
+  }
+}
+
+}  // namespace
+
+bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
+  if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS))) return false;
+  if (a.prologue != PCS_PRO_RAW || a.K % (2 * BK) != 0 || a.Ncols % BN != 0) return false;
+  if (a.epilogue == PCS_EPI_FWD) return a.C == nullptr && a.scene_bias == nullptr;
+  if (a.epilogue == PCS_EPI_DGRAD)   // mask read from the operand itself, no S2, no addend
+    return a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask &&
+           (!a.pool_w || a.pool_c <= SPMAX);
+  return false;
+}
+
+int pcs_gemm_glds_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s) {
+  const int ncb = g.Ncols / BN;
+  const int nb = ncb * (int)(g.num_scenes * g.chunks_per_scene);
+  if (g.epilogue == PCS_EPI_FWD)
+    hipLaunchKernelGGL((gemm_glds_kernel<MODE_FWD>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<MODE_DGRAD>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

@@ -143,7 +143,7 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, const float *cf, int64_t
   }
 }
 
-template <typename T, int BM, int BN, int PRO, int EPI, bool POOL, bool MASK>
+template <typename T, int BM, int BN, int PRO, int EPI, bool POOL, bool MASK, bool SPARSE>
 __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                           int tiles_per_chunk, int ncb) {
   constexpr int EPC = Elem<T>::EPC;
@@ -163,10 +163,15 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
                                  : (CTILE_BYTES > RED_BYTES ? CTILE_BYTES : RED_BYTES);
   constexpr int PCOEF = Coef<PRO>::N * KMAX;            // floats
   constexpr int ECOEF = EPI == PCS_EPI_DGRAD ? 4 * BN : 0;
-  constexpr int LDS_BYTES = MAIN_BYTES + 4 * (PCOEF + ECOEF);
+  constexpr int SPMAX = 1024;                            // sparse rows: [pool_c] idx | coef | bitmap
+  constexpr int SP_BYTES = SPARSE ? 2 * SPMAX * 4 + BM / 8 : 0;
+  constexpr int LDS_BYTES = MAIN_BYTES + 4 * (PCOEF + ECOEF) + SP_BYTES;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   float *cf = reinterpret_cast<float *>(lds + MAIN_BYTES);
   float *ecf = cf + PCOEF;
+  int *spi = reinterpret_cast<int *>(ecf + ECOEF);
+  float *spc = reinterpret_cast<float *>(spi + SPMAX);
+  uint32_t *tbits = reinterpret_cast<uint32_t *>(spc + SPMAX);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -198,10 +203,16 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
       reinterpret_cast<int *>(cf)[3 * KMAX + k] = a.pool_idx[(int64_t)scene * K + k];
     }
   }
-  if constexpr (EPI == PCS_EPI_DGRAD) {
+  if constexpr (EPI == PCS_EPI_DGRAD) {   // NULL es/et: mask Yp > 0; NULL erstd: no S2
     for (int c = tid; c < BN; c += THREADS) {
-      ecf[c] = a.es[n0 + c]; ecf[BN + c] = a.et[n0 + c];
-      ecf[2 * BN + c] = a.emean[n0 + c]; ecf[3 * BN + c] = a.erstd[n0 + c];
+      ecf[c] = a.es ? a.es[n0 + c] : 1.f; ecf[BN + c] = a.et ? a.et[n0 + c] : 0.f;
+      ecf[2 * BN + c] = a.emean ? a.emean[n0 + c] : 0.f; ecf[3 * BN + c] = a.erstd ? a.erstd[n0 + c] : 0.f;
+    }
+  }
+  if constexpr (SPARSE) {
+    for (int c = tid; c < a.pool_c; c += THREADS) {
+      spi[c] = a.pool_idx[(int64_t)scene * a.pool_c + c];
+      spc[c] = a.pool_coef[(int64_t)scene * a.pool_c + c];
     }
   }
 
@@ -243,6 +254,17 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
                                     K, n0, (tail ? 0 : ks_next) * KSTEP + slot * EPC, srow, ra, ra2, rb, mk);
     };
 
+    if constexpr (SPARSE) {   // bitmap of the tile's rows that carry sparse terms
+      __syncthreads();
+      if (tid < BM / 32) tbits[tid] = 0u;
+      __syncthreads();
+      for (int c = tid; c < a.pool_c; c += THREADS) {
+        const int64_t m = (int64_t)spi[c] - row_base;
+        if (m >= 0 && m < valid) atomicOr(&tbits[m >> 5], 1u << (m & 31));
+      }
+      __syncthreads();
+    }
+
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -281,7 +303,10 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
     // ---- epilogue phase 1: accumulators (+bias) -> LDS tile [BM][BN] in T ----
     {
       const float *bias = nullptr;
-      if constexpr (EPI == PCS_EPI_FWD) bias = a.scene_bias ? a.scene_bias + scene * Ncols : a.bias;
+      if constexpr (EPI == PCS_EPI_FWD || EPI == PCS_EPI_BNRELU)
+        bias = a.scene_bias ? a.scene_bias + scene * Ncols : a.bias;
+      else if constexpr (EPI == PCS_EPI_DGRAD)
+        bias = a.bias;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int m = wm * WTM + i * 16 + (lane & 15);
@@ -292,6 +317,12 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
           if (bias) {
             const float4 bb = *reinterpret_cast<const float4 *>(bias + n0 + n);
             v0 += bb.x; v1 += bb.y; v2 += bb.z; v3 += bb.w;
+          }
+          if constexpr (EPI == PCS_EPI_BNRELU) {   // this layer's BN + ReLU on the way out
+            const float4 s4 = *reinterpret_cast<const float4 *>(a.es + n0 + n);
+            const float4 t4 = *reinterpret_cast<const float4 *>(a.et + n0 + n);
+            v0 = fmaxf(fmaf(v0, s4.x, t4.x), 0.f); v1 = fmaxf(fmaf(v1, s4.y, t4.y), 0.f);
+            v2 = fmaxf(fmaf(v2, s4.z, t4.z), 0.f); v3 = fmaxf(fmaf(v3, s4.w, t4.w), 0.f);
           }
           char *dst = lds + m * CROW + n * SZ;
           if constexpr (SZ == 4) {
@@ -367,6 +398,17 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) v[e] += ad[e];
               }
+              if constexpr (SPARSE) {   // rare: rows carrying max-pool terms (pool_w)
+                if ((tbits[rr >> 5] >> (rr & 31)) & 1u) {
+                  for (int c = 0; c < a.pool_c; ++c) {
+                    if (spi[c] != (int)grow) continue;
+                    const float w = spc[c];
+                    const float *wr = a.pool_w + (int64_t)c * a.pool_ldw + ecol;
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) v[e] = fmaf(w, wr[e], v[e]);
+                  }
+                }
+              }
               if (a.c_mask) {
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) v[e] *= ((mb[q] >> e) & 1u) ? a.c_keep_scale : 0.f;
@@ -439,15 +481,15 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
   }
 }
 
-template <typename T, int BM, int BN, int PRO, int EPI, bool POOL>
+template <typename T, int BM, int BN, int PRO, int EPI, bool POOL, bool SPARSE = false>
 int launch_t(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
   const int ncb = a.Ncols / BN;
   const int nb = ncb * (int)(a.num_scenes * a.chunks_per_scene);
   if (PRO == PCS_PRO_BNRELU && a.a_mask)
-    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL, PRO == PCS_PRO_BNRELU>), dim3(nb),
+    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL, PRO == PCS_PRO_BNRELU, SPARSE>), dim3(nb),
                        dim3(THREADS), 0, s, a, tps, tpc, ncb);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL, false>), dim3(nb), dim3(THREADS), 0, s,
+    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, PRO, EPI, POOL, false, SPARSE>), dim3(nb), dim3(THREADS), 0, s,
                        a, tps, tpc, ncb);
   PCS_CHECK_LAUNCH();
   return 0;
@@ -464,7 +506,8 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
           return pool ? launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_FWD, true>(a, tps, tpc, s)
                       : launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_FWD, false>(a, tps, tpc, s);
         case PCS_PRO_RAW:
-          return launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_FWD, false>(a, tps, tpc, s);
+          return pool ? launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_FWD, true>(a, tps, tpc, s)
+                      : launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_FWD, false>(a, tps, tpc, s);
         default: break;
       }
       break;
@@ -475,6 +518,16 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
           return launch_t<T, BM, BN, PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
         case PCS_PRO_BNRELU:   // a_{l-1} H (folded BN backward of a wide layer, see pcs_bn_fold)
           return launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
+        case PCS_PRO_RAW:      // a5 H + c + max-pool rows (global_feat, folded)
+          return a.pool_w ? launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_DGRAD, false, true>(a, tps, tpc, s)
+                          : launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
+        default: break;
+      }
+      break;
+    case PCS_EPI_BNRELU:
+      switch (a.prologue) {
+        case PCS_PRO_BNRELU: return launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_BNRELU, false>(a, tps, tpc, s);
+        case PCS_PRO_RAW: return launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_BNRELU, false>(a, tps, tpc, s);
         default: break;
       }
       break;
@@ -496,10 +549,20 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
 
 static constexpr int GEMM_BM = 128;
 
+// The row-chunk geometry depends only on shapes, dtype and flags, never on which optional
+// operands are set: callers size their partial buffers from pcs_gemm_geometry() before the
+// pointers exist.  Shapes the 256x256 kernels can take use 256-row-multiple chunks; if a call
+// of that class ends up on the generic kernel (an operand combination the wide kernels do not
+// implement), that kernel walks the same chunks in 128-row tiles.
+static bool wide_class(const pcs_gemm_args &a) {
+  return a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && a.K % 64 == 0 && a.Ncols % 256 == 0 &&
+         a.K >= 128 && a.K <= 1024;
+}
+
 extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Ncols <= 0)
     return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
-  if (pcs_gemm_big_applicable(*a))
+  if (wide_class(*a))
     return pcs_fill_geometry(a, PCS_BIG_BM, 256, a->Ncols / 256);   // one 512-thread WG per CU
   const int64_t ncb = a->Ncols >= 128 ? a->Ncols / 128 : 1;
   return pcs_fill_geometry(a, GEMM_BM, 2048, ncb);                 // ~8 WGs per CU
@@ -519,9 +582,16 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
     return pcs_set_einval("pcs_gemm", "PRO_BWD_POOL needs beta, gamma, pool_idx, pool_coef");
   if (a.prologue == PCS_PRO_BNRELU && (!a.pa || !a.pb))
     return pcs_set_einval("pcs_gemm", "PRO_BNRELU needs s and t");
-  if (a.epilogue == PCS_EPI_DGRAD && (!a.Yp || !a.es || !a.et || !a.emean || !a.erstd || !a.C))
-    return pcs_set_einval("pcs_gemm", "EPI_DGRAD needs Yp, es, et, emean, erstd and C");
+  if (a.epilogue < PCS_EPI_FWD || a.epilogue > PCS_EPI_BNRELU) return pcs_set_einval("pcs_gemm", "bad epilogue");
+  if (a.epilogue == PCS_EPI_DGRAD && (!a.Yp || !a.C || !a.es != !a.et || (a.erstd && !a.emean)))
+    return pcs_set_einval("pcs_gemm", "EPI_DGRAD needs Yp and C (es/et both or neither, emean with erstd)");
+  if (a.epilogue == PCS_EPI_BNRELU && (!a.es || !a.et || !a.C || a.stats || a.pool))
+    return pcs_set_einval("pcs_gemm", "EPI_BNRELU needs es, et and C (no statistics)");
   if (a.pool && a.epilogue != PCS_EPI_FWD) return pcs_set_einval("pcs_gemm", "pool needs EPI_FWD");
+  if (a.pool_w && (a.epilogue != PCS_EPI_DGRAD || a.prologue != PCS_PRO_RAW || !a.pool_idx || !a.pool_coef ||
+                   a.pool_c <= 0 || a.pool_c > 1024 || a.pool_ldw < a.Ncols))
+    return pcs_set_einval("pcs_gemm", "pool_w (sparse rows) needs EPI_DGRAD, PRO_RAW, pool_idx, pool_coef, "
+                                      "0 < pool_c <= 1024, pool_ldw >= Ncols");
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31)
     return pcs_set_einval("pcs_gemm", "M must be < 2^31 rows");
   if (a.K > KMAX) return pcs_set_einval("pcs_gemm", "K must be <= 1024");
@@ -530,7 +600,11 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (pcs_gemm_big_applicable(a)) {
+  if (wide_class(a) && pcs_gemm_glds_applicable(a)) {
+    const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
+    return pcs_gemm_glds_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
+  }
+  if (wide_class(a) && pcs_gemm_big_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_big_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
   }

@@ -109,11 +109,10 @@ extern "C" int pcs_gram_wgrad(const float *G, const float *S, const float *W, in
 // ---------------------------------------------------------------------------------------
 namespace {
 
-// WsT[n][k] = W[k][n] * alpha[k];  c[n] = sum_k beta[k] W[k][n]       (one thread per (n, k) / n)
+// WsT[n][k] = W[k][n] * alpha[k]   (one thread per (n, k))
 template <typename T>
 __global__ void fold_wt_kernel(const float *__restrict__ W, int64_t ldw, int Cout, int Cin,
-                               const float *__restrict__ alpha, const float *__restrict__ beta,
-                               T *__restrict__ WsT, float *__restrict__ c) {
+                               const float *__restrict__ alpha, T *__restrict__ WsT) {
   const int64_t n_el = (int64_t)Cout * Cin;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el; i += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(i / Cout), k = (int)(i % Cout);
@@ -121,13 +120,86 @@ __global__ void fold_wt_kernel(const float *__restrict__ W, int64_t ldw, int Cou
     if constexpr (sizeof(T) == 2) WsT[i] = (T)(pack2bf(v, 0.f) & 0xffffu);
     else WsT[i] = v;
   }
-  if (blockIdx.x == 0) {
-    for (int n = threadIdx.x; n < Cin; n += blockDim.x) {
-      float acc = 0.f;
-      for (int k = 0; k < Cout; ++k) acc = fmaf(beta[k], W[(int64_t)k * ldw + n], acc);
-      c[n] = acc;
-    }
+}
+
+// c[n] = sum_k beta[k] W[k][n]: block = 64 columns n x 4 parts of k (fixed-order combine)
+__global__ __launch_bounds__(256) void fold_c_kernel(const float *__restrict__ W, int64_t ldw, int Cout, int Cin,
+                                                     const float *__restrict__ beta, float *__restrict__ c) {
+  __shared__ float red[4][64];
+  const int nn = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + nn;
+  const int k0 = (int)((int64_t)Cout * pr / 4), k1 = (int)((int64_t)Cout * (pr + 1) / 4);
+  float acc = 0.f;
+  if (n < Cin) {
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) acc = fmaf(beta[k], W[(int64_t)k * ldw + n], acc);
   }
+  red[pr][nn] = acc;
+  __syncthreads();
+  if (pr == 0 && n < Cin) c[n] = ((red[0][nn] + red[1][nn]) + red[2][nn]) + red[3][nn];
+}
+
+// H[i][j] = sum_k (W[k][i] gamma[k]) W[k][j]: 64 x 64 output tile per block, k in steps of 32
+// through LDS (rows of W are contiguous in i and j: coalesced), 4 x 4 outputs per thread
+template <typename T>
+__global__ __launch_bounds__(256) void fold_h_tiled_kernel(const float *__restrict__ W, int64_t ldw, int Cout,
+                                                           int Cin, const float *__restrict__ gamma,
+                                                           T *__restrict__ H) {
+  __shared__ float Xs[32][64 + 4];
+  __shared__ float Ys[32][64 + 4];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < Cout; k0 += 32) {
+    for (int e = tid; e < 32 * 64; e += 256) {
+      const int kk = e >> 6, cc = e & 63, k = k0 + kk;
+      const bool ok = k < Cout;
+      Xs[kk][cc] = ok ? W[(int64_t)k * ldw + i0 + cc] * gamma[k] : 0.f;
+      Ys[kk][cc] = ok ? W[(int64_t)k * ldw + j0 + cc] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < 32; ++kk) {
+      const float4 xv = *reinterpret_cast<const float4 *>(&Xs[kk][ty * 4]);
+      const float4 yv = *reinterpret_cast<const float4 *>(&Ys[kk][tx * 4]);
+      const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[p][q] = fmaf(xa[p], ya[q], acc[p][q]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t o = (int64_t)(i0 + ty * 4 + p) * Cin + j0 + tx * 4 + q;
+      if constexpr (sizeof(T) == 2) H[o] = (T)(pack2bf(acc[p][q], 0.f) & 0xffffu);
+      else H[o] = acc[p][q];
+    }
+}
+
+// S2 of a BN-fed layer from R = dz^T a: rstd (sum_k W[c,k] R[c,k] - mean S1), rewritten into
+// the per-chunk partials (chunk 0 = total, others 0).  One block per channel, fp64 sums.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_s2_kernel(float *__restrict__ stats, int64_t nch, int C,
+                                                    const float *__restrict__ R, const T *__restrict__ W,
+                                                    int64_t ldw, int Cin, const float *__restrict__ mean,
+                                                    const float *__restrict__ rstd) {
+  __shared__ double sh[256][2];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double dot = 0.0, s1 = 0.0;
+  for (int k = tid; k < Cin; k += 256) dot += (double)load_elem(W, (int64_t)c * ldw + k) * (double)R[(int64_t)c * Cin + k];
+  for (int64_t ch = tid; ch < nch; ch += 256) s1 += (double)stats[(ch * C + c) * 2];
+  sh[tid][0] = dot; sh[tid][1] = s1;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) { sh[tid][0] += sh[tid + st][0]; sh[tid][1] += sh[tid + st][1]; }
+    __syncthreads();
+  }
+  for (int64_t ch = tid; ch < nch; ch += 256)
+    stats[(ch * C + c) * 2 + 1] = ch == 0 ? (float)((double)rstd[c] * (sh[0][0] - (double)mean[c] * sh[0][1])) : 0.f;
 }
 
 // H[i][j] = sum_k W[k][i] gamma[k] W[k][j]: block = row i, 4 parts of k (fixed-order combine)
@@ -155,26 +227,53 @@ __global__ __launch_bounds__(256) void fold_h_kernel(const float *__restrict__ W
 
 }  // namespace
 
+template <typename T>
+void launch_fold(const float *W, int Cout, int Cin, int64_t ldw, const float *alpha, const float *beta,
+                 const float *gamma, T *WsT, float *c, T *H, hipStream_t st) {
+  if (WsT) {
+    const int nb = (int)pcs_min64(1024, ((int64_t)Cout * Cin + 255) / 256);
+    hipLaunchKernelGGL(fold_wt_kernel<T>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, WsT);
+  }
+  hipLaunchKernelGGL(fold_c_kernel, dim3((Cin + 63) / 64), dim3(256), 0, st, W, ldw, Cout, Cin, beta, c);
+  if (Cin % 64 == 0)
+    hipLaunchKernelGGL(fold_h_tiled_kernel<T>, dim3(Cin / 64, Cin / 64), dim3(256), 0, st, W, ldw, Cout, Cin,
+                       gamma, H);
+  else
+    hipLaunchKernelGGL(fold_h_kernel<T>, dim3(Cin), dim3(256), 0, st, W, ldw, Cout, Cin, gamma, H);
+}
+
 extern "C" int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const float *alpha,
                            const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
                            pcs_stream_t stream) {
-  if (!W || !alpha || !beta || !gamma || !WsT || !c || !H || Cout <= 0 || Cin <= 0 || ldw < Cin)
+  if (!W || !beta || !gamma || (WsT && !alpha) || !c || !H || Cout <= 0 || Cin <= 0 || ldw < Cin)
     return pcs_set_einval("pcs_bn_fold", "bad arguments");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int nb = (int)pcs_min64(1024, ((int64_t)Cout * Cin + 255) / 256);
-  if (dtype == PCS_BF16) {
-    hipLaunchKernelGGL(fold_wt_kernel<bf16_t>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, beta,
-                       reinterpret_cast<bf16_t *>(WsT), c);
-    hipLaunchKernelGGL(fold_h_kernel<bf16_t>, dim3(Cin), dim3(256), 0, st, W, ldw, Cout, Cin, gamma,
-                       reinterpret_cast<bf16_t *>(H));
-  } else if (dtype == PCS_F32) {
-    hipLaunchKernelGGL(fold_wt_kernel<float>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, beta,
-                       reinterpret_cast<float *>(WsT), c);
-    hipLaunchKernelGGL(fold_h_kernel<float>, dim3(Cin), dim3(256), 0, st, W, ldw, Cout, Cin, gamma,
-                       reinterpret_cast<float *>(H));
-  } else {
+  if (dtype == PCS_BF16)
+    launch_fold<bf16_t>(W, Cout, Cin, ldw, alpha, beta, gamma, reinterpret_cast<bf16_t *>(WsT), c,
+                        reinterpret_cast<bf16_t *>(H), st);
+  else if (dtype == PCS_F32)
+    launch_fold<float>(W, Cout, Cin, ldw, alpha, beta, gamma, reinterpret_cast<float *>(WsT), c,
+                       reinterpret_cast<float *>(H), st);
+  else
     return pcs_set_einval("pcs_bn_fold", "bad dtype");
-  }
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_bn_s2_from_r(float *stats, int64_t num_chunks, int32_t C, const float *R, const void *W,
+                                int32_t dtype, int64_t ldw, int32_t Cin, const float *mean, const float *rstd,
+                                pcs_stream_t stream) {
+  if (!stats || !R || !W || !mean || !rstd || num_chunks <= 0 || C <= 0 || Cin <= 0 || ldw < Cin)
+    return pcs_set_einval("pcs_bn_s2_from_r", "bad arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(bn_s2_kernel<bf16_t>, dim3(C), dim3(256), 0, st, stats, num_chunks, (int)C, R,
+                       reinterpret_cast<const bf16_t *>(W), ldw, (int)Cin, mean, rstd);
+  else if (dtype == PCS_F32)
+    hipLaunchKernelGGL(bn_s2_kernel<float>, dim3(C), dim3(256), 0, st, stats, num_chunks, (int)C, R,
+                       reinterpret_cast<const float *>(W), ldw, (int)Cin, mean, rstd);
+  else
+    return pcs_set_einval("pcs_bn_s2_from_r", "bad dtype");
   PCS_CHECK_LAUNCH();
   return 0;
 }

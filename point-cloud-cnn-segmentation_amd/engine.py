@@ -6,6 +6,11 @@ current stream.  Nothing here computes on the CPU; every numeric op is a C-ABI c
 
 Per layer l the forward stores only Y_l = conv_l(a_{l-1}) (pre-BN, fp32 or bf16);
 a_l = relu(bn_l(Y_l)) [* dropout] is recomputed inside whichever kernel consumes it.
+The exception is the 1024-wide pair conv5 / global_feat: conv5 runs twice (a statistics pass,
+then a pass that applies bn5 + ReLU on the way out), so a5 = relu(bn5(y5)) is stored instead of
+y5, and global_feat's output is never stored (its epilogue keeps only BN statistics and the
+max-pool candidates).  Both 1024-deep global_feat GEMMs then read a5 raw, which lets them stage
+it HBM -> LDS by DMA (csrc/gemm_glds.hip).
 The backward stores dZ_l = dL/d(BN_l output) after the ReLU / dropout masks and forms
 dy_l = alpha*dZ_l + beta + gamma*Y_l on the fly in the dgrad / wgrad kernels.
 
@@ -185,7 +190,8 @@ class Engine:
                        prologue=pro, epilogue=epi, chunks_per_scene=cps, flags=self.flags,
                        A=L.ptr(A), W=L.ptr(W), C=L.ptr(C),
                        a_keep_scale=kw.pop("a_keep_scale", 1.0),
-                       c_keep_scale=kw.pop("c_keep_scale", 1.0))
+                       c_keep_scale=kw.pop("c_keep_scale", 1.0),
+                       pool_ldw=kw.pop("pool_ldw", 0), pool_c=kw.pop("pool_c", 0))
         for k, v in kw.items():
             setattr(a, k, L.ptr(v))
         self._launch(tag, "pcs_gemm", ct.byref(a), self._stream())
@@ -269,16 +275,28 @@ class Engine:
         layer("conv2", "conv1", "bn1", 64, 64, "bn2", P["conv2.bias"])
         layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"])
         layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"])
-        layer("conv5", "conv4", "bn4", 128, 1024, "bn5", P["conv5.bias"])
 
-        # global_feat: GEMM + store with BN statistics and max-pool partials in the epilogue
-        yg = self._empty(M, 1024, device=dev)
-        cps_g, rpc_g = self.geometry(B, N, 1024, 1024)
+        # conv5 (P:110): a statistics-only pass (nothing stored), then the same GEMM with
+        # bn5 + ReLU applied in the epilogue, storing a5 = relu(bn5(y5)) for global_feat
+        st, cps, rpc = stats_buf(128, 1024) if train else (None, 0, 0)
+        if train:
+            self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_FWD, sv.ys["conv4"], wc["conv5"][0], None,
+                       stats=st, tag="fwd_stats:conv5", **bnrelu("bn4"))
+        sv.bn["bn5"] = self._bn_finalize("bn5", st, B, N, 1024, cps, rpc, P, bufs, train, dev,
+                                         offset=P["conv5.bias"])
+        a5 = self._empty(M, 1024, device=dev)
+        c5 = sv.bn["bn5"]
+        self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU, sv.ys["conv4"], wc["conv5"][0], a5,
+                   es=c5.scale, et=c5.shift, tag="fwd:conv5", **bnrelu("bn4"))
+        sv.ys["a5"] = a5
+
+        # global_feat (P:113-114): a5 W^T with BN statistics and max-pool partials in the
+        # epilogue; the 1024-wide output itself is never stored
+        cps_g, rpc_g = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD)
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
         st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
-        self._gemm(B, N, 1024, 1024, L.PRO_BNRELU, L.EPI_FWD, sv.ys["conv5"], wc["global_feat"][0], yg,
-                   stats=st, pool=pool, tag="fwd:global_feat", **bnrelu("bn5"))
-        sv.ys["global_feat"] = yg
+        self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, wc["global_feat"][0], None,
+                   stats=st, pool=pool, tag="fwd:global_feat")
         sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_g, rpc_g, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]
@@ -461,39 +479,53 @@ class Engine:
                    A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
         wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
 
-        # global_feat (dy from the sparse max-pool gradient); the epilogue applies the
-        # ReLU/BN5-backward input stage and sums S1/S2 for bn5
+        # global_feat input gradient in folded form (P:113 at P:254): with dy_g = beta_g +
+        # gamma_g * y_g + (max-pool rows) and y_g = a5 Wg^T,
+        #   dA5 = a5 H + 1 c^T + sum_b sp[b, c] Wg[c, :] at the row am[b, c],
+        # H = Wg^T diag(gamma_g) Wg, c = Wg^T beta_g (pcs_bn_fold); the epilogue masks with
+        # a5 > 0 (bn5's ReLU) and sums S1 = sum dz5; S2 comes from R = dz5^T a4 below.
+        a5 = ys["a5"]
+        Wg = P["global_feat.weight"]
+        Hg = self._empty(1024, 1024, device=dev)
+        cvec = torch.empty(1024, dtype=torch.float32, device=dev)
+        L.call("pcs_bn_fold", L.ptr(Wg), 1024, 1024, Wg.shape[1], None, L.ptr(bg), L.ptr(gg), self.dt,
+               None, L.ptr(cvec), L.ptr(Hg), s)
         pc5 = sv.bn["bn5"]
-        cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD)
-        st = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
-        self._gemm(B, N, 1024, 1024, L.PRO_BWD_POOL, L.EPI_DGRAD, ys["global_feat"],
-                   wc["global_feat"][1], bufB, pb=bg, pc=gg, pool_idx=sv.am, pool_coef=sp,
-                   Yp=ys["conv5"], es=pc5.scale, et=pc5.shift, emean=pc5.mean, erstd=pc5.rstd,
-                   stats=st, tag="dgrad:global_feat")
-        # global_feat weight gradient from the Gram of a5 = relu(bn5(y5)): the symmetric
-        # a5^T a5 (upper tiles) + an O(C^3) assemble instead of the M x 1024 x 1024 GEMM
+        cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD)
+        st5 = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
+        self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
+                   pool_idx=sv.am, pool_coef=sp, pool_w=Wg, pool_ldw=Wg.shape[1], pool_c=1024,
+                   stats=st5, tag="dgrad:global_feat")
+        dz5 = bufB
+        # global_feat weight gradient from the Gram of a5: the symmetric a5^T a5 (upper tiles)
+        # + an O(C^3) assemble instead of the M x 1024 x 1024 GEMM
+        ones = torch.ones(1024, dtype=torch.float32, device=dev)
+        zeros = torch.zeros(1024, dtype=torch.float32, device=dev)
         gram = torch.empty(1024, 1024, dtype=torch.float32, device=dev)
         colsum = torch.empty(1024, dtype=torch.float32, device=dev)
         sps = ct.c_int32(0)
         nbytes = L.load().pcs_gram_workspace(B, N, 1024, self.dt, ct.byref(sps))
         ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
-        keepalive.append(ws)
-        self._launch("wgrad:global_feat", "pcs_gram", L.ptr(ys["conv5"]), L.ptr(pc5.scale), L.ptr(pc5.shift),
+        self._launch("wgrad:global_feat", "pcs_gram", L.ptr(a5), L.ptr(ones), L.ptr(zeros),
                      B, N, 1024, self.dt, sps.value, L.ptr(ws), L.ptr(gram), L.ptr(colsum), s)
-        Wg = P["global_feat.weight"]
         self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg),
-                     Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(ys["conv5"]),
-                     L.ptr(pc5.scale), L.ptr(pc5.shift), B, 1024, 1024, self.dt, None, None,
+                     Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(a5),
+                     L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.dt, None, None,
                      L.ptr(G("global_feat.weight")), 1024, s)
-        keepalive.append((gram, colsum))
-        bn_bwd("bn5", "conv5", st, cps5)
-        dz5 = bufB
+        keepalive.append((Hg, cvec, ones, zeros, gram, colsum, ws))
 
-        # conv5 (128 -> 1024) in folded form: neither gradient reads the wide y5 (gram.hip)
+        # conv5 (128 -> 1024): R = dz5^T a4 gives bn5's S2 (y5 = a4 W5^T is not stored) and
+        # the alpha-term of dW5; then the folded input gradient and the Gram-form dW5:
         #   dA4 = dz5 (diag(alpha5) W5) + a4 (W5^T diag(gamma5) W5) + W5^T beta5
-        #   dW5 = diag(alpha5) dz5^T a4 + beta5 (x) colsum(a4) + diag(gamma5) W5 (a4^T a4)
-        al5, be5, ga5 = coefs["bn5"]
+        #   dW5 = diag(alpha5) R + beta5 (x) colsum(a4) + diag(gamma5) W5 (a4^T a4)
         pc4 = sv.bn["bn4"]
+        r5 = torch.empty(1024, 128, dtype=torch.float32, device=dev)
+        keepalive.append(self._wgrad(B, N, 1024, 128, L.PRO_RAW, L.PRO_BNRELU, r5, tag="wgrad:conv5",
+                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift))
+        L.call("pcs_bn_s2_from_r", L.ptr(st5), B * cps5, 1024, L.ptr(r5), L.ptr(wc["conv5"][0]), self.dt,
+               128, 128, L.ptr(pc5.mean), L.ptr(pc5.rstd), s)
+        bn_bwd("bn5", "conv5", st5, cps5)
+        al5, be5, ga5 = coefs["bn5"]
         W5 = P["conv5.weight"]
         ws_t = self._empty(128, 1024, device=dev)
         c5 = torch.empty(128, dtype=torch.float32, device=dev)
@@ -507,9 +539,6 @@ class Engine:
         self._gemm(B, N, 128, 128, L.PRO_BNRELU, L.EPI_DGRAD, ys["conv4"], h4, bufA, pa=pc4.scale,
                    pb=pc4.shift, Yp=ys["conv4"], es=pc4.scale, et=pc4.shift, emean=pc4.mean,
                    erstd=pc4.rstd, addend=pbuf, stats=st, tag="dgrad2:conv5")
-        r5 = torch.empty(1024, 128, dtype=torch.float32, device=dev)
-        keepalive.append(self._wgrad(B, N, 1024, 128, L.PRO_RAW, L.PRO_BNRELU, r5, tag="wgrad:conv5",
-                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift))
         g4 = torch.empty(128, 128, dtype=torch.float32, device=dev)
         s4 = torch.empty(128, dtype=torch.float32, device=dev)
         sps4 = ct.c_int32(0)

@@ -1,0 +1,169 @@
+"""The global_feat GEMMs on the stored a5 = relu(bn5(y5)) (csrc/gemm_glds.hip: LDS-DMA
+256x256 kernel; the generic kernel with FLAG_NO_GLDS / fp32) against torch fp32 on the same
+operands, through the C ABI:
+
+* forward epilogue: BN statistics + max-pool partials of y = a5 W^T with nothing stored,
+  finalised by pcs_bn_fwd_finalize / pcs_pool_finalize (mean / variance / per-scene max);
+* folded input-gradient epilogue: dz = (a5 > 0) * (a5 H + c + max-pool rows), S1 = sum dz;
+* EPI_BNRELU (conv5's second pass): relu((A W^T + b) * s + t) stored.
+
+Ragged scenes (the last row tile of a scene partial) and several tiles per workgroup chunk
+exercise the cross-tile pipeline; duplicate max-pool rows exercise the sparse sums."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _args(L, B, N, K, Nc, dt, pro, epi, flags, cps=0):
+    a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=Nc, dtype=dt, prologue=pro, epilogue=epi,
+                   chunks_per_scene=cps, flags=flags)
+    rpc = L.load().pcs_gemm_geometry(ct.byref(a))
+    assert rpc > 0
+    return a, rpc
+
+
+def _variant(L, v):
+    return {"glds": (L.BF16, torch.bfloat16, 0), "noglds": (L.BF16, torch.bfloat16, L.FLAG_NO_GLDS),
+            "fp32": (L.F32, torch.float32, 0)}[v]
+
+
+@pytest.mark.parametrize("variant", ["glds", "noglds", "fp32"])
+@pytest.mark.parametrize("B,N,cps", [(2, 256 * 7 + 77, 2), (1, 200, 0), (3, 1024, 1)])
+def test_forward_stats_and_pool(variant, B, N, cps):
+    import pcs_amd._lib as L
+    dt, tdt, flags = _variant(L, variant)
+    K = Nc = 512
+    g = torch.Generator().manual_seed(B * 1000 + N)
+    A = torch.relu(torch.randn(B * N, K, generator=g)).to(tdt).to(DEV)
+    W = (torch.randn(Nc, K, generator=g) * 0.05).to(tdt).to(DEV)
+    a, rpc = _args(L, B, N, K, Nc, dt, L.PRO_RAW, L.EPI_FWD, flags, cps)
+    nch = B * a.chunks_per_scene
+    st = torch.empty(nch, Nc, 2, device=DEV)
+    pool = torch.empty(nch, Nc, 4, device=DEV)
+    a.A, a.W, a.C, a.stats, a.pool = A.data_ptr(), W.data_ptr(), None, st.data_ptr(), pool.data_ptr()
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    gamma = torch.randn(Nc, generator=g).to(DEV)       # signs pick max or min in the pool
+    beta = torch.zeros(Nc, device=DEV)
+    mean, rstd, scale, shift = (torch.empty(Nc, device=DEV) for _ in range(4))
+    ssum = torch.empty(B, Nc, device=DEV)
+    s = L.stream_ptr()
+    L.call("pcs_bn_fwd_finalize", L.ptr(st), B, N, Nc, a.chunks_per_scene, rpc, L.ptr(gamma), L.ptr(beta),
+           None, None, None, 0.1, 1e-5, 0, L.ptr(mean), L.ptr(rstd), L.ptr(scale), L.ptr(shift), L.ptr(ssum), s)
+    gp = torch.empty(B, Nc, device=DEV)
+    am = torch.empty(B, Nc, dtype=torch.int32, device=DEV)
+    ysel = torch.empty(B, Nc, device=DEV)
+    L.call("pcs_pool_finalize", L.ptr(pool), B, N, Nc, a.chunks_per_scene, L.ptr(scale), L.ptr(shift),
+           L.ptr(gp), L.ptr(am), L.ptr(ysel), s)
+    torch.cuda.synchronize()
+    y = (A.double() @ W.double().T)
+    ym, yv = y.mean(0), y.var(0, unbiased=False)
+    scl = y.abs().max().item()
+    # the 256x256 register-staged kernel (noglds) takes its statistics from the bf16-rounded
+    # stored tile; the LDS-DMA and fp32 kernels from the fp32 accumulators
+    mtol, vtol = (5e-4, 5e-3) if variant == "noglds" else (1e-5, 1e-4)
+    err_m = float((mean.double() - ym).abs().max())
+    assert err_m < mtol * scl, err_m
+    var = 1.0 / rstd.double() ** 2 - 1e-5
+    err_v = float(((var - yv).abs() / yv).max())
+    assert err_v < vtol, err_v
+    assert abs(ssum.double().sum().item() - y.sum().item()) < mtol * y.abs().sum().item()
+    yb = y.view(B, N, Nc)
+    sgn = torch.where(gamma > 0, 1.0, -1.0).double()
+    ext = (yb * sgn).max(1).values * sgn                   # max for gamma > 0, min for gamma < 0
+    ptol = 4e-3 if variant == "noglds" else 1e-5          # noglds: bf16-rounded candidates
+    assert float((ysel.double() - ext).abs().max()) < ptol * scl
+    rows = am.long() - (torch.arange(B, device=DEV) * N)[:, None]
+    assert ((rows >= 0) & (rows < N)).all()
+    at = yb.gather(1, rows[:, None, :]).squeeze(1)         # value at the reported row
+    assert float((at - ext).abs().max()) < ptol * scl
+
+
+@pytest.mark.parametrize("variant", ["glds", "noglds", "fp32"])
+@pytest.mark.parametrize("B,N,cps", [(2, 256 * 5 + 33, 2), (1, 300, 0)])
+def test_folded_dgrad_sparse_mask_s1(variant, B, N, cps):
+    import pcs_amd._lib as L
+    dt, tdt, flags = _variant(L, variant)
+    K = 512
+    g = torch.Generator().manual_seed(7 + N)
+    A = torch.relu(torch.randn(B * N, K, generator=g)).to(tdt).to(DEV)
+    H = (torch.randn(K, K, generator=g) * 0.05).to(tdt).to(DEV)
+    c = (torch.randn(K, generator=g) * 0.1).to(DEV)
+    Pc = 256
+    Wsp = (torch.randn(Pc, K, generator=g) * 0.1).to(DEV)
+    am = torch.randint(0, N, (B, Pc), generator=g)
+    am[:, 1] = am[:, 0]                                   # two channels on one row
+    am[:, 2] = N - 1                                      # the scene's last (ragged-tile) row
+    am = (am + torch.arange(B)[:, None] * N).int().to(DEV)
+    sp = torch.randn(B, Pc, generator=g).to(DEV)
+    a, rpc = _args(L, B, N, K, K, dt, L.PRO_RAW, L.EPI_DGRAD, flags, cps)
+    nch = B * a.chunks_per_scene
+    st = torch.empty(nch, K, 2, device=DEV)
+    out = torch.empty(B * N, K, dtype=tdt, device=DEV)
+    a.A, a.W, a.C, a.Yp, a.bias = A.data_ptr(), H.data_ptr(), out.data_ptr(), A.data_ptr(), c.data_ptr()
+    a.pool_idx, a.pool_coef, a.pool_w, a.pool_ldw, a.pool_c = am.data_ptr(), sp.data_ptr(), Wsp.data_ptr(), K, Pc
+    a.stats = st.data_ptr()
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    torch.cuda.synchronize()
+    v = A.double() @ H.double().T + c.double()
+    for b in range(B):
+        for q in range(Pc):
+            v[am[b, q].long()] += sp[b, q].double() * Wsp[q].double()
+    dz = torch.where(A.double() > 0, v, torch.zeros_like(v))
+    tol = 1e-5 if variant == "fp32" else 1e-2
+    err = float((out.double() - dz).abs().max())
+    assert err < tol * dz.abs().max().item(), err
+    s1 = st[..., 0].double().sum(0)
+    err = float((s1 - dz.sum(0)).abs().max())
+    assert err < (1e-5 if variant == "fp32" else 1e-3) * dz.abs().sum(0).max().item(), err
+
+
+@pytest.mark.parametrize("variant", ["big", "fp32"])
+def test_bnrelu_epilogue(variant):
+    import pcs_amd._lib as L
+    dt, tdt = (L.BF16, torch.bfloat16) if variant == "big" else (L.F32, torch.float32)
+    B, N, K, Nc = 2, 700, 128, 1024
+    g = torch.Generator().manual_seed(3)
+    Y = torch.randn(B * N, K, generator=g).to(tdt).to(DEV)
+    ps = (torch.rand(K, generator=g) + 0.5).to(DEV)
+    pt = (torch.randn(K, generator=g) * 0.2).to(DEV)
+    W = (torch.randn(Nc, K, generator=g) * 0.1).to(tdt).to(DEV)
+    bias = (torch.randn(Nc, generator=g) * 0.1).to(DEV)
+    es = torch.randn(Nc, generator=g).to(DEV)
+    et = (torch.randn(Nc, generator=g) * 0.3).to(DEV)
+    a, _ = _args(L, B, N, K, Nc, dt, L.PRO_BNRELU, L.EPI_BNRELU, 0)
+    out = torch.empty(B * N, Nc, dtype=tdt, device=DEV)
+    a.A, a.W, a.C, a.pa, a.pb, a.bias, a.es, a.et = (Y.data_ptr(), W.data_ptr(), out.data_ptr(), ps.data_ptr(),
+                                                      pt.data_ptr(), bias.data_ptr(), es.data_ptr(), et.data_ptr())
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    torch.cuda.synchronize()
+    x = torch.relu(Y.float() * ps + pt).to(tdt).double()     # the prologue rounds to dtype
+    ref = torch.relu((x @ W.double().T + bias.double()) * es.double() + et.double())
+    tol = 1e-5 if variant == "fp32" else 1e-2
+    err = float((out.double() - ref).abs().max())
+    assert err < tol * ref.abs().max().item(), err
+
+
+def test_bn_s2_from_r():
+    """S2 = rstd (sum_k W R - mean S1), rewritten into the (S1, S2) partials (chunk 0 total)."""
+    import pcs_amd._lib as L
+    g = torch.Generator().manual_seed(11)
+    C, Cin, nch = 256, 128, 5
+    R = torch.randn(C, Cin, generator=g).to(DEV)
+    W = torch.randn(C, Cin, generator=g).to(DEV)
+    mean = torch.randn(C, generator=g).to(DEV)
+    rstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    st = torch.randn(nch, C, 2, generator=g).to(DEV)
+    s1 = st[..., 0].double().sum(0)
+    L.call("pcs_bn_s2_from_r", L.ptr(st), nch, C, L.ptr(R), L.ptr(W), L.F32, Cin, Cin, L.ptr(mean), L.ptr(rstd),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    ref = rstd.double() * ((W.double() * R.double()).sum(1) - mean.double() * s1)
+    err = float((st[0, :, 1].double() - ref).abs().max())
+    assert err < 1e-5 * ref.abs().max().item(), err
+    assert (st[1:, :, 1] == 0).all()
+    assert torch.equal(st[..., 0].double().sum(0), s1)

@@ -1,0 +1,75 @@
+"""Micro-benchmark of the global_feat GEMMs at the cfg2 shape (M = 4 x 128^3 rows, 1024 x 1024,
+bf16, a5-like operand) with each epilogue feature on/off: the LDS-DMA kernel (gemm_glds.hip)
+against the register-staged 256x256 kernel (FLAG_NO_GLDS).  Prints ms and TF/s per variant."""
+import ctypes as ct
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pcs_amd._lib as L  # noqa: E402
+
+
+def timeit(fn, reps=4):
+    fn()
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / reps
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    N = 128 ** 3
+    M = B * N
+    K = Nc = 1024
+    dev = torch.device("cuda")
+    lib = L.load()
+    A = torch.relu(torch.randn(M, K, device=dev)).to(torch.bfloat16)
+    W = (torch.randn(Nc, K, device=dev) * 0.03).to(torch.bfloat16)
+    C = torch.empty(M, Nc, device=dev, dtype=torch.bfloat16)
+    c = torch.randn(Nc, device=dev) * 0.1
+    am = torch.randint(0, N, (B, K), device=dev, dtype=torch.int32) + \
+        (torch.arange(B, device=dev, dtype=torch.int32) * N)[:, None]
+    sp = torch.randn(B, K, device=dev)
+    Wsp = torch.randn(K, Nc, device=dev) * 0.03
+    flops = 2.0 * M * K * Nc
+
+    def run(name, epi, flags=0, **kw):
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=Nc, dtype=L.BF16, prologue=L.PRO_RAW,
+                       epilogue=epi, chunks_per_scene=0, flags=flags)
+        lib.pcs_gemm_geometry(ct.byref(a))
+        nch = B * a.chunks_per_scene
+        keep = {}
+        if kw.pop("stats", False):
+            keep["stats"] = torch.empty(nch, Nc, 2, device=dev)
+        if kw.pop("pool", False):
+            keep["pool"] = torch.empty(nch, Nc, 4, device=dev)
+        kw.update(keep)
+        a.A, a.W = A.data_ptr(), W.data_ptr()
+        a.C = kw.pop("C").data_ptr() if "C" in kw else None
+        if kw.pop("sparse", False):
+            a.pool_idx, a.pool_coef, a.pool_w, a.pool_ldw, a.pool_c = am.data_ptr(), sp.data_ptr(), Wsp.data_ptr(), Nc, K
+        for k, v in kw.items():
+            setattr(a, k, L.ptr(v))
+        ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
+        print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
+
+    for fl, tag in ((0, "glds"), (L.FLAG_NO_GLDS, "big ")):
+        run(f"[{tag}] fwd, no epilogue work", L.EPI_FWD, fl)
+        run(f"[{tag}] fwd + stats", L.EPI_FWD, fl, stats=True)
+        run(f"[{tag}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True)
+    run("[glds] dgrad: mask + store", L.EPI_DGRAD, 0, C=C, Yp=A)
+    run("[glds] dgrad: mask + store + bias + S1", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True)
+    run("[glds] dgrad: + sparse rows", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True, sparse=True)
+    run("[gen ] dgrad (generic kernel, FLAG_NO_GLDS)", L.EPI_DGRAD, L.FLAG_NO_GLDS, C=C, Yp=A, bias=c, stats=True,
+        sparse=True)
+
+
+if __name__ == "__main__":
+    main()
