@@ -35,7 +35,8 @@ enum { PCS_OK = 0, PCS_EINVAL = -1000 };
 /* pcs_gemm_args.flags */
 enum {
   PCS_FLAG_GENERIC = 1, /* force the generic 128x{64,128} kernel (cross-checks)            */
-  PCS_FLAG_NO_GLDS = 2  /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
+  PCS_FLAG_NO_GLDS = 2, /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
+  PCS_FLAG_GLDS_FWD = 4 /* use the LDS-DMA kernel for a RAW statistics/max-pool forward too  */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
@@ -327,6 +328,21 @@ int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_i
 int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const float *alpha,
                 const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
                 pcs_stream_t stream);
+
+/*
+ * BatchNorm statistics of y = a W^T (W [C, Cin] in dtype, row stride ldw) from the Gram of a
+ * (G = a^T a [Cin, Cin] fp32, S = column sums [Cin], count rows): mean = W S / count and
+ * M2[c] = w_c (G - S S^T / count) w_c^T, assembled in fp64.  Written as per-scene partials
+ * stats[b, c] = (mean[c], M2[c] / num_scenes) for pcs_bn_fwd_finalize with
+ * chunks_per_scene = 1 and rows_per_chunk = scene_rows (merging B identical partials gives
+ * the totals).  The bf16 path's bn5 statistics (P:110): the Gram of a4 is needed by conv5's
+ * weight gradient anyway, and this replaces a statistics-only pass of the 1024-wide GEMM.
+ * Conditioning: the relative error is the Gram's times sum|w||w|G / var (~1e2 here), so the
+ * fp32 parity path keeps the direct statistics.
+ */
+int pcs_bn_stats_from_gram(const float *G, const float *S, int64_t count, const void *W, int32_t dtype,
+                           int64_t ldw, int32_t C, int32_t Cin, int64_t num_scenes, float *stats,
+                           pcs_stream_t stream);
 
 /*
  * S2 of a BN-fed layer's backward from R = dz^T a (pcs_wgrad with dy_mode RAW) instead of the

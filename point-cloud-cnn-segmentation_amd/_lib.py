@@ -43,6 +43,7 @@ class GemmArgs(ct.Structure):
 
 FLAG_GENERIC = 1
 FLAG_NO_GLDS = 2
+FLAG_GLDS_FWD = 4
 
 
 class WgradArgs(ct.Structure):
@@ -120,6 +121,7 @@ SIGNATURES = [
                                   _i32, _vp, _vp, _vp, _i64, _vp]),
     ("pcs_bn_fold", ct.c_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     ("pcs_bn_s2_from_r", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    ("pcs_bn_stats_from_gram", ct.c_int, [_vp, _vp, _i64, _vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp]),
     ("pcs_confusion", ct.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcs_argmax", ct.c_int, [_vp, _i64, _i64, _i32, _vp, _vp]),
     ("pcs_last_error", ct.c_char_p, []),

@@ -35,10 +35,10 @@ constexpr int OFF_RUN = STAGE_BYTES;               // [2 wm][256] float2: (mean,
 constexpr int OFF_POOL = OFF_RUN + 2 * 256 * 8;    // [2][256] float4: max, argmax, min, argmin
 constexpr int OFF_BIAS = OFF_POOL + 2 * 256 * 16;  // [256] f32
 constexpr int OFF_RUNN = OFF_BIAS + 256 * 4;       // [2] f32: rows merged per wave half
-constexpr int OFF_SPI = OFF_RUNN + 16;             // [1024] i32: sparse rows (max-pool argmax)
-constexpr int OFF_SPC = OFF_SPI + 1024 * 4;        // [1024] f32: sparse coefficients
-constexpr int OFF_BITS = OFF_SPC + 1024 * 4;       // [8] u32: hit bitmap of the tile's rows
-constexpr int LDS_BYTES = OFF_BITS + 64;
+constexpr int OFF_SPI = OFF_RUNN + 16;             // [1024] i32: sparse rows, sorted (max-pool argmax)
+constexpr int OFF_SPC = OFF_SPI + 1024 * 4;        // [1024] f32: their coefficients
+constexpr int OFF_SPK = OFF_SPC + 1024 * 4;        // [1024] u16: their channel (row of pool_w)
+constexpr int LDS_BYTES = OFF_SPK + 1024 * 2;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 constexpr int SPMAX = 1024;
 
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   float *runn = reinterpret_cast<float *>(lds + OFF_RUNN);
   int *spi = reinterpret_cast<int *>(lds + OFF_SPI);
   float *spc = reinterpret_cast<float *>(lds + OFF_SPC);
-  uint32_t *bits = reinterpret_cast<uint32_t *>(lds + OFF_BITS);
+  uint16_t *spk = reinterpret_cast<uint16_t *>(lds + OFF_SPK);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -155,10 +155,22 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     }
   }
   if (tid < 2) runn[tid] = 0.f;
-  if (sparse) {
-    for (int c = tid; c < a.pool_c; c += THREADS) {
-      spi[c] = a.pool_idx[(int64_t)scene * a.pool_c + c];
-      spc[c] = a.pool_coef[(int64_t)scene * a.pool_c + c];
+  int nsp = 0;
+  if (sparse) {   // the scene's max-pool rows sorted by row (rank sort; staging LDS is free here)
+    nsp = a.pool_c;
+    int *tr = reinterpret_cast<int *>(lds);
+    for (int c = tid; c < nsp; c += THREADS) tr[c] = a.pool_idx[(int64_t)scene * nsp + c];
+    __syncthreads();
+    for (int c = tid; c < nsp; c += THREADS) {
+      const int r = tr[c];
+      int rank = 0;
+      for (int q = 0; q < nsp; ++q) {
+        const int rq = tr[q];
+        rank += rq < r || (rq == r && q < c);
+      }
+      spi[rank] = r;
+      spc[rank] = a.pool_coef[(int64_t)scene * nsp + c];
+      spk[rank] = (uint16_t)c;
     }
   }
   __syncthreads();
@@ -424,35 +436,32 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         run_n += (float)nvw;
       }
     } else {   // MODE_DGRAD
-      if (sparse) {   // the tile's max-pool rows: a bitmap, then the rare per-row sums
-        if (tid < 8) bits[tid] = 0u;
-        lds_barrier();
-        for (int c = tid; c < a.pool_c; c += THREADS) {
-          const int64_t m = (int64_t)spi[c] - rb;
-          if (m >= 0 && m < valid) atomicOr(&bits[m >> 5], 1u << (m & 31));
+      if (sparse) {   // the tile's max-pool rows (rare): first entry >= rb by binary search
+        int lo = 0, hi = nsp;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if ((int64_t)spi[mid] < rb) lo = mid + 1; else hi = mid;
         }
-        lds_barrier();
+        for (int p = lo; p < nsp && (int64_t)spi[p] < rb + valid; ++p) {
+          const int m = (int)((int64_t)spi[p] - rb) - wm * 128;   // row within this wave's half
+          if (m < 0 || m >= 128 || (m & 15) != lr) continue;
+          const float w = spc[p];
+          const float *wr = a.pool_w + (int64_t)spk[p] * a.pool_ldw + n0 + wn * 64 + 4 * lg;
+          float4 q[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int m = wm * 128 + i * 16 + lr;
-          if ((bits[m >> 5] >> (m & 31)) & 1u) {
-            const int grow = (int)(rb + m);
-            for (int c = 0; c < a.pool_c; ++c) {
-              if (spi[c] != grow) continue;
-              const float w = spc[c];
-              const float *wr = a.pool_w + (int64_t)c * a.pool_ldw + n0 + wn * 64 + 4 * lg;
+          for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(wr + j * 16);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const float4 q = *reinterpret_cast<const float4 *>(wr + j * 16);
-                acc[i][j][0] = fmaf(w, q.x, acc[i][j][0]);
-                acc[i][j][1] = fmaf(w, q.y, acc[i][j][1]);
-                acc[i][j][2] = fmaf(w, q.z, acc[i][j][2]);
-                acc[i][j][3] = fmaf(w, q.w, acc[i][j][3]);
-              }
+          for (int i = 0; i < 8; ++i) {
+            if (i != (m >> 4)) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              acc[i][j][0] = fmaf(w, q[j].x, acc[i][j][0]);
+              acc[i][j][1] = fmaf(w, q[j].y, acc[i][j][1]);
+              acc[i][j][2] = fmaf(w, q[j].z, acc[i][j][2]);
+              acc[i][j][3] = fmaf(w, q[j].w, acc[i][j][3]);
             }
           }
         }
-        lds_barrier();   // bitmap reads done before the next tile's reset
       }
       float s1[16];
 #pragma unroll
@@ -528,7 +537,10 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS))) return false;
   if (a.prologue != PCS_PRO_RAW || a.K % (2 * BK) != 0 || a.Ncols % BN != 0) return false;
-  if (a.epilogue == PCS_EPI_FWD) return a.C == nullptr && a.scene_bias == nullptr;
+  // forward (statistics + max-pool epilogue): measured slower than the register-staged
+  // 256x256 kernel on the same RAW operand (tools/bench_glds.py), so only on request
+  if (a.epilogue == PCS_EPI_FWD)
+    return (a.flags & PCS_FLAG_GLDS_FWD) && a.C == nullptr && a.scene_bias == nullptr;
   if (a.epilogue == PCS_EPI_DGRAD)   // mask read from the operand itself, no S2, no addend
     return a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask &&
            (!a.pool_w || a.pool_c <= SPMAX);

@@ -180,6 +180,40 @@ __global__ __launch_bounds__(256) void fold_h_tiled_kernel(const float *__restri
     }
 }
 
+// BN statistics of y = a W^T from G = a^T a and S: one block per output channel c,
+// mean = w.S / n, M2 = sum_jk w_j w_k (G_jk - S_j S_k / n), fp64 (w cached in LDS)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_gram_kernel(const float *__restrict__ G, const float *__restrict__ S,
+                                                            double n, const T *__restrict__ W, int64_t ldw, int C,
+                                                            int Cin, int B, float *__restrict__ stats) {
+  __shared__ double w[1024];
+  __shared__ double sh[256][2];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double dm = 0.0;
+  for (int k = tid; k < Cin; k += 256) {
+    w[k] = (double)load_elem(W, (int64_t)c * ldw + k);
+    dm += w[k] * (double)S[k];
+  }
+  __syncthreads();
+  double q = 0.0;
+  for (int j = tid; j < Cin; j += 256) {
+    const double sj = (double)S[j] / n;
+    double row = 0.0;
+    for (int k = 0; k < Cin; ++k) row += ((double)G[(int64_t)j * Cin + k] - sj * (double)S[k]) * w[k];
+    q += w[j] * row;
+  }
+  sh[tid][0] = dm; sh[tid][1] = q;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) { sh[tid][0] += sh[tid + st][0]; sh[tid][1] += sh[tid + st][1]; }
+    __syncthreads();
+  }
+  if (tid < B) {
+    const double mean = sh[0][0] / n, m2 = sh[0][1] > 0.0 ? sh[0][1] : 0.0;
+    *reinterpret_cast<float2 *>(stats + ((int64_t)tid * C + c) * 2) = make_float2((float)mean, (float)(m2 / B));
+  }
+}
+
 // S2 of a BN-fed layer from R = dz^T a: rstd (sum_k W[c,k] R[c,k] - mean S1), rewritten into
 // the per-chunk partials (chunk 0 = total, others 0).  One block per channel, fp64 sums.
 template <typename T>
@@ -274,6 +308,25 @@ extern "C" int pcs_bn_s2_from_r(float *stats, int64_t num_chunks, int32_t C, con
                        reinterpret_cast<const float *>(W), ldw, (int)Cin, mean, rstd);
   else
     return pcs_set_einval("pcs_bn_s2_from_r", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_bn_stats_from_gram(const float *G, const float *S, int64_t count, const void *W, int32_t dtype,
+                                      int64_t ldw, int32_t C, int32_t Cin, int64_t num_scenes, float *stats,
+                                      pcs_stream_t stream) {
+  if (!G || !S || !W || !stats || count <= 0 || C <= 0 || Cin <= 0 || Cin > 1024 || ldw < Cin ||
+      num_scenes <= 0 || num_scenes > 256)
+    return pcs_set_einval("pcs_bn_stats_from_gram", "bad arguments (Cin <= 1024, num_scenes <= 256)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(bn_stats_gram_kernel<bf16_t>, dim3(C), dim3(256), 0, st, G, S, (double)count,
+                       reinterpret_cast<const bf16_t *>(W), ldw, (int)C, (int)Cin, (int)num_scenes, stats);
+  else if (dtype == PCS_F32)
+    hipLaunchKernelGGL(bn_stats_gram_kernel<float>, dim3(C), dim3(256), 0, st, G, S, (double)count,
+                       reinterpret_cast<const float *>(W), ldw, (int)C, (int)Cin, (int)num_scenes, stats);
+  else
+    return pcs_set_einval("pcs_bn_stats_from_gram", "bad dtype");
   PCS_CHECK_LAUNCH();
   return 0;
 }

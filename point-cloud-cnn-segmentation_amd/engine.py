@@ -91,6 +91,7 @@ class Saved:
     x: torch.Tensor = None
     logits: torch.Tensor = None
     wc: dict = None                               # cast weights used by this pass
+    gram4: tuple = None                           # (G, S) of a4 when the forward computed it
 
 
 class Engine:
@@ -215,6 +216,18 @@ class Engine:
         self._launch(tag, fn, ct.byref(a), self._stream())
         return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
+    def _gram(self, Y, s_, t_, B, N, C, tag=None):
+        """(G, S) = (a^T a, column sums of a) for a = relu(Y*s + t) (pcs_gram)."""
+        dev = Y.device
+        G = torch.empty(C, C, dtype=torch.float32, device=dev)
+        S = torch.empty(C, dtype=torch.float32, device=dev)
+        sps = ct.c_int32(0)
+        nbytes = L.load().pcs_gram_workspace(B, N, C, self.dt, ct.byref(sps))
+        ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
+        self._launch(tag, "pcs_gram", L.ptr(Y), L.ptr(s_), L.ptr(t_), B, N, C, self.dt, sps.value, L.ptr(ws),
+                     L.ptr(G), L.ptr(S), self._stream())
+        return G, S, ws
+
     # ------------------------------------------------------------------ forward
     def forward(self, P, bufs, x, *, train, masks=None, seed=0, head_mode=L.HEAD_FWD,
                 labels=None, class_weight=None, wsum=None, want_logits=True, saved=None):
@@ -276,10 +289,19 @@ class Engine:
         layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"])
         layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"])
 
-        # conv5 (P:110): a statistics-only pass (nothing stored), then the same GEMM with
-        # bn5 + ReLU applied in the epilogue, storing a5 = relu(bn5(y5)) for global_feat
-        st, cps, rpc = stats_buf(128, 1024) if train else (None, 0, 0)
-        if train:
+        # conv5 (P:110): bn5's statistics first, then the GEMM with bn5 + ReLU applied in the
+        # epilogue, storing a5 = relu(bn5(y5)) for global_feat.  fp32: a statistics-only pass
+        # of the GEMM.  bf16: from the Gram of a4 (which conv5's weight gradient needs anyway),
+        # mean = W5 S4 / M and M2 = w (G4 - S4 S4^T / M) w^T per channel.
+        st, cps, rpc = (None, 0, 0)
+        if train and self.dt == L.BF16:
+            c4 = sv.bn["bn4"]
+            sv.gram4 = self._gram(sv.ys["conv4"], c4.scale, c4.shift, B, N, 128, tag="fwd_stats:conv5")
+            st, cps, rpc = torch.empty(B, 1024, 2, dtype=torch.float32, device=dev), 1, N
+            L.call("pcs_bn_stats_from_gram", L.ptr(sv.gram4[0]), L.ptr(sv.gram4[1]), M, L.ptr(wc["conv5"][0]),
+                   self.dt, 128, 1024, 128, B, L.ptr(st), s)
+        elif train:
+            st, cps, rpc = stats_buf(128, 1024)
             self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_FWD, sv.ys["conv4"], wc["conv5"][0], None,
                        stats=st, tag="fwd_stats:conv5", **bnrelu("bn4"))
         sv.bn["bn5"] = self._bn_finalize("bn5", st, B, N, 1024, cps, rpc, P, bufs, train, dev,
@@ -539,13 +561,8 @@ class Engine:
         self._gemm(B, N, 128, 128, L.PRO_BNRELU, L.EPI_DGRAD, ys["conv4"], h4, bufA, pa=pc4.scale,
                    pb=pc4.shift, Yp=ys["conv4"], es=pc4.scale, et=pc4.shift, emean=pc4.mean,
                    erstd=pc4.rstd, addend=pbuf, stats=st, tag="dgrad2:conv5")
-        g4 = torch.empty(128, 128, dtype=torch.float32, device=dev)
-        s4 = torch.empty(128, dtype=torch.float32, device=dev)
-        sps4 = ct.c_int32(0)
-        nbytes = L.load().pcs_gram_workspace(B, N, 128, self.dt, ct.byref(sps4))
-        ws4 = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
-        self._launch("gram:conv4", "pcs_gram", L.ptr(ys["conv4"]), L.ptr(pc4.scale), L.ptr(pc4.shift), B, N,
-                     128, self.dt, sps4.value, L.ptr(ws4), L.ptr(g4), L.ptr(s4), s)
+        g4, s4, ws4 = sv.gram4 if sv.gram4 is not None else \
+            self._gram(ys["conv4"], pc4.scale, pc4.shift, B, N, 128, tag="gram:conv4")
         self._launch("wgrad_asm:conv5", "pcs_gram_wgrad", L.ptr(g4), L.ptr(s4), L.ptr(W5), 128, L.ptr(be5),
                      L.ptr(ga5), None, None, None, None, None, B, 1024, 128, self.dt, L.ptr(r5), L.ptr(al5),
                      L.ptr(G("conv5.weight")), 128, s)

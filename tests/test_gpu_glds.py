@@ -37,6 +37,8 @@ def _variant(L, v):
 def test_forward_stats_and_pool(variant, B, N, cps):
     import pcs_amd._lib as L
     dt, tdt, flags = _variant(L, variant)
+    if variant == "glds":
+        flags |= L.FLAG_GLDS_FWD        # the LDS-DMA forward is opt-in (see gemm_glds.hip)
     K = Nc = 512
     g = torch.Generator().manual_seed(B * 1000 + N)
     A = torch.relu(torch.randn(B * N, K, generator=g)).to(tdt).to(DEV)
@@ -146,6 +148,34 @@ def test_bnrelu_epilogue(variant):
     tol = 1e-5 if variant == "fp32" else 1e-2
     err = float((out.double() - ref).abs().max())
     assert err < tol * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_bn_stats_from_gram(dtype):
+    """bn5 statistics of y = a W^T from the Gram of a (bf16 path): the per-scene partials
+    finalise to the batch mean / biased variance of y."""
+    import pcs_amd._lib as L
+    dt, tdt = (L.BF16, torch.bfloat16) if dtype == "bf16" else (L.F32, torch.float32)
+    g = torch.Generator().manual_seed(5)
+    B, N, Cin, C = 3, 1000, 128, 512
+    a = torch.relu(torch.randn(B * N, Cin, generator=g) + 0.3).to(tdt).to(DEV)
+    W = (torch.randn(C, Cin, generator=g) * 0.08).to(tdt).to(DEV)
+    ad = a.double()
+    G = (ad.T @ ad).float()
+    S = ad.sum(0).float()
+    st = torch.empty(B, C, 2, device=DEV)
+    L.call("pcs_bn_stats_from_gram", L.ptr(G), L.ptr(S), B * N, L.ptr(W), dt, Cin, C, Cin, B, L.ptr(st),
+           L.stream_ptr())
+    mean, rstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
+    ones, zeros = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    L.call("pcs_bn_fwd_finalize", L.ptr(st), B, N, C, 1, N, L.ptr(ones), L.ptr(zeros), None, None, None,
+           0.1, 1e-5, 0, L.ptr(mean), L.ptr(rstd), L.ptr(scale), L.ptr(shift), None, L.stream_ptr())
+    torch.cuda.synchronize()
+    y = ad @ W.double().T
+    err_m = float((mean.double() - y.mean(0)).abs().max() / y.std(0).min())
+    var = 1.0 / rstd.double() ** 2 - 1e-5
+    err_v = float(((var - y.var(0, unbiased=False)) / y.var(0, unbiased=False)).abs().max())
+    assert err_m < 1e-5 and err_v < 1e-4, (err_m, err_v)
 
 
 def test_bn_s2_from_r():
