@@ -35,8 +35,7 @@ enum { PCS_OK = 0, PCS_EINVAL = -1000 };
 /* pcs_gemm_args.flags */
 enum {
   PCS_FLAG_GENERIC = 1, /* force the generic 128x{64,128} kernel (cross-checks)            */
-  PCS_FLAG_NO_GLDS = 2, /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
-  PCS_FLAG_GLDS_FWD = 4 /* use the LDS-DMA kernel for a RAW statistics/max-pool forward too  */
+  PCS_FLAG_NO_GLDS = 2  /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
@@ -93,7 +92,9 @@ typedef struct {
   const uint8_t *c_mask;/* [M, Ncols/8] keep bits of the dropout after BN_{l-1} (DGRAD) */
   float c_keep_scale;
   const void *Yp;       /* [M, Ncols] dtype: Y_{l-1} (DGRAD) */
-  const float *es, *et; /* [Ncols] BN_{l-1} scale/shift (DGRAD ReLU mask) */
+  const float *es, *et; /* [Ncols] BN_{l-1} scale/shift (DGRAD ReLU mask); BNRELU: this layer's;
+                           FWD with pool: optional, only sign(es) is used (the pool may then keep
+                           just the max (es >= 0) or the min (es < 0) that pcs_pool_finalize reads) */
   const float *emean, *erstd; /* [Ncols] BN_{l-1} batch mean / rstd (DGRAD S2) */
   float *stats;         /* [B*chunks_per_scene, Ncols, 2] partials (FWD, DGRAD) or NULL */
   float *pool;          /* [B*chunks_per_scene, Ncols, 4] (maxv, argmax, minv, argmin) or NULL */

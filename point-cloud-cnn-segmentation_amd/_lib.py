@@ -43,7 +43,6 @@ class GemmArgs(ct.Structure):
 
 FLAG_GENERIC = 1
 FLAG_NO_GLDS = 2
-FLAG_GLDS_FWD = 4
 
 
 class WgradArgs(ct.Structure):

@@ -32,13 +32,16 @@ constexpr int REG = 128 * BK * 2;                  // one region: 128 rows x 128
 constexpr int KBUF = 4 * REG;                      // A-lo | A-hi | B-lo | B-hi
 constexpr int STAGE_BYTES = 2 * KBUF;              // 128 KB
 constexpr int OFF_RUN = STAGE_BYTES;               // [2 wm][256] float2: (mean, m2) | (S1, 0)
-constexpr int OFF_POOL = OFF_RUN + 2 * 256 * 8;    // [2][256] float4: max, argmax, min, argmin
-constexpr int OFF_BIAS = OFF_POOL + 2 * 256 * 16;  // [256] f32
+constexpr int OFF_BIAS = OFF_RUN + 2 * 256 * 8;    // [256] f32
 constexpr int OFF_RUNN = OFF_BIAS + 256 * 4;       // [2] f32: rows merged per wave half
 constexpr int OFF_SPI = OFF_RUNN + 16;             // [1024] i32: sparse rows, sorted (max-pool argmax)
 constexpr int OFF_SPC = OFF_SPI + 1024 * 4;        // [1024] f32: their coefficients
 constexpr int OFF_SPK = OFF_SPC + 1024 * 4;        // [1024] u16: their channel (row of pool_w)
-constexpr int LDS_BYTES = OFF_SPK + 1024 * 2;
+constexpr int OFF_UNI = OFF_SPK + 1024 * 2;        // 16 KB, per mode:
+constexpr int OFF_POOL = OFF_UNI;                  //   FWD: [2][256] float4 max, argmax, min, argmin
+constexpr int OFF_SGN = OFF_UNI + 2 * 256 * 16;    //        [256] f32 +1 / -1 (pool keeps max / min)
+constexpr int OFF_MASK = OFF_UNI;                  //   DGRAD: 2 x [256 rows][8 words] ReLU mask bits
+constexpr int LDS_BYTES = OFF_UNI + 2 * 256 * 8 * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 constexpr int SPMAX = 1024;
 
@@ -118,6 +121,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   int *spi = reinterpret_cast<int *>(lds + OFF_SPI);
   float *spc = reinterpret_cast<float *>(lds + OFF_SPC);
   uint16_t *spk = reinterpret_cast<uint16_t *>(lds + OFF_SPK);
+  float *lsgn = reinterpret_cast<float *>(lds + OFF_SGN);
+  uint32_t *mbits = reinterpret_cast<uint32_t *>(lds + OFF_MASK);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -148,10 +153,13 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   if (tid < BN) {
     lbias[tid] = a.bias ? a.bias[n0 + tid] : 0.f;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      run[h * BN + tid] = make_float2(0.f, 0.f);
-      runp[h * BN + tid] = make_float4(-__builtin_huge_valf(), __int_as_float(0x7fffffff),
-                                       __builtin_huge_valf(), __int_as_float(0x7fffffff));
+    for (int h = 0; h < 2; ++h) run[h * BN + tid] = make_float2(0.f, 0.f);
+    if constexpr (MODE == MODE_FWD) {
+      lsgn[tid] = (a.es && a.es[n0 + tid] < 0.f) ? -1.f : 1.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        runp[h * BN + tid] = make_float4(-__builtin_huge_valf(), __int_as_float(0x7fffffff),
+                                         __builtin_huge_valf(), __int_as_float(0x7fffffff));
     }
   }
   if (tid < 2) runn[tid] = 0.f;
@@ -230,36 +238,37 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         bfr[j0 + j][kk] = *reinterpret_cast<const bf16x8 *>(base + q * 128 + swz(q, kk * 4 + lg) * 16);
     }
   };
-  // DGRAD: the ReLU mask of bn5 comes from the operand (Yp == A, K == Ncols): the wave's
-  // output columns n0 + wn*64 .. +64 are the k-columns of K-tile (n0 >> 6) + wn.  Bit j*4+r
-  // of mbit(i) <-> (row wm*128 + i*16 + lr, column wn*64 + j*16 + 4*lg + r); two rows per word.
-  uint32_t mb[4];
-  auto read_mask = [&](int buf, int region, int i0) {
-    const char *base = lds + buf * KBUF + region * REG;
+  // DGRAD: the ReLU mask of bn5 comes from the operand (Yp == A, K == Ncols): the tile's
+  // output columns n0 .. n0+255 are the k-columns of K-tiles (n0 >> 6) .. +3.  In phase 1 of
+  // each of those K-tiles all 512 threads turn the staged a5 values into bits (thread: tile
+  // row tid/2, 32 columns; bf16 x > 0 <=> sign clear and magnitude nonzero) in a per-tile-
+  // parity LDS bitmap [256 rows][8 words] that the epilogue reads: the work is spread evenly
+  // over all waves instead of stalling one wave column at the phase barriers.
+  // region: 0 = A-lo (phase 1), 1 = A-hi (phase 3); thread: region row tid/4, 16 columns
+  auto extract_mask = [&](int buf, int region, int kq, int par) {
+    const int q = tid >> 2, h = tid & 3;
+    const int t = a_row(region, q);
+    const char *base = lds + buf * KBUF + region * REG + q * 128;
+    uint32_t w = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = wm * 64 + i * 16 + lr;
-      uint32_t m = 0;
+    for (int c = 0; c < 2; ++c) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(base + q * 128 + swz(q, 2 * j + (lg >> 1)) * 16 +
-                                                         (lg & 1) * 8);
-        const uint32_t b0 = (int16_t)(v.x & 0xffffu) > 0, b1 = (int16_t)(v.x >> 16) > 0;
-        const uint32_t b2 = (int16_t)(v.y & 0xffffu) > 0, b3 = (int16_t)(v.y >> 16) > 0;
-        m |= (b0 | (b1 << 1) | (b2 << 2) | (b3 << 3)) << (4 * j);
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t x = v[d];
+        const uint32_t pos = ((x & 0x7fff7fffu) + 0x7fff7fffu) & ~x & 0x80008000u;
+        w |= ((pos >> 15) & 1u) << (c * 8 + d * 2);
+        w |= (pos >> 31) << (c * 8 + d * 2 + 1);
       }
-      if (i & 1) mb[(i0 + i) >> 1] |= m << 16;
-      else mb[(i0 + i) >> 1] = m;
     }
+    reinterpret_cast<uint16_t *>(mbits + par * 2048 + t * 8 + kq * 2)[h] = (uint16_t)w;
   };
 
   f32x4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i < 4) mb[i] = 0u;
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
   auto mfma_quad = [&](int i0, int j0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -277,8 +286,14 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   wait_vm<6>();
   barrier_raw();
 
-  const int ktm = (n0 >> 6) + wn;   // DGRAD: the K-tile holding this wave's mask columns
+  const int kq0 = n0 >> 6;          // DGRAD: first K-tile holding this tile's mask columns
   float run_n = 0.f;                // rows of this wave's half merged so far (uniform)
+  // The two wave halves run one barrier apart (the template's stagger): while the waves of
+  // one half issue their MFMAs, the other half's ds_reads / glds / waits proceed, so each
+  // SIMD (one wave of each half) keeps its matrix pipe busy.  Each wave retires its own
+  // fragment reads before arriving at a phase's first barrier, which keeps the restaging of
+  // a region one phase after its last read safe across the stagger.
+  if (wm == 1) barrier_raw();
 
   for (int qs = 0; qs < total; ++qs) {
     const int buf = qs & 1;
@@ -286,11 +301,11 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
     read_a(buf, 0);
     read_b(buf, 2, 0);
-    if (MODE == MODE_DGRAD && kt == ktm) read_mask(buf, 0, 0);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
     issue(qs + 1, 1);
     wait_vm<10>();
-    barrier_raw();
     wait_lgkm0();
+    barrier_raw();
     __builtin_amdgcn_s_setprio(1);
     mfma_quad(0, 0);
     __builtin_amdgcn_s_setprio(0);
@@ -299,18 +314,18 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     read_b(buf, 3, 2);
     issue(qs + 2, 0);
     wait_vm<10>();
-    barrier_raw();
     wait_lgkm0();
+    barrier_raw();
     __builtin_amdgcn_s_setprio(1);
     mfma_quad(0, 2);
     __builtin_amdgcn_s_setprio(0);
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
-    if (MODE == MODE_DGRAD && kt == ktm) read_mask(buf, 1, 4);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
     issue(qs + 2, 2);
-    barrier_raw();
     wait_lgkm0();
+    barrier_raw();
     __builtin_amdgcn_s_setprio(1);
     mfma_quad(4, 0);
     __builtin_amdgcn_s_setprio(0);
@@ -343,92 +358,88 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
     for (int i = 0; i < 8; ++i) rowok |= (uint32_t)(wm * 128 + i * 16 + lr < valid) << i;
 
+    // after the 16-lane row reductions every lane of a row group holds its group's 16 column
+    // results; lane lr then owns column e = lr of its group for the LDS bookkeeping
+    const int cme = wm * BN + wn * 64 + (lr >> 2) * 16 + 4 * lg + (lr & 3);
     if constexpr (MODE == MODE_FWD) {
       if (nvw > 0) {
         if (do_stats) {
-          // sums shifted by the half's running column mean, one Chan merge per column
-          float sh[16], s1[16], s2[16];
+          // sums shifted by the half's running column mean, one Chan merge per column;
+          // processed 4 columns (one j) at a time to keep registers for the accumulators
+          float S1 = 0.f, S2 = 0.f, SH = 0.f;
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            sh[e] = run[wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3)].x;
-            s1[e] = 0.f;
-            s2[e] = 0.f;
-          }
+          for (int j = 0; j < 4; ++j) {
+            float sh[4], s1[4], s2[4];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if ((rowok >> i) & 1u) {
-#pragma unroll
-              for (int e = 0; e < 16; ++e) {
-                const float d = acc[i][e >> 2][e & 3] - sh[e];
-                s1[e] += d;
-                s2[e] = fmaf(d, d, s2[e]);
-              }
+            for (int r = 0; r < 4; ++r) {
+              sh[r] = run[wm * BN + wn * 64 + j * 16 + 4 * lg + r].x;
+              s1[r] = 0.f;
+              s2[r] = 0.f;
             }
-          }
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            s1[e] = row_sum(s1[e]);
-            s2[e] = row_sum(s2[e]);
-          }
-          if (lr == 0) {
-            const float nt = (float)nvw;
+            for (int i = 0; i < 8; ++i) {
+              if ((rowok >> i) & 1u) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              const int c = wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3);
-              const float d1 = s1[e] / nt;
-              float n = run_n, mean = run[c].x, m2 = run[c].y;
-              chan_merge(n, mean, m2, nt, sh[e] + d1, fmaxf(s2[e] - s1[e] * d1, 0.f));
-              run[c] = make_float2(mean, m2);
-            }
-          }
-        }
-        if (do_pool) {
-          float mx[16], mn[16];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            mx[e] = -__builtin_huge_valf();
-            mn[e] = __builtin_huge_valf();
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if ((rowok >> i) & 1u) {
-#pragma unroll
-              for (int e = 0; e < 16; ++e) {
-                mx[e] = fmaxf(mx[e], acc[i][e >> 2][e & 3]);
-                mn[e] = fminf(mn[e], acc[i][e >> 2][e & 3]);
-              }
-            }
-          }
-          bool upd = false;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            mx[e] = row_max(mx[e]);
-            mn[e] = row_min(mn[e]);
-            const float4 q = runp[wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3)];
-            upd |= mx[e] > q.x || mn[e] < q.z;
-          }
-          // a tile beats a column's running max / min rarely: only then find its first row
-          if (__builtin_amdgcn_ballot_w64(upd)) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              int ix = 0x7fffffff, in = 0x7fffffff;
-#pragma unroll
-              for (int i = 7; i >= 0; --i) {
-                if ((rowok >> i) & 1u) {
-                  const float v = acc[i][e >> 2][e & 3];
-                  const int row = (int)(rb + wm * 128 + i * 16 + lr);
-                  if (v == mx[e]) ix = row;
-                  if (v == mn[e]) in = row;
+                for (int r = 0; r < 4; ++r) {
+                  const float d = acc[i][j][r] - sh[r];
+                  s1[r] += d;
+                  s2[r] = fmaf(d, d, s2[r]);
                 }
               }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              s1[r] = row_sum(s1[r]);
+              s2[r] = row_sum(s2[r]);
+              if (lr == j * 4 + r) { S1 = s1[r]; S2 = s2[r]; SH = sh[r]; }
+            }
+          }
+          const float nt = (float)nvw, d1 = S1 / nt;
+          float n = run_n, mean = run[cme].x, m2 = run[cme].y;
+          chan_merge(n, mean, m2, nt, SH + d1, fmaxf(S2 - S1 * d1, 0.f));
+          run[cme] = make_float2(mean, m2);
+        }
+        if (do_pool) {
+          // only the extremum pool_finalize will use: max where es >= 0 (bn scale > 0), min
+          // where es < 0, as vx = max(sgn * y); the argmax row is searched only for columns
+          // whose running extremum this tile improves (rare after the first tiles)
+          const float4 q = runp[cme];
+          const float sgl = lsgn[cme - wm * BN];
+          const float cur = sgl > 0.f ? q.x : -q.z;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float vx[4], sg[4];
+            float mine = -__builtin_huge_valf();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              sg[r] = lsgn[wn * 64 + j * 16 + 4 * lg + r];
+              float mx = -__builtin_huge_valf(), mn = __builtin_huge_valf();
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                if ((rowok >> i) & 1u) {
+                  mx = fmaxf(mx, acc[i][j][r]);
+                  mn = fminf(mn, acc[i][j][r]);
+                }
+              }
+              vx[r] = row_max(sg[r] > 0.f ? mx : -mn);
+              if (lr == j * 4 + r) mine = vx[r];
+            }
+            const bool upd = (lr >> 2) == j && mine > cur;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (__builtin_amdgcn_ballot_w64(upd && (lr & 3) == r) == 0) continue;
+              int ix = 0x7fffffff;
+#pragma unroll
+              for (int i = 7; i >= 0; --i) {
+                const float v = sg[r] > 0.f ? acc[i][j][r] : -acc[i][j][r];
+                if (((rowok >> i) & 1u) && v == vx[r]) ix = (int)(rb + wm * 128 + i * 16 + lr);
+              }
               ix = row_mini(ix);
-              in = row_mini(in);
-              if (lr == 0) {
-                const int c = wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3);
-                float4 q = runp[c];
-                if (mx[e] > q.x) { q.x = mx[e]; q.y = __int_as_float(ix); }
-                if (mn[e] < q.z) { q.z = mn[e]; q.w = __int_as_float(in); }
-                runp[c] = q;
+              if (upd && (lr & 3) == r) {
+                float4 u = q;
+                if (sgl > 0.f) { u.x = vx[r]; u.y = __int_as_float(ix); }
+                else { u.z = -vx[r]; u.w = __int_as_float(ix); }
+                runp[cme] = u;
               }
             }
           }
@@ -463,47 +474,49 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
           }
         }
       }
-      float s1[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) s1[e] = 0.f;
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
+      const uint32_t *mrow = mbits + ((qs / nks) & 1) * 2048 + wn * 2;
+      uint2 mw[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bool ok = (rowok >> i) & 1u;
-        const int64_t grow = rb + wm * 128 + i * 16 + lr;
+      for (int i = 0; i < 8; ++i) mw[i] = *reinterpret_cast<const uint2 *>(mrow + (wm * 128 + i * 16 + lr) * 8);
+      float S1 = 0.f;
+      const bool full = valid == BM;   // uniform: only a scene's last tile is partial
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j) {
+        float s1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool ok = full || ((rowok >> i) & 1u);
+          const uint32_t word = (j < 2 ? mw[i].x : mw[i].y) >> ((j & 1) * 16 + 4 * lg);
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            v[r] = ((mb[i >> 1] >> ((i & 1) * 16 + j * 4 + r)) & 1u) ? acc[i][j][r] : 0.f;
-            s1[j * 4 + r] += ok ? v[r] : 0.f;
+            v[r] = ((word >> r) & 1u) ? acc[i][j][r] : 0.f;
+            s1[r] += ok ? v[r] : 0.f;
           }
           if (ok)
-            *reinterpret_cast<uint2 *>(Cg + grow * Ncols + n0 + wn * 64 + j * 16 + 4 * lg) =
+            *reinterpret_cast<uint2 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + n0 + wn * 64 + j * 16 + 4 * lg) =
                 make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
         }
-      }
 #pragma unroll
-      for (int e = 0; e < 16; ++e) s1[e] = row_sum(s1[e]);
-      if (lr == 0 && do_stats) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int c = wm * BN + wn * 64 + (e >> 2) * 16 + 4 * lg + (e & 3);
-          run[c].x += s1[e];
+        for (int r = 0; r < 4; ++r) {
+          s1[r] = row_sum(s1[r]);
+          if (lr == j * 4 + r) S1 = s1[r];
         }
       }
-      // stores count in vmcnt: retire them so the next tile's counted waits stay exact
-      wait_vm<0>();
+      if (do_stats) run[cme].x += S1;
+      // The stores count in vmcnt but are not waited for here: the next counted wait
+      // (vmcnt(10), phase 1) only relies on the LOADS completing in order among themselves
+      // (pending stores can only make it wait longer), so they drain behind phase 1's reads.
     }
 
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (i < 4) mb[i] = 0u;
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
   }
+
+  if (wm == 0) barrier_raw();   // re-align the halves (matching the stagger above)
 
   // ---- chunk end: merge the two wave halves and write this workgroup's partials
   if (wn == 0 && lane == 0) runn[wm] = run_n;
@@ -537,10 +550,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS))) return false;
   if (a.prologue != PCS_PRO_RAW || a.K % (2 * BK) != 0 || a.Ncols % BN != 0) return false;
-  // forward (statistics + max-pool epilogue): measured slower than the register-staged
-  // 256x256 kernel on the same RAW operand (tools/bench_glds.py), so only on request
-  if (a.epilogue == PCS_EPI_FWD)
-    return (a.flags & PCS_FLAG_GLDS_FWD) && a.C == nullptr && a.scene_bias == nullptr;
+  // forward: statistics / max-pool only (nothing stored); the pool keeps one extremum per
+  // column, chosen by sign(es), so a pool needs es
+  if (a.epilogue == PCS_EPI_FWD) return a.C == nullptr && a.scene_bias == nullptr && (!a.pool || a.es);
   if (a.epilogue == PCS_EPI_DGRAD)   // mask read from the operand itself, no S2, no addend
     return a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask &&
            (!a.pool_w || a.pool_c <= SPMAX);

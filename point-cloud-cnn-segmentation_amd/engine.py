@@ -317,8 +317,9 @@ class Engine:
         cps_g, rpc_g = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD)
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
         st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
+        # (es = bn_global's gamma: its sign tells the pool which extremum pcs_pool_finalize uses)
         self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, wc["global_feat"][0], None,
-                   stats=st, pool=pool, tag="fwd:global_feat")
+                   stats=st, pool=pool, es=P["bn_global.weight"], tag="fwd:global_feat")
         sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_g, rpc_g, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]

@@ -37,8 +37,6 @@ def _variant(L, v):
 def test_forward_stats_and_pool(variant, B, N, cps):
     import pcs_amd._lib as L
     dt, tdt, flags = _variant(L, variant)
-    if variant == "glds":
-        flags |= L.FLAG_GLDS_FWD        # the LDS-DMA forward is opt-in (see gemm_glds.hip)
     K = Nc = 512
     g = torch.Generator().manual_seed(B * 1000 + N)
     A = torch.relu(torch.randn(B * N, K, generator=g)).to(tdt).to(DEV)
@@ -47,9 +45,10 @@ def test_forward_stats_and_pool(variant, B, N, cps):
     nch = B * a.chunks_per_scene
     st = torch.empty(nch, Nc, 2, device=DEV)
     pool = torch.empty(nch, Nc, 4, device=DEV)
-    a.A, a.W, a.C, a.stats, a.pool = A.data_ptr(), W.data_ptr(), None, st.data_ptr(), pool.data_ptr()
-    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
     gamma = torch.randn(Nc, generator=g).to(DEV)       # signs pick max or min in the pool
+    a.A, a.W, a.C, a.stats, a.pool = A.data_ptr(), W.data_ptr(), None, st.data_ptr(), pool.data_ptr()
+    a.es = gamma.data_ptr()                            # EPI_FWD: only sign(es) matters (pool side)
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
     beta = torch.zeros(Nc, device=DEV)
     mean, rstd, scale, shift = (torch.empty(Nc, device=DEV) for _ in range(4))
     ssum = torch.empty(B, Nc, device=DEV)

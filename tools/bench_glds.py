@@ -38,6 +38,7 @@ def main():
         (torch.arange(B, device=dev, dtype=torch.int32) * N)[:, None]
     sp = torch.randn(B, K, device=dev)
     Wsp = torch.randn(K, Nc, device=dev) * 0.03
+    gsign = torch.randn(Nc, device=dev)
     flops = 2.0 * M * K * Nc
 
     def run(name, epi, flags=0, **kw):
@@ -61,9 +62,9 @@ def main():
         print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
 
     for fl, tag in ((0, "glds"), (L.FLAG_NO_GLDS, "big ")):
-        run(f"[{tag}] fwd, no epilogue work", L.EPI_FWD, fl)
-        run(f"[{tag}] fwd + stats", L.EPI_FWD, fl, stats=True)
-        run(f"[{tag}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True)
+        run(f"[{tag}] fwd, no epilogue work", L.EPI_FWD, fl, es=gsign)
+        run(f"[{tag}] fwd + stats", L.EPI_FWD, fl, stats=True, es=gsign)
+        run(f"[{tag}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True, es=gsign)
     run("[glds] dgrad: mask + store", L.EPI_DGRAD, 0, C=C, Yp=A)
     run("[glds] dgrad: mask + store + bias + S1", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True)
     run("[glds] dgrad: + sparse rows", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True, sparse=True)
