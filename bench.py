@@ -38,9 +38,9 @@ LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (
 
 # bench tag -> HIP kernel symbol (as summarised from rocprofv3 in profiles/pmc_<round>.json)
 TAG_KERNEL = {
-    "wgrad:global_feat": "wgrad_big_kernel<1, false>",          # Gram a5^T a5 (upper tiles)
-    "fwd:global_feat": "gemm_big_kernel<1, 0, false, false>",   # + BN stats + max-pool epilogue
-    "dgrad:global_feat": "gemm_big_kernel<3, 1, false, false>",  # + ReLU/BN5-backward epilogue
+    "wgrad:global_feat": "wgrad_big_kernel<1, false>",     # Gram a5^T a5 (upper tiles)
+    "fwd:global_feat": "gemm_glds_kernel<0>",              # LDS-DMA: BN stats + max-pool epilogue
+    "dgrad:global_feat": "gemm_glds_kernel<1>",            # LDS-DMA: folded a5 H, mask, sparse rows
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_r01.json")
 GRAM_TILE_FRACTION = 10.0 / 16.0   # upper 256-tiles of the symmetric 1024 x 1024 Gram
@@ -63,8 +63,12 @@ def kernel_model(tag, M, ab):
         return None
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
-    if kind == "wgrad" and conv == "global_feat":   # Gram of a5: upper tiles, reads y5 once
+    if kind == "wgrad" and conv == "global_feat":   # Gram of a5: upper tiles, reads a5 once
         return flops * GRAM_TILE_FRACTION, M * cin * ab
+    if conv == "global_feat" and kind == "fwd":     # reads a5; statistics + pool only, no store
+        return flops, M * cin * ab
+    if conv == "global_feat" and kind == "dgrad":   # a5 (also the ReLU mask) in, dz5 out
+        return flops, M * (cin + cout) * ab
     if conv == "conv5" and kind in ("dgrad", "wgrad"):   # folded form: dz5 + y4/128-wide out
         return flops, M * (cout + cin) * ab
     if kind == "fwd":
