@@ -387,6 +387,18 @@ int pcs_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
              const float *grad_scale, float lr, float beta1, float beta2, float eps,
              float weight_decay, int64_t step, pcs_stream_t stream);
 
+/*
+ * Device-side collate (replaces collate_fn's host padding, P:44-63).
+ * CSR input: scene b owns rows offsets[b] .. offsets[b+1] (int64 [num_scenes+1], device) of
+ * points (fp32 [T, 4], 16-byte aligned) and labels (int32 or int64 [T], label_bytes 4 / 8).
+ * Outputs [num_scenes, scene_rows] (each may be NULL): points_out fp32 [.., 4] with (0,0,0,0)
+ * pads, labels_out int64 with -1 pads, mask_out bool (uint8) 1 on real points.  The caller
+ * guarantees every scene length <= scene_rows (the batch max, like collate_fn).
+ */
+int pcs_pad_scatter(const float *points, const void *labels, int32_t label_bytes,
+                    const int64_t *offsets, int64_t num_scenes, int64_t scene_rows,
+                    float *points_out, int64_t *labels_out, uint8_t *mask_out, pcs_stream_t stream);
+
 /* Build-time identification and error string. */
 int pcs_abi_version(void);
 const char *pcs_last_error(void);

@@ -21,6 +21,12 @@ _LAZY = {
     "load_checkpoint": ("checkpoint", "load_checkpoint"),
     "predict": ("checkpoint", "predict"),
     "ConfusionMeter": ("metrics", "ConfusionMeter"),
+    "RaggedBatch": ("data", "RaggedBatch"),
+    "ragged_collate": ("data", "ragged_collate"),
+    "CSRPointCloudDataset": ("data", "CSRPointCloudDataset"),
+    "PointCloudDataset": ("data", "PointCloudDataset"),
+    "pad_on_device": ("loader", "pad_on_device"),
+    "DevicePrefetcher": ("loader", "DevicePrefetcher"),
 }
 
 
@@ -29,7 +35,7 @@ def __getattr__(name):
         import importlib
         mod, attr = _LAZY[name]
         return getattr(importlib.import_module(f"{__name__}.{mod}"), attr)
-    if name in ("data", "model", "optim", "train", "engine", "metrics", "checkpoint"):
+    if name in ("data", "model", "optim", "train", "engine", "metrics", "checkpoint", "loader"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
     raise AttributeError(name)

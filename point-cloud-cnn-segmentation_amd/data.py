@@ -11,10 +11,19 @@ Pure numpy/torch host code (no HIP).  Mirrors the reference's data contract:
   a random sphere and a random line "track".
 * ``shard_batch`` — the ``tensor.chunk`` rule nn.DataParallel uses to split a padded
   batch over ranks (torch/nn/parallel/scatter_gather.py).
+* ``PointCloudDataset`` — P:20-42, the HDF5 vlen event reader (needs h5py, absent in this
+  image: it raises ImportError with a pointer to the CSR store instead).
+* ``CSRPointCloudDataset`` / ``write_csr_store`` — the same per-event contract over a
+  memory-mapped CSR store (flat points f32 [T,4], labels [T], offsets [E+1] as .npy files),
+  the vlen layout of the reference's HDF5 files without the h5py dependency.
+* ``RaggedBatch`` / ``ragged_collate`` — CSR batching for the DataLoader: no host padding;
+  ``pcs_amd.loader`` pads on the device (pcs_pad_scatter) after a pinned async copy.
 """
 from __future__ import annotations
 
+import os
 from collections import Counter
+from typing import NamedTuple
 
 import numpy as np
 
@@ -127,3 +136,133 @@ def shard_batch(tensors, rank, world_size):
     """Slice each [B,...] tensor to this rank's scenes (DataParallel's scatter rule)."""
     lo, hi = shard_bounds(tensors[0].shape[0], rank, world_size)
     return tuple(t[lo:hi] for t in tensors)
+
+
+# ----------------------------------------------------------------------------- event stores
+class PointCloudDataset:
+    """The reference's HDF5 event reader (P:20-42): ``data`` holds one flat float32 vlen
+    array (x,y,z,e per point) per event, ``labels`` one int array per event.  Returns
+    (points f32 [N,4], labels i64 [N]) torch tensors like P:31-36."""
+
+    def __init__(self, data_path, label_path):
+        try:
+            import h5py
+        except ImportError as e:   # h5py is not part of this image
+            raise ImportError(
+                "PointCloudDataset needs h5py to read the reference's HDF5 files; convert them "
+                "with convert_hdf5_to_csr() on a machine that has it, then use "
+                "CSRPointCloudDataset") from e
+        self.data_file = h5py.File(data_path, "r")
+        self.label_file = h5py.File(label_path, "r")
+        self.num_events = len(self.data_file["data"])
+
+    def __len__(self):
+        return self.num_events
+
+    def __getitem__(self, idx):
+        import torch
+        points = torch.tensor(np.asarray(self.data_file["data"][idx]).reshape(-1, 4), dtype=torch.float32)
+        labels = torch.tensor(np.asarray(self.label_file["labels"][idx]), dtype=torch.long)
+        return points, labels
+
+    def __del__(self):
+        for f in ("data_file", "label_file"):
+            if hasattr(self, f):
+                getattr(self, f).close()
+
+
+CSR_FILES = ("points.npy", "labels.npy", "offsets.npy")
+
+
+def write_csr_store(path, clouds, label_dtype=np.int32):
+    """Write [(points[N_i,4], labels[N_i])] as a CSR store directory (three .npy files)."""
+    os.makedirs(path, exist_ok=True)
+    lens = np.array([len(p) for p, _ in clouds], np.int64)
+    offsets = np.zeros(len(clouds) + 1, np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    pts = np.concatenate([np.asarray(p, np.float32).reshape(-1, 4) for p, _ in clouds]) if clouds \
+        else np.zeros((0, 4), np.float32)
+    lab = np.concatenate([np.asarray(l).reshape(-1) for _, l in clouds]).astype(label_dtype) if clouds \
+        else np.zeros(0, label_dtype)
+    for name, arr in zip(CSR_FILES, (pts, lab, offsets)):
+        np.save(os.path.join(path, name), arr)
+    return path
+
+
+def convert_hdf5_to_csr(data_path, label_path, out_dir, label_dtype=np.int32):
+    """Stream the reference's HDF5 vlen files (P:20-36) into a CSR store (needs h5py)."""
+    ds = PointCloudDataset(data_path, label_path)
+    clouds = [(p.numpy(), l.numpy()) for p, l in (ds[i] for i in range(len(ds)))]
+    return write_csr_store(out_dir, clouds, label_dtype)
+
+
+class CSRPointCloudDataset:
+    """Per-event (points f32 [N,4], labels i64 [N]) over a memory-mapped CSR store: the
+    __getitem__ contract of PointCloudDataset (P:30-36) without h5py.  ``__getitem__``
+    returns torch tensors; ``cloud(idx)`` returns the numpy views (no copy)."""
+
+    def __init__(self, path):
+        self.points, self.labels, self.offsets = (
+            np.load(os.path.join(path, n), mmap_mode="r") for n in CSR_FILES)
+        if self.points.ndim != 2 or self.points.shape[1] != 4 or self.offsets[-1] != len(self.points) \
+                or len(self.labels) != len(self.points) or np.any(np.diff(self.offsets) < 0):
+            raise ValueError(f"{path}: inconsistent CSR store")
+        self.num_events = len(self.offsets) - 1
+
+    def __len__(self):
+        return self.num_events
+
+    def cloud(self, idx):
+        lo, hi = int(self.offsets[idx]), int(self.offsets[idx + 1])
+        return self.points[lo:hi], self.labels[lo:hi]
+
+    def __getitem__(self, idx):
+        import torch
+        p, l = self.cloud(idx)
+        return torch.from_numpy(np.array(p, np.float32)), torch.from_numpy(np.array(l, np.int64))
+
+
+# ----------------------------------------------------------------------------- CSR batching
+class RaggedBatch(NamedTuple):
+    """A batch in CSR form: scene b owns rows offsets[b]:offsets[b+1] of points / labels.
+    A NamedTuple of tensors, so DataLoader(pin_memory=True) pins every field."""
+    points: "torch.Tensor"    # f32 [T, 4]
+    labels: "torch.Tensor"    # i32 or i64 [T]
+    offsets: "torch.Tensor"   # i64 [B + 1]
+
+    @property
+    def num_scenes(self):
+        return self.offsets.numel() - 1
+
+    @property
+    def max_points(self):
+        """The padded length collate_fn would use (P:50)."""
+        if self.num_scenes == 0:
+            return 0
+        return int((self.offsets[1:] - self.offsets[:-1]).max())
+
+
+def ragged_collate(batch, label_dtype=None):
+    """DataLoader collate building a RaggedBatch (no padding) from (points, labels) pairs;
+    the padded view collate_fn (P:44-63) returns is produced on the device by
+    pcs_amd.loader.pad_on_device."""
+    import torch
+    points_list, labels_list = zip(*batch)
+    lens = torch.tensor([p.shape[0] for p in points_list], dtype=torch.int64)
+    offsets = torch.zeros(len(points_list) + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=offsets[1:])
+    pts = torch.cat([p.reshape(-1, 4).float() for p in points_list])
+    lab = torch.cat([l.reshape(-1) for l in labels_list])
+    if label_dtype is not None:
+        lab = lab.to(label_dtype)
+    return RaggedBatch(pts.contiguous(), lab.contiguous(), offsets)
+
+
+def occupied_clouds(seed, num_scenes, grid=256, occupancy=0.02, jitter=0.1, num_classes=2):
+    """Occupied-only sparse clouds of SURVEY §8(d) cfg3: each scene keeps a ragged
+    ~``occupancy`` fraction of the grid^3 lattice voxels (count drawn per scene within
+    +-``jitter``), xyz = voxel centres, e ~ Exp(1), labels as synthetic_clouds."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    base = occupancy * grid ** 3
+    n = [int(base * rng.uniform(1 - jitter, 1 + jitter)) for _ in range(num_scenes)]
+    return [_scene(rng, grid, k, num_classes, dense=False) for k in n]
