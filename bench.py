@@ -153,6 +153,11 @@ def main():
     ap.add_argument("--classes", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],
+                    help="cfg2: dense G^3 grid (the bench line); cfg3: occupied-only ragged "
+                         "clouds on a 256^3 lattice (~2%% occupancy), CSR batch resident in HBM, "
+                         "padded on the device inside every timed step")
+    ap.add_argument("--occupancy", type=float, default=0.02)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,12 +169,34 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     B, G, C = args.scenes, args.grid, args.classes
-    N = G ** 3
-    pts, lab, _ = synthetic_batch(1234 + rank, [N] * B, C, grid=G, dense=True)
-    w = class_weights([lab[b] for b in range(B)], num_classes=C)
-    x = torch.from_numpy(pts).to(dev)
-    y = torch.from_numpy(lab).to(dev)
-    del pts, lab
+    rb = None
+    if args.workload == "cfg3":
+        # occupied-only ragged scenes: CSR in HBM, device-side collate
+        # (pcs_pad_scatter) to the DP-global max length inside the step, like collate_fn + H2D
+        from pcs_amd.data import occupied_clouds, ragged_collate
+        from pcs_amd.loader import global_max_points, pad_on_device
+        G = 256 if args.grid == 128 else args.grid
+        clouds = occupied_clouds(1234 + rank, B, grid=G, occupancy=args.occupancy, num_classes=C)
+        w = class_weights([l for _, l in clouds], num_classes=C)
+        rb = ragged_collate([(torch.from_numpy(p), torch.from_numpy(l)) for p, l in clouds], torch.int32)
+        N = global_max_points(rb.max_points, None, dev)
+        real_points = int(rb.offsets[-1])
+        rb = type(rb)(*(t.to(dev) for t in rb))
+        del clouds
+    else:
+        N = G ** 3
+        pts, lab, _ = synthetic_batch(1234 + rank, [N] * B, C, grid=G, dense=True)
+        w = class_weights([lab[b] for b in range(B)], num_classes=C)
+        x = torch.from_numpy(pts).to(dev)
+        y = torch.from_numpy(lab).to(dev)
+        real_points = B * N
+        del pts, lab
+
+    def run_step():
+        if rb is not None:
+            xs, ys, _ = pad_on_device(rb, dev, scene_rows=N)
+            return step(xs, ys)
+        return step(x, y)
 
     torch.manual_seed(0)
     model = PointNetSegmentation(C, compute_dtype=args.dtype).to(dev)
@@ -180,7 +207,7 @@ def main():
     step = FusedTrainStep(model, opt, class_weight=w)
 
     for i in range(args.warmup):
-        loss = step(x, y)
+        loss = run_step()
     torch.cuda.synchronize()
     timing = {} if not args.no_kernel_timing else None
     step.timing = timing
@@ -189,7 +216,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = step(x, y)
+        loss = run_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -202,7 +229,11 @@ def main():
     loss_v = float(loss.item())
 
     M = B * N
-    total_points = world * M * args.steps
+    if world > 1:
+        t = torch.tensor([real_points], device=dev, dtype=torch.int64)
+        dist.all_reduce(t)
+        real_points = int(t.item())
+    total_points = real_points * args.steps
     ab = 2 if args.dtype == "bf16" else 4
     roof = None
     kernels = {}
@@ -257,10 +288,17 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.dtype, "data": "synthetic (dense voxel-centre clouds, seeded)",
-            "config": {"workload": f"PointNetSegmentation train step, {B} scenes x {G}^3 points "
-                                   f"per GPU, C={C}", "global_batch": B * world,
-                       "points_per_scene": N, "parallelism": f"dp{world}"},
+            "dtype": args.dtype,
+            "data": ("synthetic (dense voxel-centre clouds, seeded)" if rb is None else
+                     "synthetic (occupied-only voxel-centre clouds, ragged, seeded)"),
+            "config": ({"workload": f"PointNetSegmentation train step, {B} scenes x {G}^3 points "
+                                    f"per GPU, C={C}", "global_batch": B * world,
+                        "points_per_scene": N, "parallelism": f"dp{world}"} if rb is None else
+                       {"workload": f"cfg3: PointNetSegmentation train step, {B} occupied-only "
+                                    f"ragged scenes per GPU on a {G}^3 lattice ({args.occupancy:g} "
+                                    f"occupancy), device-side collate in the step, C={C}",
+                        "global_batch": B * world, "padded_points_per_scene": N,
+                        "real_points_per_step": real_points, "parallelism": f"dp{world}"}),
             "loss": round(loss_v, 6),
             "roofline": roof,
             "step_roofline": step_roofline(M, C, ab, el / args.steps * 1e3),
