@@ -59,10 +59,12 @@ def pmc_traffic(tag, dtype):
 def kernel_model(tag, M, ab):
     """Algorithmic FLOPs and HBM bytes of one launch (SURVEY.md §8(d) accounting)."""
     kind, conv = tag.split(":", 1)
-    if conv not in LAYER_DIMS or kind not in ("fwd", "dgrad", "wgrad"):
+    if conv not in LAYER_DIMS or kind not in ("fwd", "dgrad", "wgrad", "dgrad+wgrad"):
         return None
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
+    if kind == "dgrad+wgrad":   # fused (seg_conv1 local half): dZ, Y in once, x in, dX out
+        return 2 * flops, M * (2 * cout + 2 * cin) * ab
     if kind == "wgrad" and conv == "global_feat":   # Gram of a5: upper tiles, reads a5 once
         return flops * GRAM_TILE_FRACTION, M * cin * ab
     if conv == "global_feat" and kind == "fwd":     # reads a5; statistics + pool only, no store

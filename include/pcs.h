@@ -148,6 +148,16 @@ int pcs_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream);
 int pcs_conv1_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream); /* X = points f32 */
 
 /*
+ * Fused input + weight gradient of seg_conv1's local half (bf16; Cout 512, Cin 64):
+ * dy = alpha*dZ + beta + gamma*Y (dy_mode PCS_PRO_BWD), x = relu(X*s + t) (x_mode
+ * PCS_PRO_BNRELU, no x_mask);  dX[M, 64] = dy . Wt^T (Wt = W^T, [64, 512] bf16, no epilogue)
+ * and dW += dy^T x as pcs_wgrad (fp32 partials summed in a fixed order into dW, row stride
+ * ldw).  Replaces the pcs_gemm(PRO_BWD, EPI_RAW) + pcs_wgrad pair, reading dy's inputs once.
+ */
+int64_t pcs_dgrad_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_per_scene */
+int pcs_dgrad_wgrad(const pcs_wgrad_args *args, const void *Wt, void *dX, pcs_stream_t stream);
+
+/*
  * Streaming column statistics of a stored activation Y [M, C] (C/8 (bf16) or C/4 (fp32)
  * must divide 256): per-chunk (mean, M2) BN partials and optional max-pool partials, in
  * pcs_gemm's epilogue formats.  One HBM pass; used for the 1024-wide global_feat output.

@@ -123,6 +123,8 @@ SIGNATURES = [
     ("pcs_bn_stats_from_gram", ct.c_int, [_vp, _vp, _i64, _vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp]),
     ("pcs_confusion", ct.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcs_argmax", ct.c_int, [_vp, _i64, _i64, _i32, _vp, _vp]),
+    ("pcs_dgrad_wgrad_workspace", _i64, [ct.POINTER(WgradArgs)]),
+    ("pcs_dgrad_wgrad", ct.c_int, [ct.POINTER(WgradArgs), _vp, _vp, _vp]),
     ("pcs_pad_scatter", ct.c_int, [_vp, _vp, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     ("pcs_last_error", ct.c_char_p, []),
 ]

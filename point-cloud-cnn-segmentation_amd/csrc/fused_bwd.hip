@@ -1,0 +1,257 @@
+// Fused input + weight gradient of seg_conv1's local half (autograd of P:117-123 at P:254):
+//
+//   dy      = alpha * dZ + beta + gamma * Y          (bn_seg1 backward, [M, 512])
+//   dA2     = dy . W_l                               ([M, 64], W_l = seg_conv1.weight[:, :64])
+//   dW_l   += dy^T . relu(bn2(Y2))                   ([512, 64])
+//
+// Both gradients read the same dy, which is formed from the two widest tensors of the head
+// (dZ and Y of bn_seg1, 2 KB per point in bf16).  Separately (pcs_gemm + pcs_wgrad) they
+// read them twice; here each row slab is staged into LDS once and feeds both contractions,
+// so the pair moves 2.3 KB per point instead of 4.5 KB.  MFMA work is small (14 % of the
+// CU's MFMA time at the HBM rate), so the kernel is HBM-bound by design.
+//
+// One 512-thread workgroup per CU (W_l^T stays resident in LDS for the workgroup's life),
+// scene-aligned row slices as pcs_wgrad, 64-row steps:
+//   compute(step s) from LDS -> dA2 tile of step s to LDS -> barrier -> store it, write the
+//   registers (step s+1) into LDS, issue the loads of step s+2 -> barrier.
+// dgrad: wave w owns rows 16*(w>>1).. and columns 32*(w&1).. (2 accumulators, K = 512);
+// wgrad: wave w owns output channels 64*w.. x all 64 inputs (16 accumulators, K = 64 rows).
+// The dy tile is a [m][col] image (rows permuted as pcs_wgrad's bf16 tiles, 32-B padding)
+// read with ds_read_b128 for the dgrad operand and ds_read_b64_tr_b16 for the wgrad one.
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 512;
+constexpr int COUT = 512, CIN = 64, MS = 64;
+constexpr int WT_ROWB = COUT * 2;                  // W_l^T [CIN][COUT], XOR-swizzled 16-B slots
+constexpr int DY_ROWB = COUT * 2 + 32;             // dy [MS][COUT] (+32 B pad)
+constexpr int X_ROWB = CIN * 2 + 32;               // x  [MS][CIN]
+constexpr int OFF_DY = CIN * WT_ROWB;              // 64 KB
+constexpr int OFF_X = OFF_DY + MS * DY_ROWB;
+constexpr int OFF_OUT = OFF_X + MS * X_ROWB;       // dA2 tile [MS][CIN] bf16
+constexpr int OFF_COEF = OFF_OUT + MS * CIN * 2;  // alpha | beta | gamma [COUT], s | t [CIN]
+constexpr int LDS_BYTES = OFF_COEF + (3 * COUT + 2 * CIN) * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+constexpr int DY_CPR = COUT / 8, DY_RP = THREADS / DY_CPR, DY_NCH = MS / DY_RP;   // 64, 8, 8
+constexpr int X_CPR = CIN / 8, X_RP = THREADS / X_CPR;                            // 8, 64
+static_assert(X_RP == MS, "one x chunk per thread");
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+PCS_DEV int wt_off(int c, int slot) { return c * WT_ROWB + ((slot ^ (c & 7)) << 4); }
+
+PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4 *>(p);
+  const float4 b = *reinterpret_cast<const float4 *>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+PCS_DEV int xcd_remap(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+PCS_DEV bf16x8 tr_read(const char *base, int r0, int r1, int rowb, int col) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(base + r0 * rowb + col * 2));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(base + r1 * rowb + col * 2));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args a, const bf16_t *__restrict__ Wt,
+                                                                 bf16_t *__restrict__ dX, int64_t rows_per_split) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int sps = a.splits_per_scene;
+  const int scene = L / sps, sis = L % sps;
+  const int64_t N = a.scene_rows;
+  const int64_t lo = (int64_t)sis * rows_per_split;
+  const int64_t hi = pcs_min64(lo + rows_per_split, N);
+  const int64_t sbase = (int64_t)scene * N;
+
+  const bf16_t *__restrict__ dZ = reinterpret_cast<const bf16_t *>(a.dZ);
+  const bf16_t *__restrict__ Yg = reinterpret_cast<const bf16_t *>(a.Y);
+  const bf16_t *__restrict__ Xg = reinterpret_cast<const bf16_t *>(a.X);
+
+  // W_l^T [CIN][COUT] -> LDS once (64 KB: 8 chunks per thread)
+  for (int i = tid; i < CIN * COUT / 8; i += THREADS) {
+    const int c = i / (COUT / 8), slot = i % (COUT / 8);
+    *reinterpret_cast<u32x4 *>(lds + wt_off(c, slot)) =
+        *reinterpret_cast<const u32x4 *>(Wt + (int64_t)c * COUT + slot * 8);
+  }
+
+  // per-channel prologue coefficients -> LDS (read back at each store: fewer live registers)
+  float *cf = reinterpret_cast<float *>(lds + OFF_COEF);
+  for (int i = tid; i < COUT; i += THREADS) {
+    cf[i] = a.alpha[i]; cf[COUT + i] = a.beta[i]; cf[2 * COUT + i] = a.gamma[i];
+  }
+  if (tid < CIN) { cf[3 * COUT + tid] = a.s[tid]; cf[3 * COUT + CIN + tid] = a.t[tid]; }
+  __syncthreads();
+
+  // staging ownership: dy column chunk dc (8 channels), rows dr0 + 8 i; x chunk xc, row xr
+  const int dc = tid % DY_CPR, dr0 = tid / DY_CPR;
+  const int xc = tid % X_CPR, xr = tid / X_CPR;
+
+  u32x4 rz[DY_NCH], ry[DY_NCH], rx;
+  auto load_step = [&](int64_t m0) {   // rows clamped to the slice (zeroed at store time)
+#pragma unroll
+    for (int i = 0; i < DY_NCH; ++i) {
+      const int64_t r = pcs_min64(m0 + dr0 + DY_RP * i, hi - 1);
+      const int64_t off = (sbase + r) * COUT + dc * 8;
+      rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
+      ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
+    }
+    const int64_t r = pcs_min64(m0 + xr, hi - 1);
+    rx = *reinterpret_cast<const u32x4 *>(Xg + (sbase + r) * CIN + xc * 8);
+  };
+  auto store_step = [&](int64_t m0) {
+    float ca[8], cb[8], cg[8];
+    lds_vec8(cf + dc * 8, ca); lds_vec8(cf + COUT + dc * 8, cb); lds_vec8(cf + 2 * COUT + dc * 8, cg);
+#pragma unroll
+    for (int i = 0; i < DY_NCH; ++i) {
+      const int rl = dr0 + DY_RP * i;
+      float v[8], y[8];
+      unpack_chunk(rz[i], v);
+      unpack_chunk(ry[i], y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+      u32x4 out = pack_chunk(v);
+      if (m0 + rl >= hi) out = mk_u32x4(0, 0, 0, 0);
+      *reinterpret_cast<u32x4 *>(lds + OFF_DY + prow(rl) * DY_ROWB + dc * 16) = out;
+    }
+    float v[8], xs[8], xt[8];
+    lds_vec8(cf + 3 * COUT + xc * 8, xs); lds_vec8(cf + 3 * COUT + CIN + xc * 8, xt);
+    unpack_chunk(rx, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+    u32x4 out = pack_chunk(v);
+    if (m0 + xr >= hi) out = mk_u32x4(0, 0, 0, 0);
+    *reinterpret_cast<u32x4 *>(lds + OFF_X + prow(xr) * X_ROWB + xc * 16) = out;
+  };
+
+  f32x4 accw[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (int)((hi - lo + MS - 1) / MS);
+  if (nsteps > 0) {
+    load_step(lo);
+    store_step(lo);
+    __builtin_amdgcn_sched_barrier(0);
+    load_step(lo + MS);   // clamped: harmless when nsteps == 1
+  }
+  __syncthreads();   // W_l^T, step 0 visible
+
+  const int g = lane >> 4, l16 = lane & 15;
+  const int mb = wid >> 1, cb0 = 2 * (wid & 1);   // dgrad rows 16*mb.., column blocks cb0, cb0+1
+  const char *tDY = lds + OFF_DY, *tX = lds + OFF_X;
+  for (int st = 0; st < nsteps; ++st) {
+    const int64_t m0 = lo + (int64_t)st * MS;
+    // dgrad: out^T[c][m] = sum_k Wt[c][k] dy[m][k]
+    f32x4 accd[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int mrow = prow(mb * 16 + l16);
+#pragma unroll 4
+    for (int kk = 0; kk < COUT / 32; ++kk) {
+      const int slot = 4 * kk + g;
+      const bf16x8 yf = *reinterpret_cast<const bf16x8 *>(tDY + mrow * DY_ROWB + slot * 16);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(lds + wt_off((cb0 + j) * 16 + l16, slot));
+        accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf, accd[j], 0, 0, 0);
+      }
+    }
+    // wgrad: dW[o][c] += sum_m dy[m][o] x[m][c]; lane group g holds m = 8g..8g+7 of 32
+#pragma unroll
+    for (int kk = 0; kk < MS / 32; ++kk) {
+      const int q = (lane >> 2) & 3, p = lane & 3;
+      const int r0 = prow(32 * kk + 8 * g + q), r1 = prow(32 * kk + 8 * g + 4 + q);
+      bf16x8 xf[4], yf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[j] = tr_read(tX, r0, r1, X_ROWB, j * 16 + 4 * p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) yf[i] = tr_read(tDY, r0, r1, DY_ROWB, wid * 64 + i * 16 + 4 * p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          accw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], yf[i], accw[i][j], 0, 0, 0);
+    }
+    // dA2 tile -> LDS: lane holds out[m = 16 mb + l16][c = 16 cb + 4 g + r]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = (cb0 + j) * 16 + 4 * g;
+      *reinterpret_cast<uint2 *>(lds + OFF_OUT + (mb * 16 + l16) * CIN * 2 + c * 2) =
+          make_uint2(pack2bf(accd[j][0], accd[j][1]), pack2bf(accd[j][2], accd[j][3]));
+    }
+    lds_barrier();   // step st consumed; its dA2 tile complete
+    {
+      const int r = tid >> 3, ch = tid & 7;   // 64 rows x 8 chunks of 16 B
+      if (m0 + r < hi)
+        *reinterpret_cast<u32x4 *>(dX + (sbase + m0 + r) * CIN + ch * 8) =
+            *reinterpret_cast<const u32x4 *>(lds + OFF_OUT + r * CIN * 2 + ch * 16);
+    }
+    if (st + 1 < nsteps) {
+      store_step(m0 + MS);
+      __builtin_amdgcn_sched_barrier(0);
+      load_step(m0 + 2 * MS);   // clamped past the end: never consumed
+    }
+    lds_barrier();
+  }
+
+  // this slice's dW partial: lane holds dW[o = 64 w + 16 i + l16][c = 16 j + 4 g ..]
+  float *out = a.partial + (int64_t)L * COUT * CIN;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int o = wid * 64 + i * 16 + l16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<float4 *>(out + o * CIN + j * 16 + 4 * g) =
+          make_float4(accw[i][j][0], accw[i][j][1], accw[i][j][2], accw[i][j][3]);
+  }
+}
+
+int64_t splits_of(const pcs_wgrad_args &a) {
+  int64_t sps = (256 + a.num_scenes - 1) / a.num_scenes;   // one workgroup per CU
+  const int64_t max_sps = (a.scene_rows + 4 * MS - 1) / (4 * MS);
+  if (sps > max_sps) sps = max_sps;
+  return sps < 1 ? 1 : sps;
+}
+
+bool shapes_ok(const pcs_wgrad_args &a) {
+  return a.dtype == PCS_BF16 && a.Cout == COUT && a.Cin == CIN && a.dy_mode == PCS_PRO_BWD &&
+         a.x_mode == PCS_PRO_BNRELU && !a.x_mask && !(a.flags & PCS_FLAG_GENERIC);
+}
+
+}  // namespace
+
+extern "C" int64_t pcs_dgrad_wgrad_workspace(pcs_wgrad_args *a) {
+  if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_dgrad_wgrad_workspace", "bad geometry");
+  if (!shapes_ok(*a))
+    return pcs_set_einval("pcs_dgrad_wgrad_workspace",
+                          "bf16, Cout=512, Cin=64, dy_mode PRO_BWD, x_mode PRO_BNRELU, no x_mask only");
+  a->splits_per_scene = (int32_t)splits_of(*a);
+  return (int64_t)a->num_scenes * a->splits_per_scene * COUT * CIN * 4;
+}
+
+extern "C" int pcs_dgrad_wgrad(const pcs_wgrad_args *ap, const void *Wt, void *dX, pcs_stream_t stream) {
+  if (!ap || !Wt || !dX) return pcs_set_einval("pcs_dgrad_wgrad", "null argument");
+  pcs_wgrad_args a = *ap;
+  if (pcs_dgrad_wgrad_workspace(&a) < 0) return PCS_EINVAL;
+  if (!a.dZ || !a.Y || !a.alpha || !a.beta || !a.gamma || !a.X || !a.s || !a.t || !a.partial || !a.dW)
+    return pcs_set_einval("pcs_dgrad_wgrad", "missing operand");
+  if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31) return pcs_set_einval("pcs_dgrad_wgrad", "M must be < 2^31");
+  const int64_t rps = ((a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene + MS - 1) / MS * MS;
+  const int nb = (int)(a.num_scenes * a.splits_per_scene);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(dgrad_wgrad_s1_kernel, dim3(nb), dim3(THREADS), 0, s, a, static_cast<const bf16_t *>(Wt),
+                     static_cast<bf16_t *>(dX), rps);
+  PCS_CHECK_LAUNCH();
+  return pcs_reduce_partials(a.partial, nb, (int64_t)COUT * CIN, 1.0f, a.dW, a.ldw ? a.ldw : CIN, CIN, stream);
+}

@@ -498,9 +498,27 @@ class Engine:
 
         # seg_conv1 local half: dA2 contribution (raw) and dW[:, :64]
         dA2 = torch.empty(M, 64, dtype=self.tdt, device=dev)
-        self._gemm(B, N, 512, 64, L.PRO_BWD, L.EPI_RAW, dz_s1, wc["seg_conv1"][1], dA2,
-                   A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
-        wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
+        if self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC):
+            # one pass over dy's inputs for both gradients (csrc/fused_bwd.hip)
+            p2 = sv.bn["bn2"]
+            fa = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=512, Cin=64, dtype=self.dt,
+                             splits_per_scene=0, dy_mode=L.PRO_BWD, x_mode=L.PRO_BNRELU,
+                             x_keep_scale=1.0, dW=L.ptr(G("seg_conv1.weight")), ldw=Ws1.shape[1],
+                             flags=self.flags, dZ=L.ptr(dz_s1), Y=L.ptr(ys["seg_conv1"]), alpha=L.ptr(a1),
+                             beta=L.ptr(b1), gamma=L.ptr(g1), X=L.ptr(ys["conv2"]), s=L.ptr(p2.scale),
+                             t=L.ptr(p2.shift))
+            nbytes = L.load().pcs_dgrad_wgrad_workspace(ct.byref(fa))
+            if nbytes < 0:
+                raise L.PcsError(L.load().pcs_last_error().decode())
+            ws1 = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            fa.partial = ws1.data_ptr()
+            self._launch("dgrad+wgrad:seg_conv1", "pcs_dgrad_wgrad", ct.byref(fa), L.ptr(wc["seg_conv1"][1]),
+                         L.ptr(dA2), s)
+            keepalive.append(ws1)
+        else:
+            self._gemm(B, N, 512, 64, L.PRO_BWD, L.EPI_RAW, dz_s1, wc["seg_conv1"][1], dA2,
+                       A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
+            wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
 
         # global_feat input gradient in folded form (P:113 at P:254): with dy_g = beta_g +
         # gamma_g * y_g + (max-pool rows) and y_g = a5 Wg^T,

@@ -63,3 +63,14 @@ def test_geometry_is_scene_aligned():
         assert rpc % 128 == 0 and rpc > 0
         cps = a.chunks_per_scene
         assert (cps - 1) * rpc < N <= cps * rpc      # no empty chunk, full coverage
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
+def test_fused_dgrad_wgrad_validates_shapes_without_gpu():
+    import pcs_amd._lib as L
+    lib = L.load()
+    a = L.WgradArgs(num_scenes=1, scene_rows=128, Cout=256, Cin=64, dtype=L.BF16, dy_mode=L.PRO_BWD,
+                    x_mode=L.PRO_BNRELU)
+    assert lib.pcs_dgrad_wgrad_workspace(ct.byref(a)) < 0
+    a.Cout = 512
+    assert lib.pcs_dgrad_wgrad_workspace(ct.byref(a)) == a.splits_per_scene * 512 * 64 * 4
