@@ -63,8 +63,9 @@ def kernel_model(tag, M, ab):
         return None
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
-    if kind == "dgrad+wgrad":   # fused (seg_conv1 local half): dZ, Y in once, x in, dX out
-        return 2 * flops, M * (2 * cout + 2 * cin) * ab
+    if kind == "dgrad+wgrad":   # fused: dZ, Y in once, Y_{l-1} (+ addend) in, dZ_{l-1} out
+        extra = cin if conv == "conv3" else 0
+        return 2 * flops, M * (2 * cout + 2 * cin + extra) * ab
     if kind == "wgrad" and conv == "global_feat":   # Gram of a5: upper tiles, reads a5 once
         return flops * GRAM_TILE_FRACTION, M * cin * ab
     if conv == "global_feat" and kind == "fwd":     # reads a5; statistics + pool only, no store
@@ -106,6 +107,8 @@ def northstar_64(kernels, M, ab):
     """HBM-only fraction of the 64->64 conv fwd+bwd (conv2: fwd, dgrad, wgrad)
     against t_HBM = 6 x 64 ch x M x bytes / 8 TB/s."""
     tags = ("fwd:conv2", "dgrad:conv2", "wgrad:conv2")
+    if "dgrad+wgrad:conv2" in kernels:   # fused backward (csrc/fused_bwd.hip)
+        tags = ("fwd:conv2", "dgrad+wgrad:conv2")
     if not all(t in kernels for t in tags):
         return None
     ms = sum(kernels[t][0] / kernels[t][1] for t in tags)

@@ -158,6 +158,19 @@ int64_t pcs_dgrad_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_
 int pcs_dgrad_wgrad(const pcs_wgrad_args *args, const void *Wt, void *dX, pcs_stream_t stream);
 
 /*
+ * Fused input + weight gradient of a layer whose input gradient ends in the previous
+ * layer's ReLU / dropout / BN-statistics epilogue (bf16; (Cout, Cin) = (K, Ncols) in
+ * {64x64, 128x64}: conv2, conv3, conv4).  Takes the pcs_gemm arguments
+ * of the PRO_BWD / EPI_DGRAD call (A = dZ, A2 = Y, pa/pb/pc, W = W^T [Cin, Cout], C, Yp,
+ * es, et, emean, erstd, stats, c_mask | addend) and also writes dW = dy^T relu(es*Yp + et)
+ * (* c_mask * c_keep_scale) into dW (row stride ldw, 0 = Cin) through the fp32 workspace.
+ * chunks_per_scene (and so the stats rows) must come from the _workspace call.
+ */
+int64_t pcs_dgrad_wgrad_bn_workspace(pcs_gemm_args *args); /* bytes; fills chunks_per_scene */
+int pcs_dgrad_wgrad_bn(const pcs_gemm_args *args, float *workspace, float *dW, int64_t ldw,
+                       pcs_stream_t stream);
+
+/*
  * Streaming column statistics of a stored activation Y [M, C] (C/8 (bf16) or C/4 (fp32)
  * must divide 256): per-chunk (mean, M2) BN partials and optional max-pool partials, in
  * pcs_gemm's epilogue formats.  One HBM pass; used for the 1024-wide global_feat output.

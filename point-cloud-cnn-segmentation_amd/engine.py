@@ -462,12 +462,41 @@ class Engine:
                 Y=ycur, alpha=al, beta=be, gamma=ga, X=sv.ys[prev_conv], s=pc.scale, t=pc.shift,
                 x_mask=x_mask, x_keep_scale=keep if x_mask is not None else 1.0))
 
+        def dgrad_wgrad(conv, bn, cin, cout, dz, ycur, prev_conv, prev_bn, out, c_mask=None,
+                        addend=None):
+            """Both gradients of one layer in one pass (csrc/fused_bwd.hip) where the fused
+            kernel covers the shape (bf16); otherwise the pcs_gemm(DGRAD) + pcs_wgrad pair."""
+            if self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC):
+                al, be, ga = coefs[bn]
+                pc = sv.bn[prev_bn]
+                a = L.GemmArgs(num_scenes=B, scene_rows=N, K=cout, Ncols=cin, dtype=self.dt,
+                               prologue=L.PRO_BWD, epilogue=L.EPI_DGRAD, chunks_per_scene=0,
+                               flags=self.flags, A=L.ptr(dz), W=L.ptr(wc[conv][1]), C=L.ptr(out),
+                               a_keep_scale=1.0, c_keep_scale=keep if c_mask is not None else 1.0)
+                for k, v in dict(A2=ycur, pa=al, pb=be, pc=ga, Yp=sv.ys[prev_conv], es=pc.scale,
+                                 et=pc.shift, emean=pc.mean, erstd=pc.rstd, c_mask=c_mask,
+                                 addend=addend).items():
+                    setattr(a, k, L.ptr(v))
+                nbytes = L.load().pcs_dgrad_wgrad_bn_workspace(ct.byref(a))
+                if nbytes > 0:
+                    cps = a.chunks_per_scene
+                    st = torch.empty(B * cps, cin, 2, dtype=torch.float32, device=dev)
+                    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+                    a.stats = L.ptr(st)
+                    self._launch(f"dgrad+wgrad:{conv}", "pcs_dgrad_wgrad_bn", ct.byref(a), L.ptr(ws),
+                                 L.ptr(G(f"{conv}.weight")), 0, s)
+                    keepalive.append(ws)
+                    return st, cps
+            st, cps = dgrad(conv, bn, cin, cout, dz, ycur, prev_conv, prev_bn, out, c_mask=c_mask,
+                            addend=addend)
+            wgrad(conv, bn, cin, cout, dz, ycur, prev_conv, prev_bn, x_mask=c_mask)
+            return st, cps
+
         ys = sv.ys
         # seg_conv3 (input: dropout(relu(bn_seg2(y_s2))))
         dz_s3 = bufA
-        st, cps = dgrad("seg_conv3", "bn_seg3", 256, 128, dz_s3, ys["seg_conv3"], "seg_conv2",
-                        "bn_seg2", bufB, c_mask=m2)
-        wgrad("seg_conv3", "bn_seg3", 256, 128, dz_s3, ys["seg_conv3"], "seg_conv2", "bn_seg2", x_mask=m2)
+        st, cps = dgrad_wgrad("seg_conv3", "bn_seg3", 256, 128, dz_s3, ys["seg_conv3"], "seg_conv2",
+                              "bn_seg2", bufB, c_mask=m2)
         bn_bwd("bn_seg2", "seg_conv2", st, cps)
         # seg_conv2 (input: dropout(relu(bn_seg1(y_s1))))
         dz_s2 = bufB
@@ -588,16 +617,13 @@ class Engine:
         keepalive.append((ws_t, c5, h4, pbuf, r5, g4, s4, ws4))
         bn_bwd("bn4", "conv4", st, cps4)
         dz4 = bufA
-        st, cps = dgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3", bufB)
-        wgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3")
+        st, cps = dgrad_wgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3", bufB)
         bn_bwd("bn3", "conv3", st, cps)
         dz3 = bufB
-        st, cps = dgrad("conv3", "bn3", 64, 64, dz3, ys["conv3"], "conv2", "bn2", bufA, addend=dA2)
-        wgrad("conv3", "bn3", 64, 64, dz3, ys["conv3"], "conv2", "bn2")
+        st, cps = dgrad_wgrad("conv3", "bn3", 64, 64, dz3, ys["conv3"], "conv2", "bn2", bufA, addend=dA2)
         bn_bwd("bn2", "conv2", st, cps)
         dz2 = bufA
-        st, cps = dgrad("conv2", "bn2", 64, 64, dz2, ys["conv2"], "conv1", "bn1", bufB)
-        wgrad("conv2", "bn2", 64, 64, dz2, ys["conv2"], "conv1", "bn1")
+        st, cps = dgrad_wgrad("conv2", "bn2", 64, 64, dz2, ys["conv2"], "conv1", "bn1", bufB)
         bn_bwd("bn1", "conv1", st, cps)
         dz1 = bufB
         al, be, ga = coefs["bn1"]

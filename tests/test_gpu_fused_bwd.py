@@ -61,3 +61,64 @@ def test_dgrad_wgrad_rejects_other_shapes():
     a = L.WgradArgs(num_scenes=1, scene_rows=128, Cout=256, Cin=64, dtype=L.BF16, dy_mode=L.PRO_BWD,
                     x_mode=L.PRO_BNRELU)
     assert L.load().pcs_dgrad_wgrad_workspace(ct.byref(a)) < 0
+
+
+@pytest.mark.parametrize("cout,cin,variant,B,N", [
+    (64, 64, "plain", 3, 1000), (64, 64, "addend", 2, 4096 + 33), (128, 64, "plain", 4, 4096),
+    (128, 64, "plain", 1, 64 * 40 + 5), (128, 64, "mask", 3, 777)])
+def test_dgrad_wgrad_bn_matches_torch(cout, cin, variant, B, N):
+    """pcs_dgrad_wgrad_bn (conv2/conv3/conv4) vs torch fp32 on the same bf16 inputs:
+    dz' = (es*Yp + et > 0) * keep * ks * (dy W + addend), its per-chunk S1 / S2 statistics
+    (S2 = rstd * (sum dz' Yp - mean * S1)) and dW = dy^T x."""
+    import pcs_amd._lib as L
+    g = torch.Generator(device="cpu").manual_seed(cout * 31 + cin + N)
+    M = B * N
+    bf = lambda t: t.to(DEV, torch.bfloat16)   # noqa: E731
+    dZ, Y = bf(torch.randn(M, cout, generator=g) * 0.1), bf(torch.randn(M, cout, generator=g))
+    Yp = bf(torch.randn(M, cin, generator=g))
+    al, be, ga = (torch.randn(cout, generator=g).to(DEV) * s for s in (1.0, 0.01, 0.05))
+    es, et = torch.rand(cin, generator=g).to(DEV) + 0.5, torch.randn(cin, generator=g).to(DEV) * 0.3
+    emean, erstd = torch.randn(cin, generator=g).to(DEV) * 0.1, torch.rand(cin, generator=g).to(DEV) + 0.5
+    W = torch.randn(cout, cin, generator=g).to(DEV) * 0.05
+    Wt = W.t().contiguous().to(torch.bfloat16)          # [cin, cout] = the dgrad GEMM's W
+    add = bf(torch.randn(M, cin, generator=g) * 0.1) if variant == "addend" else None
+    keep = (torch.rand(M, cin, generator=g) < 0.7) if variant == "mask" else None
+    ks = 1.0 / 0.7 if keep is not None else 1.0
+    bits = None
+    if keep is not None:
+        w8 = (1 << torch.arange(8)).to(torch.uint8)
+        bits = (keep.view(M, cin // 8, 8).to(torch.uint8) * w8).sum(-1).to(torch.uint8).to(DEV)
+    out = torch.empty(M, cin, device=DEV, dtype=torch.bfloat16)
+    dW = torch.zeros(cout, cin, device=DEV)
+    a = L.GemmArgs(num_scenes=B, scene_rows=N, K=cout, Ncols=cin, dtype=L.BF16, prologue=L.PRO_BWD,
+                   epilogue=L.EPI_DGRAD, chunks_per_scene=0, A=dZ.data_ptr(), W=Wt.data_ptr(), C=out.data_ptr(),
+                   a_keep_scale=1.0, c_keep_scale=ks)
+    for k, v in dict(A2=Y, pa=al, pb=be, pc=ga, Yp=Yp, es=es, et=et, emean=emean, erstd=erstd,
+                     c_mask=bits, addend=add).items():
+        setattr(a, k, L.ptr(v))
+    nbytes = L.load().pcs_dgrad_wgrad_bn_workspace(ct.byref(a))
+    assert nbytes > 0
+    cps = a.chunks_per_scene
+    st = torch.empty(B * cps, cin, 2, device=DEV)
+    ws = torch.empty(nbytes // 4, device=DEV)
+    a.stats = st.data_ptr()
+    L.call("pcs_dgrad_wgrad_bn", ct.byref(a), ws.data_ptr(), dW.data_ptr(), 0, L.stream_ptr())
+    torch.cuda.synchronize()
+
+    dy = (al * dZ.float() + (ga * Y.float() + be)).to(torch.bfloat16).float()
+    yp = Yp.float()
+    kf = keep.to(DEV).float() if keep is not None else torch.ones_like(yp)
+    x = (torch.relu(yp * es + et) * kf * ks).to(torch.bfloat16).float()
+    gv = dy @ Wt.float().t()
+    if add is not None:
+        gv = gv + add.float()
+    dz = torch.where(yp * es + et > 0, gv * kf * ks, torch.zeros_like(gv))
+    assert _rel(out.float(), dz) < 1e-2
+    assert _rel(dW, dy.t() @ x) < 1e-4
+    # statistics: per scene sums over the chunks equal the per-scene sums of dz (fp32)
+    s1 = st[..., 0].view(B, cps, cin).sum(1)
+    s2 = st[..., 1].view(B, cps, cin).sum(1)
+    dzs = dz.view(B, N, cin)
+    r1 = dzs.sum(1)
+    r2 = erstd * ((dzs * yp.view(B, N, cin)).sum(1) - emean * r1)
+    assert _rel(s1, r1) < 1e-3 and _rel(s2, r2) < 1e-3
