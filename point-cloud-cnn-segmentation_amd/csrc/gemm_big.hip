@@ -18,6 +18,10 @@
 //   generic kernel's partial layout.
 #include "common.h"
 
+#ifndef PCS_DGRAD_BATCH
+#define PCS_DGRAD_BATCH 4   // DGRAD epilogue: rows of Yp (and mask / addend) loaded per batch
+#endif
+
 namespace {
 
 constexpr int THREADS = 512;
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       const int lc = ecc * EPC;
       lds_vec8(ecf + lc, es); lds_vec8(ecf + BN + lc, et);
       const float ks = a.c_keep_scale;
-      constexpr int BATCH = 4;
+      constexpr int BATCH = ADD ? (PCS_DGRAD_BATCH + 1) / 2 : PCS_DGRAD_BATCH;
 #pragma unroll
       for (int p0 = 0; p0 < NPASS; p0 += BATCH) {
         u32x4 yv[BATCH], adv[BATCH];

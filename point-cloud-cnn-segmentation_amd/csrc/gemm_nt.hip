@@ -555,6 +555,9 @@ static constexpr int GEMM_BM = 128;
 // of that class ends up on the generic kernel (an operand combination the wide kernels do not
 // implement), that kernel walks the same chunks in 128-row tiles.
 static bool wide_class(const pcs_gemm_args &a) {
+  // seg_conv3's input gradient (K 128 -> 256 columns, DGRAD epilogue): the 128-row kernel
+  // measured faster at cfg2 (3.13 vs 3.38 ms, tools/bench_bwd_shapes.py)
+  if (a.K == 128 && a.Ncols == 256 && a.epilogue == PCS_EPI_DGRAD) return false;
   return a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && a.K % 64 == 0 && a.Ncols % 256 == 0 &&
          a.K >= 128 && a.K <= 1024;
 }
