@@ -268,46 +268,57 @@ extern "C" int pcs_dgrad_wgrad(const pcs_wgrad_args *ap, const void *Wt, void *d
 // The dgrad epilogue and the weight gradient read the same Yp (and dropout bits), and both
 // contractions read the same dy, so one pass moves dZ, Y, Yp (+ addend) in and dz' out:
 // e.g. conv4 0.77 KB per point instead of 1.41 KB for pcs_gemm(DGRAD) + pcs_wgrad.
-// Structure as dgrad_wgrad_s1_kernel: W^T [CIN][COUT] resident in LDS, MS-row steps with one
-// register prefetch stage; the dgrad accumulators run the epilogue in place (lane: one row,
-// 4 consecutive columns per tile), per-lane S1/S2 over the workgroup's rows, reduced at the
-// end (16-lane shuffles, then across the waves sharing a column block through LDS).
+// A workgroup owns a CB-wide block of the CIN columns (CB = CIN for the 64-wide layers; 128
+// for seg_conv2/3, whose W^T and dW do not fit one workgroup): the CIN / CB workgroups of a
+// row chunk are consecutive, so they run together on one XCD and the dy slab they all stage
+// is served from that XCD's L2 after the first read.
+// Structure as dgrad_wgrad_s1_kernel: the W^T block [CB][COUT] resident in LDS, MS-row steps
+// with one register prefetch stage; the dgrad accumulators run the epilogue in place (lane:
+// one row, 4 consecutive columns per tile), per-lane S1/S2 over the workgroup's rows,
+// reduced at the end (16-lane shuffles, then across the waves sharing a column block).
 // =======================================================================================
 namespace {
 
-template <int COUT, int CIN, int MS, bool MASK, bool ADD> struct FB {
+template <int COUT, int CIN, int CB, int MS, bool MASK, bool ADD> struct FB {
+  static constexpr int NBLK = CIN / CB;
   static constexpr int WT_ROWB = COUT * 2;
   static constexpr int DY_ROWB = COUT * 2 + 32;
-  static constexpr int X_ROWB = CIN * 2 + 32;
-  static constexpr int YP_ROWB = CIN * 2;
-  static constexpr int OFF_DY = CIN * WT_ROWB;
+  static constexpr int X_ROWB = CB * 2 + 32;
+  static constexpr int YP_ROWB = CB * 2;
+  static constexpr int OFF_DY = CB * WT_ROWB;
   static constexpr int OFF_X = OFF_DY + MS * DY_ROWB;
   static constexpr int OFF_YP = OFF_X + MS * X_ROWB;
   static constexpr int OFF_AD = OFF_YP + MS * YP_ROWB;
   static constexpr int OFF_MK = OFF_AD + (ADD ? MS * YP_ROWB : 0);
-  static constexpr int OFF_OUT = OFF_MK + (MASK ? MS * CIN / 8 : 0);
-  static constexpr int OFF_COEF = OFF_OUT + MS * CIN * 2;   // alpha|beta|gamma [COUT], es|et [CIN]
-  static constexpr int BYTES = OFF_COEF + (3 * COUT + 2 * CIN) * 4;
-  static_assert(BYTES <= 160 * 1024, "LDS budget");
-  static constexpr int NCB = CIN / 16, NMB = MS / 16, NOB = COUT / 16;
+  static constexpr int OFF_OUT = OFF_MK + (MASK ? MS * CB / 8 : 0);
+  static constexpr int OFF_COEF = OFF_OUT + MS * CB * 2;   // alpha|beta|gamma [COUT], es|et [CB]
+  static constexpr int BYTES = OFF_COEF + (3 * COUT + 2 * CB) * 4;
+  static constexpr bool FITS = BYTES <= 160 * 1024;   // LDS budget (checked in the kernel)
+  static_assert(CIN % CB == 0, "column blocks");
+  static constexpr int NCB = CB / 16, NMB = MS / 16, NOB = COUT / 16;
   static constexpr int TPW_D = NMB * NCB / 8, TPW_W = NOB * NCB / 8;   // tiles per wave
-  static_assert(TPW_D >= 1 && TPW_W >= 1 && NCB % TPW_D == 0 && NCB % TPW_W == 0, "wave tiling");
-  static constexpr int NCH_D = MS * COUT / 8 / THREADS, NCH_P = MS * CIN / 8 / THREADS;
+  static constexpr int OBW = TPW_W > NCB ? TPW_W / NCB : 1;            // wgrad row blocks per wave
+  static_assert(TPW_D >= 1 && TPW_W >= 1 && NCB % TPW_D == 0, "dgrad wave tiling");
+  static_assert(TPW_W % NCB == 0 || NCB % TPW_W == 0, "wgrad wave tiling");
+  static constexpr int CBW = TPW_W / OBW;                              // wgrad column blocks per wave
+  static constexpr int NCH_D = MS * COUT / 8 / THREADS, NCH_P = MS * CB / 8 / THREADS;
   static_assert(NCH_D >= 1 && NCH_P >= 1 && MS % 32 == 0, "staging");
 };
 
 PCS_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 PCS_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
-template <int COUT, int CIN, int MS, bool MASK, bool ADD>
+template <int COUT, int CIN, int CB, int MS, bool MASK, bool ADD>
 __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a, float *__restrict__ wpart,
                                                                  int64_t rows_per_split) {
-  typedef FB<COUT, CIN, MS, MASK, ADD> F;
+  typedef FB<COUT, CIN, CB, MS, MASK, ADD> F;
+  static_assert(F::FITS, "LDS budget");
   __shared__ __attribute__((aligned(16))) char lds[F::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = L / F::NBLK, n0 = (L % F::NBLK) * CB;
   const int sps = a.chunks_per_scene;
-  const int scene = L / sps, sis = L % sps;
+  const int scene = chunk / sps, sis = chunk % sps;
   const int64_t N = a.scene_rows;
   const int64_t lo = (int64_t)sis * rows_per_split;
   const int64_t hi = pcs_min64(lo + rows_per_split, N);
@@ -320,14 +331,14 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
   bf16_t *__restrict__ Cg = reinterpret_cast<bf16_t *>(a.C);
   const float ks = MASK ? a.c_keep_scale : 1.f;
 
-  for (int i = tid; i < CIN * COUT / 8; i += THREADS) {   // W^T [CIN][COUT] -> LDS
+  for (int i = tid; i < CB * COUT / 8; i += THREADS) {   // W^T rows n0.. [CB][COUT] -> LDS
     const int c = i / (COUT / 8), slot = i % (COUT / 8);
     *reinterpret_cast<u32x4 *>(lds + c * F::WT_ROWB + ((slot ^ (c & 7)) << 4)) =
-        *reinterpret_cast<const u32x4 *>(Wt + (int64_t)c * COUT + slot * 8);
+        *reinterpret_cast<const u32x4 *>(Wt + (int64_t)(n0 + c) * COUT + slot * 8);
   }
   float *cf = reinterpret_cast<float *>(lds + F::OFF_COEF);
   for (int i = tid; i < COUT; i += THREADS) { cf[i] = a.pa[i]; cf[COUT + i] = a.pb[i]; cf[2 * COUT + i] = a.pc[i]; }
-  for (int i = tid; i < CIN; i += THREADS) { cf[3 * COUT + i] = a.es[i]; cf[3 * COUT + CIN + i] = a.et[i]; }
+  for (int i = tid; i < CB; i += THREADS) { cf[3 * COUT + i] = a.es[n0 + i]; cf[3 * COUT + CB + i] = a.et[n0 + i]; }
   __syncthreads();
 
   u32x4 rz[F::NCH_D], ry[F::NCH_D], rp[F::NCH_P], rd[ADD ? F::NCH_P : 1];
@@ -342,8 +353,8 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     }
 #pragma unroll
     for (int i = 0; i < F::NCH_P; ++i) {
-      const int q = tid + THREADS * i, rl = q / (CIN / 8), cc = q % (CIN / 8);
-      const int64_t off = (sbase + pcs_min64(m0 + rl, hi - 1)) * CIN + cc * 8;
+      const int q = tid + THREADS * i, rl = q / (CB / 8), cc = q % (CB / 8);
+      const int64_t off = (sbase + pcs_min64(m0 + rl, hi - 1)) * CIN + n0 + cc * 8;
       rp[i] = *reinterpret_cast<const u32x4 *>(Ypg + off);
       if constexpr (ADD) rd[i] = *reinterpret_cast<const u32x4 *>(Adg + off);
       if constexpr (MASK) rm[i] = a.c_mask[off >> 3];
@@ -365,9 +376,9 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     }
 #pragma unroll
     for (int i = 0; i < F::NCH_P; ++i) {
-      const int q = tid + THREADS * i, rl = q / (CIN / 8), cc = q % (CIN / 8);
+      const int q = tid + THREADS * i, rl = q / (CB / 8), cc = q % (CB / 8);
       float s8[8], t8[8], v[8];
-      lds_vec8(cf + 3 * COUT + cc * 8, s8); lds_vec8(cf + 3 * COUT + CIN + cc * 8, t8);
+      lds_vec8(cf + 3 * COUT + cc * 8, s8); lds_vec8(cf + 3 * COUT + CB + cc * 8, t8);
       unpack_chunk(rp[i], v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -380,13 +391,15 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
       *reinterpret_cast<u32x4 *>(lds + F::OFF_X + prow(rl) * F::X_ROWB + cc * 16) = out;
       *reinterpret_cast<u32x4 *>(lds + F::OFF_YP + rl * F::YP_ROWB + cc * 16) = rp[i];
       if constexpr (ADD) *reinterpret_cast<u32x4 *>(lds + F::OFF_AD + rl * F::YP_ROWB + cc * 16) = rd[i];
-      if constexpr (MASK) lds[F::OFF_MK + rl * (CIN / 8) + cc] = (char)rm[i];
+      if constexpr (MASK) lds[F::OFF_MK + rl * (CB / 8) + cc] = (char)rm[i];
     }
   };
 
-  f32x4 accw[F::TPW_W];
+  f32x4 accw[F::OBW][F::CBW];
 #pragma unroll
-  for (int u = 0; u < F::TPW_W; ++u) accw[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int o = 0; o < F::OBW; ++o)
+#pragma unroll
+    for (int u = 0; u < F::CBW; ++u) accw[o][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   float s1[F::TPW_D][4], s2[F::TPW_D][4];
 #pragma unroll
   for (int u = 0; u < F::TPW_D; ++u)
@@ -404,7 +417,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
 
   const int g = lane >> 4, l16 = lane & 15;
   const int td0 = wid * F::TPW_D, mb = td0 / F::NCB, cbd = td0 % F::NCB;   // dgrad tiles (same mb)
-  const int tw0 = wid * F::TPW_W, ob = tw0 / F::NCB, cbw = tw0 % F::NCB;   // wgrad tiles (same ob)
+  const int tw0 = wid * F::TPW_W, ob0 = tw0 / F::NCB, cbw = tw0 % F::NCB;  // wgrad: OBW row blocks x CBW
   const char *tDY = lds + F::OFF_DY, *tX = lds + F::OFF_X;
   const int ml = mb * 16 + l16;   // this lane's row of the dgrad tiles
   for (int st = 0; st < nsteps; ++st) {
@@ -412,7 +425,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     f32x4 accd[F::TPW_D];
 #pragma unroll
     for (int u = 0; u < F::TPW_D; ++u) accd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 2
     for (int kk = 0; kk < COUT / 32; ++kk) {
       const int slot = 4 * kk + g;
       const bf16x8 yf = *reinterpret_cast<const bf16x8 *>(tDY + prow(ml) * F::DY_ROWB + slot * 16);
@@ -427,14 +440,18 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     for (int kk = 0; kk < MS / 32; ++kk) {
       const int q = (lane >> 2) & 3, p = lane & 3;
       const int r0 = prow(32 * kk + 8 * g + q), r1 = prow(32 * kk + 8 * g + 4 + q);
-      const bf16x8 yf = tr_read(tDY, r0, r1, F::DY_ROWB, ob * 16 + 4 * p);
+      bf16x8 yf[F::OBW];   // the few dy fragments stay live; x fragments are read one at a time
 #pragma unroll
-      for (int u = 0; u < F::TPW_W; ++u) {
+      for (int o = 0; o < F::OBW; ++o) yf[o] = tr_read(tDY, r0, r1, F::DY_ROWB, (ob0 + o) * 16 + 4 * p);
+#pragma unroll
+      for (int u = 0; u < F::CBW; ++u) {
         const bf16x8 xf = tr_read(tX, r0, r1, F::X_ROWB, (cbw + u) * 16 + 4 * p);
-        accw[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, yf, accw[u], 0, 0, 0);
+#pragma unroll
+        for (int o = 0; o < F::OBW; ++o)
+          accw[o][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, yf[o], accw[o][u], 0, 0, 0);
       }
     }
-    // epilogue in place: lane holds g[m = ml][c = 16 (cbd + u) + 4 g + r]
+    // epilogue in place: lane holds g[m = ml][c = 16 (cbd + u) + 4 g + r] (block-local c)
     const bool live = m0 + ml < hi;
 #pragma unroll
     for (int u = 0; u < F::TPW_D; ++u) {
@@ -447,26 +464,26 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
         v[0] += bf_lo(ad.x); v[1] += bf_hi(ad.x); v[2] += bf_lo(ad.y); v[3] += bf_hi(ad.y);
       }
       uint32_t kb = 0xFu;
-      if constexpr (MASK) kb = ((uint32_t)(uint8_t)lds[F::OFF_MK + ml * (CIN / 8) + (c >> 3)] >> (c & 7)) & 0xFu;
+      if constexpr (MASK) kb = ((uint32_t)(uint8_t)lds[F::OFF_MK + ml * (CB / 8) + (c >> 3)] >> (c & 7)) & 0xFu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float gv = v[r];
         if constexpr (MASK) gv = ((kb >> r) & 1u) ? gv * ks : 0.f;
-        const float dz = (live && fmaf(y[r], cf[3 * COUT + c + r], cf[3 * COUT + CIN + c + r]) > 0.f) ? gv : 0.f;
+        const float dz = (live && fmaf(y[r], cf[3 * COUT + c + r], cf[3 * COUT + CB + c + r]) > 0.f) ? gv : 0.f;
         v[r] = dz;
         s1[u][r] += dz;
         s2[u][r] = fmaf(dz, y[r], s2[u][r]);
       }
-      *reinterpret_cast<uint2 *>(lds + F::OFF_OUT + ml * CIN * 2 + c * 2) =
+      *reinterpret_cast<uint2 *>(lds + F::OFF_OUT + ml * CB * 2 + c * 2) =
           make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
     }
     lds_barrier();   // step st consumed; its dz' tile complete
 #pragma unroll
     for (int i = 0; i < F::NCH_P; ++i) {
-      const int q = tid + THREADS * i, rl = q / (CIN / 8), cc = q % (CIN / 8);
+      const int q = tid + THREADS * i, rl = q / (CB / 8), cc = q % (CB / 8);
       if (m0 + rl < hi)
-        *reinterpret_cast<u32x4 *>(Cg + (sbase + m0 + rl) * CIN + cc * 8) =
-            *reinterpret_cast<const u32x4 *>(lds + F::OFF_OUT + rl * CIN * 2 + cc * 16);
+        *reinterpret_cast<u32x4 *>(Cg + (sbase + m0 + rl) * CIN + n0 + cc * 8) =
+            *reinterpret_cast<const u32x4 *>(lds + F::OFF_OUT + rl * CB * 2 + cc * 16);
     }
     if (st + 1 < nsteps) {
       store_step(m0 + MS);
@@ -476,12 +493,14 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     lds_barrier();
   }
 
-  // dW partial: lane holds dW[o = 16 ob + l16][c = 16 (cbw + u) + 4 g ..]
-  float *out = wpart + (int64_t)L * COUT * CIN;
+  // dW partial (chunk slab, columns n0..): lane holds dW[o = 16 (ob0 + o) + l16][c = 16 (cbw + u) + 4 g ..]
+  float *out = wpart + (int64_t)chunk * COUT * CIN + n0;
 #pragma unroll
-  for (int u = 0; u < F::TPW_W; ++u)
-    *reinterpret_cast<float4 *>(out + (ob * 16 + l16) * CIN + (cbw + u) * 16 + 4 * g) =
-        make_float4(accw[u][0], accw[u][1], accw[u][2], accw[u][3]);
+  for (int o = 0; o < F::OBW; ++o)
+#pragma unroll
+    for (int u = 0; u < F::CBW; ++u)
+      *reinterpret_cast<float4 *>(out + ((ob0 + o) * 16 + l16) * CIN + (cbw + u) * 16 + 4 * g) =
+          make_float4(accw[o][u][0], accw[o][u][1], accw[o][u][2], accw[o][u][3]);
 
   // S1 / S2: sum the 16 rows (lanes l16) of each column, then the NMB row blocks via LDS
 #pragma unroll
@@ -493,58 +512,72 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
         s1[u][r] += __shfl_xor(s1[u][r], o);
         s2[u][r] += __shfl_xor(s2[u][r], o);
       }
-  float2 *red = reinterpret_cast<float2 *>(lds);   // [NMB][CIN] (W^T area, no longer read)
+  float2 *red = reinterpret_cast<float2 *>(lds);   // [NMB][CB] (W^T area, no longer read)
   if (l16 == 0) {
 #pragma unroll
     for (int u = 0; u < F::TPW_D; ++u)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[mb * CIN + (cbd + u) * 16 + 4 * g + r] = make_float2(s1[u][r], s2[u][r]);
+      for (int r = 0; r < 4; ++r) red[mb * CB + (cbd + u) * 16 + 4 * g + r] = make_float2(s1[u][r], s2[u][r]);
   }
   __syncthreads();
-  for (int c = tid; c < CIN; c += THREADS) {
+  for (int c = tid; c < CB; c += THREADS) {
     float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-    for (int b = 0; b < F::NMB; ++b) { t1 += red[b * CIN + c].x; t2 += red[b * CIN + c].y; }
-    *reinterpret_cast<float2 *>(a.stats + ((int64_t)L * CIN + c) * 2) =
-        make_float2(t1, a.erstd[c] * (t2 - a.emean[c] * t1));
+    for (int b = 0; b < F::NMB; ++b) { t1 += red[b * CB + c].x; t2 += red[b * CB + c].y; }
+    *reinterpret_cast<float2 *>(a.stats + ((int64_t)chunk * CIN + n0 + c) * 2) =
+        make_float2(t1, a.erstd[n0 + c] * (t2 - a.emean[n0 + c] * t1));
   }
 }
 
-template <int COUT, int CIN, int MS>
-int launch_bn(const pcs_gemm_args &a, float *wpart, int64_t rps, int nb, hipStream_t s) {
+template <int COUT, int CIN, int CB, int MS>
+int launch_bn(const pcs_gemm_args &a, float *wpart, int64_t rps, hipStream_t s) {
+  const int nb = (int)(a.num_scenes * a.chunks_per_scene) * (CIN / CB);
   if (a.c_mask && a.addend) return pcs_set_einval("pcs_dgrad_wgrad_bn", "mask and addend together");
   if (a.c_mask)
-    hipLaunchKernelGGL((dgrad_wgrad_bn_kernel<COUT, CIN, MS, true, false>), dim3(nb), dim3(THREADS), 0, s, a, wpart, rps);
-  else if (a.addend)
-    hipLaunchKernelGGL((dgrad_wgrad_bn_kernel<COUT, CIN, MS, false, true>), dim3(nb), dim3(THREADS), 0, s, a, wpart, rps);
-  else
-    hipLaunchKernelGGL((dgrad_wgrad_bn_kernel<COUT, CIN, MS, false, false>), dim3(nb), dim3(THREADS), 0, s, a, wpart,
-                       rps);
+    hipLaunchKernelGGL((dgrad_wgrad_bn_kernel<COUT, CIN, CB, MS, true, false>), dim3(nb), dim3(THREADS), 0, s, a, wpart, rps);
+  else if (a.addend) {
+    if constexpr (FB<COUT, CIN, CB, MS, false, true>::FITS)
+      hipLaunchKernelGGL((dgrad_wgrad_bn_kernel<COUT, CIN, CB, MS, false, true>), dim3(nb), dim3(THREADS), 0, s, a, wpart,
+                         rps);
+    else
+      return pcs_set_einval("pcs_dgrad_wgrad_bn", "no addend variant at this shape (LDS)");
+  } else
+    hipLaunchKernelGGL((dgrad_wgrad_bn_kernel<COUT, CIN, CB, MS, false, false>), dim3(nb), dim3(THREADS), 0, s, a,
+                       wpart, rps);
   PCS_CHECK_LAUNCH();
   return 0;
 }
 
-// Rows per step of the supported (Cout, Cin) pairs, 0 = none.  seg_conv3 (128 x 256) fits
-// LDS only at 32-row steps, where the pass measured slower (5.1 ms at cfg2) than the
-// pcs_gemm + pcs_wgrad pair it replaces (4.9 ms), so it stays on that pair.
-int bn_ms(int K, int Ncols) {
-  if (K == 64 && Ncols == 64) return 64;
-  if (K == 128 && Ncols == 64) return 64;
-  return 0;
+// (Cout, Cin) pairs served: (column block, rows per step).  The column-block split also
+// instantiates seg_conv3 (128 x 256, CB 128, 64-row steps) and seg_conv2 (256 x 512, CB 128,
+// 32-row steps: 64 spill VGPRs); both are correct (tests/test_gpu_fused_bwd.py history) but
+// measured no faster at cfg2 than the pcs_gemm + pcs_wgrad pair they replace (seg_conv3
+// 4.96 vs 4.73 ms, seg_conv2 12.8 vs 12.6 ms: 2 TB/s, latency-bound at one workgroup per
+// CU with the dy slab staged once per column block), so they stay on the pair.
+struct BnShape { int cout, cin, cb, ms; };
+constexpr BnShape kBnShapes[] = {{64, 64, 64, 64}, {128, 64, 64, 64}};
+
+const BnShape *bn_shape(int K, int Ncols) {
+  for (const BnShape &b : kBnShapes)
+    if (b.cout == K && b.cin == Ncols) return &b;
+  return nullptr;
 }
 
 }  // namespace
 
 extern "C" int64_t pcs_dgrad_wgrad_bn_workspace(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_dgrad_wgrad_bn_workspace", "bad geometry");
-  if (a->dtype != PCS_BF16 || !bn_ms(a->K, a->Ncols) || (a->flags & PCS_FLAG_GENERIC))
+  const BnShape *sh = bn_shape(a->K, a->Ncols);
+  if (a->dtype != PCS_BF16 || !sh || (a->flags & PCS_FLAG_GENERIC))
     return pcs_set_einval("pcs_dgrad_wgrad_bn_workspace",
                           "bf16 with (Cout, Cin) = K x Ncols in {64x64, 128x64} only");
-  const int ms = bn_ms(a->K, a->Ncols);
-  int64_t sps = (256 + a->num_scenes - 1) / a->num_scenes;
-  const int64_t max_sps = (a->scene_rows + 4 * ms - 1) / (4 * ms);
+  const int nblk = sh->cin / sh->cb;
+  int64_t sps = (256 + a->num_scenes * nblk - 1) / (a->num_scenes * nblk);
+  const int64_t max_sps = (a->scene_rows + 4 * sh->ms - 1) / (4 * sh->ms);
   if (sps > max_sps) sps = max_sps;
-  a->chunks_per_scene = (int32_t)(sps < 1 ? 1 : sps);
+  if (sps < 1) sps = 1;
+  const int64_t rps = ((a->scene_rows + sps - 1) / sps + sh->ms - 1) / sh->ms * sh->ms;
+  a->chunks_per_scene = (int32_t)((a->scene_rows + rps - 1) / rps);   // no empty chunks
   return (int64_t)a->num_scenes * a->chunks_per_scene * a->K * a->Ncols * 4;
 }
 
@@ -560,13 +593,13 @@ extern "C" int pcs_dgrad_wgrad_bn(const pcs_gemm_args *ap, float *partial, float
     return pcs_set_einval("pcs_dgrad_wgrad_bn", "missing operand (A, A2, pa, pb, pc, W, C, Yp, es, et, emean, "
                                                 "erstd, stats)");
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31) return pcs_set_einval("pcs_dgrad_wgrad_bn", "M must be < 2^31");
-  const int ms = bn_ms(a.K, a.Ncols);
-  const int64_t rps = ((a.scene_rows + a.chunks_per_scene - 1) / a.chunks_per_scene + ms - 1) / ms * ms;
-  const int nb = (int)(a.num_scenes * a.chunks_per_scene);
+  const BnShape *sh = bn_shape(a.K, a.Ncols);
+  const int64_t rps = ((a.scene_rows + a.chunks_per_scene - 1) / a.chunks_per_scene + sh->ms - 1) / sh->ms * sh->ms;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc;
-  if (a.K == 64) rc = launch_bn<64, 64, 64>(a, partial, rps, nb, s);
-  else rc = launch_bn<128, 64, 64>(a, partial, rps, nb, s);
+  if (a.K == 64) rc = launch_bn<64, 64, 64, 64>(a, partial, rps, s);
+  else rc = launch_bn<128, 64, 64, 64>(a, partial, rps, s);
   if (rc) return rc;
-  return pcs_reduce_partials(partial, nb, (int64_t)a.K * a.Ncols, 1.0f, dW, ldw ? ldw : a.Ncols, a.Ncols, stream);
+  const int nslab = (int)(a.num_scenes * a.chunks_per_scene);
+  return pcs_reduce_partials(partial, nslab, (int64_t)a.K * a.Ncols, 1.0f, dW, ldw ? ldw : a.Ncols, a.Ncols, stream);
 }

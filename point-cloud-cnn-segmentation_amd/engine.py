@@ -500,9 +500,8 @@ class Engine:
         bn_bwd("bn_seg2", "seg_conv2", st, cps)
         # seg_conv2 (input: dropout(relu(bn_seg1(y_s1))))
         dz_s2 = bufB
-        st, cps = dgrad("seg_conv2", "bn_seg2", 512, 256, dz_s2, ys["seg_conv2"], "seg_conv1",
-                        "bn_seg1", bufA, c_mask=m1)
-        wgrad("seg_conv2", "bn_seg2", 512, 256, dz_s2, ys["seg_conv2"], "seg_conv1", "bn_seg1", x_mask=m1)
+        st, cps = dgrad_wgrad("seg_conv2", "bn_seg2", 512, 256, dz_s2, ys["seg_conv2"], "seg_conv1",
+                              "bn_seg1", bufA, c_mask=m1)
         scene_s1 = torch.empty(B, 512, dtype=torch.float32, device=dev)
         bn_bwd("bn_seg1", "seg_conv1", st, cps, scene_s1=scene_s1)
         dz_s1 = bufA

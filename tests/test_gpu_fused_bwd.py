@@ -67,7 +67,7 @@ def test_dgrad_wgrad_rejects_other_shapes():
     (64, 64, "plain", 3, 1000), (64, 64, "addend", 2, 4096 + 33), (128, 64, "plain", 4, 4096),
     (128, 64, "plain", 1, 64 * 40 + 5), (128, 64, "mask", 3, 777)])
 def test_dgrad_wgrad_bn_matches_torch(cout, cin, variant, B, N):
-    """pcs_dgrad_wgrad_bn (conv2/conv3/conv4) vs torch fp32 on the same bf16 inputs:
+    """pcs_dgrad_wgrad_bn (conv2/3/4) vs torch fp32 on the same bf16 inputs:
     dz' = (es*Yp + et > 0) * keep * ks * (dy W + addend), its per-chunk S1 / S2 statistics
     (S2 = rstd * (sum dz' Yp - mean * S1)) and dW = dy^T x."""
     import pcs_amd._lib as L
