@@ -312,8 +312,9 @@ int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float
                      uint8_t *bits, pcs_stream_t stream);
 
 /*
- * Gram of the BN+ReLU activations a = relu(Y * s + t) (Y [M, C] scene-major rows, the
- * stored pre-BN input of global_feat): G = a^T a (fp32 [C, C], symmetric, filled) and
+ * Gram of the BN+ReLU activations a = relu(Y * s + t) (Y [M, C] scene-major rows), or of Y
+ * itself when s = t = NULL (the stored a5 of global_feat; bf16, C % 256 == 0, no transform
+ * pass in the kernel): G = a^T a (fp32 [C, C], symmetric, filled) and
  * colsum[k] = sum_m a[m, k].  Used by pcs_gram_wgrad in place of the M x C x C weight-
  * gradient GEMM of global_feat (autograd of P:113 at P:254).  pcs_gram_workspace returns
  * the fp32 workspace bytes and the row splits per scene to pass to pcs_gram.

@@ -145,10 +145,6 @@ constexpr int PCS_BIG_BM = 256;
 bool pcs_gemm_glds_applicable(const pcs_gemm_args &a);
 int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                          hipStream_t s);
-// streaming W-resident forward kernel for the shallow-K layers (gemm_stream.hip)
-int64_t pcs_gemm_stream_geometry(pcs_gemm_args *a);   // 0 when the shape is not covered
-bool pcs_gemm_stream_applicable(const pcs_gemm_args &a);
-int pcs_gemm_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
 // wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)
 bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a);
 int pcs_wgrad_big_splits(const pcs_wgrad_args &a);

@@ -66,11 +66,28 @@ PCS_DEV void lds8(const float *p, float (&v)[8]) {
 // Transform one staged 64-row step (dy and x) and write it to LDS.  Coefficients come from
 // the workgroup's LDS copy (cf: [alpha|pool coef][beta][gamma][argmax] over its 256 Cout
 // columns, [s][t] over its 256 Cin columns); rows past the slice end are written as zeros.
-template <int DYMODE, bool MASK>
+template <int DYMODE, bool MASK, bool RAWG = false>
 PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_t rbase, int64_t rlast,
                       int bk, int cc, int r0, const u32x4 (&rz)[4], const u32x4 (&ry)[4],
                       const u32x4 (&rx)[4], const uint32_t (&mk)[4], bool diag, float (&csum)[8]) {
   char *tB = tA + OPB;
+  if constexpr (RAWG) {   // Gram of stored activations (a5): no transform, straight to LDS
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = r0 + 16 * i;
+      const bool ok = rbase + rl < rlast;
+      const u32x4 z = mk_u32x4(0, 0, 0, 0);
+      *reinterpret_cast<u32x4 *>(tA + prow(rl) * ROWB + cc * 16) = ok ? ry[i] : z;
+      *reinterpret_cast<u32x4 *>(tB + prow(rl) * ROWB + cc * 16) = ok ? rx[i] : z;
+      if (diag && ok) {
+        float w[8];
+        unpack_chunk(rx[i], w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += w[e];
+      }
+    }
+    return;
+  }
   float ca[8], cb[8], cg[8], xs[8], xt[8];
   int am[8];
   const int c8 = cc * 8;
@@ -130,7 +147,7 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_
   }
 }
 
-template <int DYMODE, bool MASK>
+template <int DYMODE, bool MASK, bool RAWG = false>
 __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, int64_t rows_per_split,
                                                             int ntn, int ntiles) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
@@ -167,6 +184,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
       cf[c] = a.pool_coef[(int64_t)scene * Cout + n0 + c];
       reinterpret_cast<int *>(cf)[768 + c] = a.pool_idx[(int64_t)scene * Cout + n0 + c];
     }
+    if constexpr (RAWG) continue;
     if constexpr (DYMODE == PCS_PRO_BNRELU) {
       cf[256 + c] = a.s[n0 + c];
       cf[512 + c] = a.t[n0 + c];
@@ -192,7 +210,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
   if (nsteps > 0) {
     const int64_t rb = scene * N + lo;
     tn_load<DYMODE, MASK>(dZ, Yg, Xg, a.x_mask, rb, rlast, Cout, Cin, an, bk, r0, rz, ry, rx, mk);
-    tn_store<DYMODE, MASK>(a, lds, cf, rb, rlast, bk, cc, r0, rz, ry, rx, mk, diag, csum);
+    tn_store<DYMODE, MASK, RAWG>(a, lds, cf, rb, rlast, bk, cc, r0, rz, ry, rx, mk, diag, csum);
     __syncthreads();
   }
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -218,8 +236,8 @@ __global__ __launch_bounds__(THREADS) void wgrad_big_kernel(pcs_wgrad_args a, in
       }
     }
     if (st + 1 < nsteps)
-      tn_store<DYMODE, MASK>(a, lds + (buf ^ 1) * STAGE, cf, rb + MS, rlast, bk, cc, r0, rz, ry, rx, mk,
-                             diag, csum);
+      tn_store<DYMODE, MASK, RAWG>(a, lds + (buf ^ 1) * STAGE, cf, rb + MS, rlast, bk, cc, r0, rz, ry, rx, mk,
+                                   diag, csum);
     lds_barrier();
   }
   // lane holds dW[n = n0 + wm*128 + i*16 + (lane&15)][k = k0 + wn*64 + j*16 + 4*(lane>>4) + r]
@@ -289,7 +307,11 @@ int pcs_wgrad_big_launch(const pcs_wgrad_args &a, hipStream_t s) {
   const int ntn = a.Cin / TN, ntiles = pcs_wgrad_big_tiles(a);
   const int nb = ntiles * (int)(a.num_scenes * a.splits_per_scene);
   if (a.dy_mode == PCS_PRO_BNRELU) {
-    hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BNRELU, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
+    if (!a.s)   // Gram of stored activations (pcs_gram with s = t = NULL)
+      hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BNRELU, false, true>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn,
+                         ntiles);
+    else
+      hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BNRELU, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
   } else if (a.dy_mode == PCS_PRO_BWD_POOL) {
     if (a.x_mask) hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD_POOL, true>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);
     else hipLaunchKernelGGL((wgrad_big_kernel<PCS_PRO_BWD_POOL, false>), dim3(nb), dim3(THREADS), 0, s, a, rps, ntn, ntiles);

@@ -565,7 +565,6 @@ static bool wide_class(const pcs_gemm_args &a) {
 extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Ncols <= 0)
     return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
-  if (const int64_t r = pcs_gemm_stream_geometry(a)) return r;   // W-resident streaming kernel
   if (wide_class(*a))
     return pcs_fill_geometry(a, PCS_BIG_BM, 256, a->Ncols / 256);   // one 512-thread WG per CU
   const int64_t ncb = a->Ncols >= 128 ? a->Ncols / 128 : 1;
@@ -604,13 +603,11 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool stream_geo = pcs_gemm_stream_geometry(&a) > 0;   // (recomputes the same geometry)
-  if (stream_geo && pcs_gemm_stream_applicable(a)) return pcs_gemm_stream_launch(a, rpc, s);
-  if (wide_class(a) && !stream_geo && pcs_gemm_glds_applicable(a)) {
+  if (wide_class(a) && pcs_gemm_glds_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_glds_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
   }
-  if (wide_class(a) && pcs_gemm_big_applicable(a)) {   // (256-row chunks under either geometry)
+  if (wide_class(a) && pcs_gemm_big_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_big_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
   }

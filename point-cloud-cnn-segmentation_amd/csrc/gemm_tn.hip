@@ -418,13 +418,15 @@ extern "C" int64_t pcs_gram_workspace(int64_t num_scenes, int64_t scene_rows, in
 extern "C" int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, int64_t scene_rows,
                         int32_t C, int32_t dtype, int32_t splits_per_scene, float *workspace, float *G,
                         float *colsum, pcs_stream_t stream) {
-  if (!Y || !s || !t || !workspace || !G || !colsum || splits_per_scene <= 0)
-    return pcs_set_einval("pcs_gram", "missing operand or splits");
+  if (!Y || !s != !t || !workspace || !G || !colsum || splits_per_scene <= 0)
+    return pcs_set_einval("pcs_gram", "missing operand or splits (s and t both set, or both NULL)");
   if (C % 64) return pcs_set_einval("pcs_gram", "C must be a multiple of 64");
   pcs_wgrad_args a = gram_args(Y, s, t, num_scenes, scene_rows, C, dtype, splits_per_scene);
   a.partial = workspace;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;
+  if (!s && !pcs_wgrad_big_applicable(a))   // s = t = NULL: Y is already the activation
+    return pcs_set_einval("pcs_gram", "s = t = NULL needs the 256x256 kernel (bf16, C % 256 == 0)");
   if (pcs_wgrad_big_applicable(a)) {
     rc = pcs_wgrad_big_launch(a, st);
   } else {

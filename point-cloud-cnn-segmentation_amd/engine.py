@@ -575,8 +575,10 @@ class Engine:
         sps = ct.c_int32(0)
         nbytes = L.load().pcs_gram_workspace(B, N, 1024, self.dt, ct.byref(sps))
         ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
-        self._launch("wgrad:global_feat", "pcs_gram", L.ptr(a5), L.ptr(ones), L.ptr(zeros),
-                     B, N, 1024, self.dt, sps.value, L.ptr(ws), L.ptr(gram), L.ptr(colsum), s)
+        raw = self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC)   # a5 is the activation itself
+        self._launch("wgrad:global_feat", "pcs_gram", L.ptr(a5), None if raw else L.ptr(ones),
+                     None if raw else L.ptr(zeros), B, N, 1024, self.dt, sps.value, L.ptr(ws), L.ptr(gram),
+                     L.ptr(colsum), s)
         self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg),
                      Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(a5),
                      L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.dt, None, None,

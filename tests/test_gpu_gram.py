@@ -69,3 +69,27 @@ def test_gram_wgrad_matches_direct(dtype):
     ref = dy.T @ ad
     err = (dW.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < (1e-5 if dtype == "fp32" else 5e-3), err
+
+
+@pytest.mark.parametrize("B,N,C", [(2, 700, 256), (4, 1000, 1024)])
+def test_raw_gram_of_stored_activations(B, N, C):
+    """s = t = NULL: the Gram of Y itself (the stored a5 >= 0), no transform pass; equals
+    torch on the same bf16 values (and the ragged row tail past each slice is excluded)."""
+    import pcs_amd._lib as L
+    g = torch.Generator().manual_seed(C + N)
+    A = torch.relu(torch.randn(B * N, C, generator=g)).to(torch.bfloat16).to(DEV)
+    sps = ct.c_int32(0)
+    nbytes = L.load().pcs_gram_workspace(B, N, C, L.BF16, ct.byref(sps))
+    ws = torch.empty(nbytes // 4, device=DEV)
+    G = torch.empty(C, C, device=DEV)
+    S = torch.empty(C, device=DEV)
+    L.call("pcs_gram", L.ptr(A), None, None, B, N, C, L.BF16, sps.value, L.ptr(ws), L.ptr(G), L.ptr(S),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    af = A.float()
+    ref = af.t() @ af
+    assert float((G - ref).norm() / ref.norm()) < 1e-5
+    assert float((S - af.sum(0)).norm() / af.sum(0).norm()) < 1e-5
+    with pytest.raises(L.PcsError):   # the identity form needs the 256x256 kernel
+        L.call("pcs_gram", L.ptr(A), None, None, B, N, 128, L.BF16, sps.value, L.ptr(ws), L.ptr(G),
+               L.ptr(S), L.stream_ptr())
