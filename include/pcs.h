@@ -423,6 +423,14 @@ int pcs_pad_scatter(const float *points, const void *labels, int32_t label_bytes
                     const int64_t *offsets, int64_t num_scenes, int64_t scene_rows,
                     float *points_out, int64_t *labels_out, uint8_t *mask_out, pcs_stream_t stream);
 
+/*
+ * out = W rounded to the compute dtype and widened back to fp32 (bf16: round-to-nearest-even,
+ * as pcs_cast_weight).  The bf16 path passes these to pcs_gram_wgrad: its dense terms
+ * beta S^T + diag(gamma) W G cancel to O(pool rows / M) of their size, so W must be the W the
+ * forward GEMM used, or the 2^-9 weight rounding dominates the gradient at large M.
+ */
+int pcs_round_weight(const float *W, int64_t n, int32_t dtype, float *out, pcs_stream_t stream);
+
 /* Build-time identification and error string. */
 int pcs_abi_version(void);
 const char *pcs_last_error(void);

@@ -1111,3 +1111,22 @@ extern "C" int pcs_adam(float *param, const float *grad, float *exp_avg, float *
   PCS_CHECK_LAUNCH();
   return 0;
 }
+
+namespace {
+__global__ void round_weight_kernel(const float *__restrict__ W, int64_t n, float *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = bf2f(pack2bf(W[i], 0.f) & 0xffffu);
+}
+}  // namespace
+
+// fp32 copy of the weights as the compute dtype sees them (bf16: round-to-nearest-even, the
+// rounding pcs_cast_weight applies), so the Gram-form weight gradients use the forward's W.
+extern "C" int pcs_round_weight(const float *W, int64_t n, int32_t dtype, float *out, pcs_stream_t stream) {
+  if (!W || !out || n < 0 || (dtype != PCS_F32 && dtype != PCS_BF16)) return pcs_set_einval("pcs_round_weight", "bad arguments");
+  if (n == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == PCS_F32) return hipMemcpyAsync(out, W, n * 4, hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : PCS_EINVAL;
+  hipLaunchKernelGGL(round_weight_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, W, n, out);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

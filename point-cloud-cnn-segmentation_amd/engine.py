@@ -216,6 +216,14 @@ class Engine:
         self._launch(tag, fn, ct.byref(a), self._stream())
         return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
+    def _rounded(self, W):
+        """fp32 copy of W as the forward's compute-dtype GEMM saw it (pcs_round_weight)."""
+        if self.dt == L.F32:
+            return W
+        out = torch.empty_like(W)
+        L.call("pcs_round_weight", L.ptr(W), W.numel(), self.dt, L.ptr(out), self._stream())
+        return out
+
     def _gram(self, Y, s_, t_, B, N, C, tag=None):
         """(G, S) = (a^T a, column sums of a) for a = relu(Y*s + t) (pcs_gram)."""
         dev = Y.device
@@ -555,9 +563,10 @@ class Engine:
         # a5 > 0 (bn5's ReLU) and sums S1 = sum dz5; S2 comes from R = dz5^T a4 below.
         a5 = ys["a5"]
         Wg = P["global_feat.weight"]
+        Wg_r = self._rounded(Wg)   # the W the forward GEMM used (see pcs_round_weight)
         Hg = self._empty(1024, 1024, device=dev)
         cvec = torch.empty(1024, dtype=torch.float32, device=dev)
-        L.call("pcs_bn_fold", L.ptr(Wg), 1024, 1024, Wg.shape[1], None, L.ptr(bg), L.ptr(gg), self.dt,
+        L.call("pcs_bn_fold", L.ptr(Wg_r), 1024, 1024, Wg.shape[1], None, L.ptr(bg), L.ptr(gg), self.dt,
                None, L.ptr(cvec), L.ptr(Hg), s)
         pc5 = sv.bn["bn5"]
         cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD)
@@ -579,11 +588,11 @@ class Engine:
         self._launch("wgrad:global_feat", "pcs_gram", L.ptr(a5), None if raw else L.ptr(ones),
                      None if raw else L.ptr(zeros), B, N, 1024, self.dt, sps.value, L.ptr(ws), L.ptr(gram),
                      L.ptr(colsum), s)
-        self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg),
+        self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg_r),
                      Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(a5),
                      L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.dt, None, None,
                      L.ptr(G("global_feat.weight")), 1024, s)
-        keepalive.append((Hg, cvec, ones, zeros, gram, colsum, ws))
+        keepalive.append((Hg, cvec, ones, zeros, gram, colsum, ws, Wg_r))
 
         # conv5 (128 -> 1024): R = dz5^T a4 gives bn5's S2 (y5 = a4 W5^T is not stored) and
         # the alpha-term of dW5; then the folded input gradient and the Gram-form dW5:
@@ -598,10 +607,11 @@ class Engine:
         bn_bwd("bn5", "conv5", st5, cps5)
         al5, be5, ga5 = coefs["bn5"]
         W5 = P["conv5.weight"]
+        W5_r = self._rounded(W5)
         ws_t = self._empty(128, 1024, device=dev)
         c5 = torch.empty(128, dtype=torch.float32, device=dev)
         h4 = self._empty(128, 128, device=dev)
-        L.call("pcs_bn_fold", L.ptr(W5), 1024, 128, 128, L.ptr(al5), L.ptr(be5), L.ptr(ga5), self.dt,
+        L.call("pcs_bn_fold", L.ptr(W5_r), 1024, 128, 128, L.ptr(al5), L.ptr(be5), L.ptr(ga5), self.dt,
                L.ptr(ws_t), L.ptr(c5), L.ptr(h4), s)
         pbuf = self._empty(M, 128, device=dev)
         self._gemm(B, N, 1024, 128, L.PRO_RAW, L.EPI_FWD, dz5, ws_t, pbuf, bias=c5, tag="dgrad:conv5")
@@ -612,10 +622,10 @@ class Engine:
                    erstd=pc4.rstd, addend=pbuf, stats=st, tag="dgrad2:conv5")
         g4, s4, ws4 = sv.gram4 if sv.gram4 is not None else \
             self._gram(ys["conv4"], pc4.scale, pc4.shift, B, N, 128, tag="gram:conv4")
-        self._launch("wgrad_asm:conv5", "pcs_gram_wgrad", L.ptr(g4), L.ptr(s4), L.ptr(W5), 128, L.ptr(be5),
+        self._launch("wgrad_asm:conv5", "pcs_gram_wgrad", L.ptr(g4), L.ptr(s4), L.ptr(W5_r), 128, L.ptr(be5),
                      L.ptr(ga5), None, None, None, None, None, B, 1024, 128, self.dt, L.ptr(r5), L.ptr(al5),
                      L.ptr(G("conv5.weight")), 128, s)
-        keepalive.append((ws_t, c5, h4, pbuf, r5, g4, s4, ws4))
+        keepalive.append((ws_t, c5, h4, pbuf, r5, g4, s4, ws4, W5_r))
         bn_bwd("bn4", "conv4", st, cps4)
         dz4 = bufA
         st, cps = dgrad_wgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3", bufB)
