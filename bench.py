@@ -168,10 +168,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL ("nccl") is the data-parallel backend; PCS_DIST_BACKEND=gloo rehearses the N>1
+    # code path with several ranks sharing the GPUs a box has (device = local rank mod count)
+    backend = os.environ.get("PCS_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     B, G, C = args.scenes, args.grid, args.classes
     rb = None
