@@ -163,7 +163,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     }
   }
   if (tid < 2) runn[tid] = 0.f;
-  int nsp = 0;
+  int nsp = 0, sp_next = 0;   // sparse (DGRAD): max-pool rows, first one not yet passed
   if (sparse) {   // the scene's max-pool rows sorted by row (rank sort; staging LDS is free here)
     nsp = a.pool_c;
     int *tr = reinterpret_cast<int *>(lds);
@@ -447,13 +447,10 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         run_n += (float)nvw;
       }
     } else {   // MODE_DGRAD
-      if (sparse) {   // the tile's max-pool rows (rare): first entry >= rb by binary search
-        int lo = 0, hi = nsp;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if ((int64_t)spi[mid] < rb) lo = mid + 1; else hi = mid;
-        }
-        for (int p = lo; p < nsp && (int64_t)spi[p] < rb + valid; ++p) {
+      if (sparse) {   // the tile's max-pool rows (rare): tiles ascend, so a running pointer
+        while (sp_next < nsp && (int64_t)spi[sp_next] < rb) ++sp_next;
+        int p = sp_next;
+        for (; p < nsp && (int64_t)spi[p] < rb + valid; ++p) {
           const int m = (int)((int64_t)spi[p] - rb) - wm * 128;   // row within this wave's half
           if (m < 0 || m >= 128 || (m & 15) != lr) continue;
           const float w = spc[p];
@@ -476,34 +473,57 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       }
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
       const uint32_t *mrow = mbits + ((qs / nks) & 1) * 2048 + wn * 2;
-      uint2 mw[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) mw[i] = *reinterpret_cast<const uint2 *>(mrow + (wm * 128 + i * 16 + lr) * 8);
-      float S1 = 0.f;
       const bool full = valid == BM;   // uniform: only a scene's last tile is partial
+      float s1[4][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float s1[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const bool ok = full || ((rowok >> i) & 1u);
-          const uint32_t word = (j < 2 ? mw[i].x : mw[i].y) >> ((j & 1) * 16 + 4 * lg);
+        for (int r = 0; r < 4; ++r) s1[j][r] = 0.f;
+      // Stores widened to 16 B (cdna_hip_programming.md T21 with v_permlane16_swap): a lane
+      // holds 4 columns (8 B) of tile j; swapping tile j with tile j+1 between lane groups
+      // 2h and 2h+1 leaves each lane 8 consecutive columns of tile j + (lg & 1), so every
+      // store instruction writes 16 rows x 64 contiguous bytes instead of 16 x 32.
+      const int scol = n0 + wn * 64 + 16 * (lg & 1) + 8 * (lg >> 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bool ok = full || ((rowok >> i) & 1u);
+        const uint2 mw = *reinterpret_cast<const uint2 *>(mrow + (wm * 128 + i * 16 + lr) * 8);
+        uint32_t pk[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t word = (j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg);
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = ((word >> r) & 1u) ? acc[i][j][r] : 0.f;
-            s1[r] += ok ? v[r] : 0.f;
+            s1[j][r] += ok ? v[r] : 0.f;
           }
-          if (ok)
-            *reinterpret_cast<uint2 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + n0 + wn * 64 + j * 16 + 4 * lg) =
-                make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+          pk[j][0] = pack2bf(v[0], v[1]);
+          pk[j][1] = pack2bf(v[2], v[3]);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s1[r] = row_sum(s1[r]);
-          if (lr == j * 4 + r) S1 = s1[r];
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(pk[2 * q][h], pk[2 * q + 1][h], false, false);
+            pk[2 * q][h] = sw[0];
+            pk[2 * q + 1][h] = sw[1];
+          }
+#ifndef PCS_GLDS_NOSTORE
+          if (ok)
+            *reinterpret_cast<u32x4 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + scol + 32 * q) =
+                mk_u32x4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
+#endif
         }
       }
+      float S1 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = row_sum(s1[j][r]);
+          if (lr == j * 4 + r) S1 = t;
+        }
       if (do_stats) run[cme].x += S1;
       // The stores count in vmcnt but are not waited for here: the next counted wait
       // (vmcnt(10), phase 1) only relies on the LOADS completing in order among themselves
