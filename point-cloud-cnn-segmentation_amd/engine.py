@@ -255,6 +255,7 @@ class Engine:
         x = x.contiguous().float()
         sv = Saved(B=B, N=N, train=train) if saved is None else saved
         sv.B, sv.N, sv.train, sv.x = B, N, train, x
+        sv.gram4 = None   # (a reused Saved must not carry the previous pass's Gram)
         sv.wc = wc = self.cast_weights(P)
         T = self.tdt
 
