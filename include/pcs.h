@@ -431,6 +431,37 @@ int pcs_pad_scatter(const float *points, const void *labels, int32_t label_bytes
  */
 int pcs_round_weight(const float *W, int64_t n, int32_t dtype, float *out, pcs_stream_t stream);
 
+/*
+ * Point -> voxel path (north-star voxel vocabulary; build-defined, the
+ * reference has no voxelisation: parity is against oracle/voxel_oracle.py, not the reference).
+ * Voxel id of a point: ix = clamp(floor((x - lo_x) / (hi_x - lo_x) * G), 0, G-1) (fp32, in this
+ * order), likewise iy, iz; id = (ix * G + iy) * G + iz.  points: fp32 [T, 4] (x, y, z, e).
+ */
+int pcs_voxel_ids(const float *points, int64_t T, int32_t grid, float lo_x, float lo_y, float lo_z,
+                  float hi_x, float hi_y, float hi_z, int64_t *ids, pcs_stream_t stream);
+/*
+ * Occupied-voxel scatter of a CSR batch (offsets [num_scenes+1], device): one voxel per
+ * distinct (scene, voxel id), ordered scene-major then by id.  vox_points[v] = (mean x, mean y,
+ * mean z, sum e) of its points (fp32 sums in point order), vox_labels[v] = most frequent label
+ * (ties: smaller; labels < 0 ignored; -1 when none; labels may be NULL), vox_counts[v] = points,
+ * vox_offsets [num_scenes+1] = voxel CSR, *num_voxels = V (device scalar), voxel_of_point[p] =
+ * p's voxel (the gather back to points).  Output capacities: T voxels.  Deterministic: stable
+ * radix sort of 64-bit keys + flag scan; integer outputs are bit-exact with the oracle.
+ */
+int64_t pcs_voxelize_workspace(int64_t T);   /* bytes */
+int pcs_voxelize(const float *points, const int64_t *labels, const int64_t *offsets, int64_t num_scenes,
+                 int64_t T, int32_t grid, float lo_x, float lo_y, float lo_z, float hi_x, float hi_y,
+                 float hi_z, int32_t num_classes, void *workspace, int64_t workspace_bytes,
+                 int64_t *voxel_of_point, float *vox_points, int64_t *vox_labels, int64_t *vox_counts,
+                 int64_t *vox_offsets, int64_t *num_voxels, pcs_stream_t stream);
+/* out[p] = row of p's voxel in a padded [num_scenes, scene_rows] voxel batch
+ * (b * scene_rows + voxel_of_point[p] - vox_offsets[b]) */
+int pcs_voxel_padded_index(const int64_t *voxel_of_point, int64_t T, const int64_t *vox_offsets,
+                           int64_t num_scenes, int64_t scene_rows, int64_t *out, pcs_stream_t stream);
+/* dst[r, :] = src[idx[r], 0:C] (row stride ld_src): per-voxel outputs back to their points */
+int pcs_gather_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t n, int32_t C,
+                    float *dst, pcs_stream_t stream);
+
 /* Build-time identification and error string. */
 int pcs_abi_version(void);
 const char *pcs_last_error(void);

@@ -27,6 +27,8 @@ _LAZY = {
     "PointCloudDataset": ("data", "PointCloudDataset"),
     "pad_on_device": ("loader", "pad_on_device"),
     "DevicePrefetcher": ("loader", "DevicePrefetcher"),
+    "voxelize": ("voxel", "voxelize"),
+    "voxel_ids": ("voxel", "voxel_ids"),
 }
 
 
@@ -35,7 +37,7 @@ def __getattr__(name):
         import importlib
         mod, attr = _LAZY[name]
         return getattr(importlib.import_module(f"{__name__}.{mod}"), attr)
-    if name in ("data", "model", "optim", "train", "engine", "metrics", "checkpoint", "loader"):
+    if name in ("data", "model", "optim", "train", "engine", "metrics", "checkpoint", "loader", "voxel"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
     raise AttributeError(name)

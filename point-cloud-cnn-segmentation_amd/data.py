@@ -266,3 +266,21 @@ def occupied_clouds(seed, num_scenes, grid=256, occupancy=0.02, jitter=0.1, num_
     base = occupancy * grid ** 3
     n = [int(base * rng.uniform(1 - jitter, 1 + jitter)) for _ in range(num_scenes)]
     return [_scene(rng, grid, k, num_classes, dense=False) for k in n]
+
+
+def jittered_clouds(seed, num_scenes, grid=256, occupancy=0.01, per_voxel=4, num_classes=2, noise=0.2):
+    """Raw-hit clouds for the voxel path (pcs_amd.voxel): occupied_clouds' lattice cells, each
+    repeated 1..per_voxel times with the points jittered inside their cell, fresh e ~ Exp(1),
+    and a fraction ``noise`` of labels redrawn from {-1, 0, .., C-1} (so voxels mix labels)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 7919))
+    out = []
+    for p, l in occupied_clouds(seed, num_scenes, grid=grid, occupancy=occupancy, num_classes=num_classes):
+        reps = rng.integers(1, per_voxel + 1, size=len(p))
+        q = np.repeat(p, reps, axis=0)
+        q[:, :3] += rng.uniform(-0.49, 0.49, size=(len(q), 3)).astype(np.float32) * (2.0 / grid)
+        q[:, 3] = rng.exponential(size=len(q)).astype(np.float32)
+        lab = np.repeat(l, reps)
+        flip = rng.random(len(lab)) < noise
+        lab[flip] = rng.integers(-1, num_classes, size=int(flip.sum()))
+        out.append((q.astype(np.float32), lab.astype(np.int64)))
+    return out
