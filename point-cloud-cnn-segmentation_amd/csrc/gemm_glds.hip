@@ -148,6 +148,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 
   // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first glds)
   const bool do_stats = a.stats != nullptr;
+  const bool has_bias = a.bias != nullptr;
   const bool do_pool = MODE == MODE_FWD && a.pool != nullptr;
   const bool sparse = MODE == MODE_DGRAD && a.pool_w != nullptr;
   if (tid < BN) {
@@ -346,17 +347,20 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     const int valid = (int)pcs_min64(BM, scene_end - rb);
     const int nvw = max(0, min(128, valid - wm * 128));   // valid rows of this wave's half
     // lane's columns c(j, r) = wn*64 + j*16 + 4*lg + r; rows m(i) = wm*128 + i*16 + lr
+    if (has_bias) {   // uniform; global_feat's forward has none (its bias only shifts bn_global's mean)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 bb = *reinterpret_cast<const float4 *>(lbias + wn * 64 + j * 16 + 4 * lg);
+      for (int j = 0; j < 4; ++j) {
+        const float4 bb = *reinterpret_cast<const float4 *>(lbias + wn * 64 + j * 16 + 4 * lg);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
+        for (int i = 0; i < 8; ++i) {
+          acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
+        }
       }
     }
     uint32_t rowok = 0;   // bit i: row m(i) is a row of the scene
 #pragma unroll
     for (int i = 0; i < 8; ++i) rowok |= (uint32_t)(wm * 128 + i * 16 + lr < valid) << i;
+    const bool tile_full = valid == BM;   // uniform: only a scene's last tile is partial
 
     // after the 16-lane row reductions every lane of a row group holds its group's 16 column
     // results; lane lr then owns column e = lr of its group for the LDS bookkeeping
@@ -376,14 +380,25 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
               s1[r] = 0.f;
               s2[r] = 0.f;
             }
+            if (tile_full) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              if ((rowok >> i) & 1u) {
+              for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   const float d = acc[i][j][r] - sh[r];
                   s1[r] += d;
                   s2[r] = fmaf(d, d, s2[r]);
+                }
+            } else {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                if ((rowok >> i) & 1u) {
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    const float d = acc[i][j][r] - sh[r];
+                    s1[r] += d;
+                    s2[r] = fmaf(d, d, s2[r]);
+                  }
                 }
               }
             }
@@ -413,15 +428,17 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               sg[r] = lsgn[wn * 64 + j * 16 + 4 * lg + r];
-              float mx = -__builtin_huge_valf(), mn = __builtin_huge_valf();
+              // max of sg * y over the lane's rows (= max y, or -min y where bn_global's scale < 0)
+              float mx = -__builtin_huge_valf();
+              if (tile_full) {
 #pragma unroll
-              for (int i = 0; i < 8; ++i) {
-                if ((rowok >> i) & 1u) {
-                  mx = fmaxf(mx, acc[i][j][r]);
-                  mn = fminf(mn, acc[i][j][r]);
-                }
+                for (int i = 0; i < 8; ++i) mx = fmaxf(mx, sg[r] * acc[i][j][r]);
+              } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                  if ((rowok >> i) & 1u) mx = fmaxf(mx, sg[r] * acc[i][j][r]);
               }
-              vx[r] = row_max(sg[r] > 0.f ? mx : -mn);
+              vx[r] = row_max(mx);
               if (lr == j * 4 + r) mine = vx[r];
             }
             const bool upd = (lr >> 2) == j && mine > cur;
