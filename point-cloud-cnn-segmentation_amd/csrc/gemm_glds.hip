@@ -526,11 +526,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
             pk[2 * q][h] = sw[0];
             pk[2 * q + 1][h] = sw[1];
           }
-#ifndef PCS_GLDS_NOSTORE
           if (ok)
             *reinterpret_cast<u32x4 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + scol + 32 * q) =
                 mk_u32x4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
-#endif
         }
       }
       float S1 = 0.f;
