@@ -148,7 +148,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 
   // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first glds)
   const bool do_stats = a.stats != nullptr;
-  const bool has_bias = a.bias != nullptr;
   const bool do_pool = MODE == MODE_FWD && a.pool != nullptr;
   const bool sparse = MODE == MODE_DGRAD && a.pool_w != nullptr;
   if (tid < BN) {
@@ -265,11 +264,18 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     reinterpret_cast<uint16_t *>(mbits + par * 2048 + t * 8 + kq * 2)[h] = (uint16_t)w;
   };
 
+  // accumulators start at the bias (zero without one): the epilogue needs no bias pass
+  // (re-read from LDS at each reset rather than held in 16 VGPRs)
+  auto bias_init = [&](f32x4 (&ac)[8][4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 bb = *reinterpret_cast<const f32x4 *>(lbias + wn * 64 + j * 16 + 4 * lg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ac[i][j] = bb;
+    }
+  };
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bias_init(acc);
   auto mfma_quad = [&](int i0, int j0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -347,16 +353,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     const int valid = (int)pcs_min64(BM, scene_end - rb);
     const int nvw = max(0, min(128, valid - wm * 128));   // valid rows of this wave's half
     // lane's columns c(j, r) = wn*64 + j*16 + 4*lg + r; rows m(i) = wm*128 + i*16 + lr
-    if (has_bias) {   // uniform; global_feat's forward has none (its bias only shifts bn_global's mean)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 bb = *reinterpret_cast<const float4 *>(lbias + wn * 64 + j * 16 + 4 * lg);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          acc[i][j][0] += bb.x; acc[i][j][1] += bb.y; acc[i][j][2] += bb.z; acc[i][j][3] += bb.w;
-        }
-      }
-    }
     uint32_t rowok = 0;   // bit i: row m(i) is a row of the scene
 #pragma unroll
     for (int i = 0; i < 8; ++i) rowok |= (uint32_t)(wm * 128 + i * 16 + lr < valid) << i;
@@ -545,10 +541,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       // (pending stores can only make it wait longer), so they drain behind phase 1's reads.
     }
 
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bias_init(acc);
   }
 
   if (wm == 0) barrier_raw();   // re-align the halves (matching the stagger above)
