@@ -128,7 +128,8 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   float run_n = 0.f;   // rows merged into the running statistics so far (uniform)
 
   const int slot = tid & 7, srow = tid >> 3;  // staging: rows srow + 64*i, fixed k-slot
-  const int ecc = tid % CPR, er0 = tid / CPR, ecol = n0 + ecc * EPC;
+  const int ecc_ = tid % CPR, er0_ = tid / CPR;
+  const int ecc = ecc_, er0 = er0_, ecol = n0 + ecc * EPC;
   const int lrow = lane & 15, lcol = 4 * (lane >> 4);
 
   u32x4 ra[4], ra2[4], rb[4];
@@ -373,6 +374,11 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
         }
       }
     } else if constexpr (EPI == PCS_EPI_DGRAD) {
+      // per-thread indices made opaque per tile: addresses derived from them are recomputed
+      // here instead of hoisted out of the tile loop and spilled across the k-loop
+      int ecc = ecc_, er0 = er0_;
+      asm volatile("" : "+v"(ecc), "+v"(er0));
+      const int ecol = n0 + ecc * EPC;
       const bf16_t *Ypg = reinterpret_cast<const bf16_t *>(a.Yp);
       const bf16_t *Addg = reinterpret_cast<const bf16_t *>(a.addend);
       float es[EPC], et[EPC];
