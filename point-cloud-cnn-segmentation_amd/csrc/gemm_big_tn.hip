@@ -47,13 +47,21 @@ PCS_DEV void tn_load(const bf16_t *__restrict__ dZ, const bf16_t *__restrict__ Y
                      const bf16_t *__restrict__ Xg, const uint8_t *__restrict__ xmask, int64_t rbase,
                      int64_t rlast, int Cout, int Cin, int an, int bk, int r0, u32x4 (&rz)[4],
                      u32x4 (&ry)[4], u32x4 (&rx)[4], uint32_t (&mk)[4]) {
+  // uniform (SGPR) step bases + 32-bit per-thread offsets (saddr + voffset loads): 64-bit
+  // per-row addresses for three operands cost 24 VGPRs and spilled at the k-loop's peak
+  const int lim = (int)pcs_min64(rlast - 1 - rbase, MS - 1);   // last valid row of the step
+  const char *zb = reinterpret_cast<const char *>(dZ + rbase * Cout);
+  const char *yb = reinterpret_cast<const char *>(Yg + rbase * Cout);
+  const char *xb = reinterpret_cast<const char *>(Xg + rbase * Cin);
+  const uint8_t *mb = MASK ? xmask + ((rbase * Cin) >> 3) : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t r = rbase + r0 + 16 * i < rlast ? rbase + r0 + 16 * i : rlast - 1;
-    if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(dZ + r * Cout + an);
-    ry[i] = *reinterpret_cast<const u32x4 *>(Yg + r * Cout + an);
-    rx[i] = *reinterpret_cast<const u32x4 *>(Xg + r * Cin + bk);
-    if constexpr (MASK) mk[i] = xmask[(r * Cin + bk) >> 3];
+    const int rl = min(r0 + 16 * i, lim);
+    const uint32_t oy = (uint32_t)(rl * Cout + an), ox = (uint32_t)(rl * Cin + bk);
+    if constexpr (DYMODE == PCS_PRO_BWD) rz[i] = *reinterpret_cast<const u32x4 *>(zb + 2 * oy);
+    ry[i] = *reinterpret_cast<const u32x4 *>(yb + 2 * oy);
+    rx[i] = *reinterpret_cast<const u32x4 *>(xb + 2 * ox);
+    if constexpr (MASK) mk[i] = mb[ox >> 3];
   }
 }
 
@@ -88,45 +96,54 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_
     }
     return;
   }
-  float ca[8], cb[8], cg[8], xs[8], xt[8];
-  int am[8];
+  // dy rows first, then x rows: only one operand's coefficients are live at a time (the
+  // k-loop runs at the 256-VGPR limit)
   const int c8 = cc * 8;
-  lds8(cf + c8, ca);
-  lds8(cf + 256 + c8, cb);
-  lds8(cf + 512 + c8, cg);
-  if constexpr (DYMODE == PCS_PRO_BWD_POOL) {
-    const int4 i0 = *reinterpret_cast<const int4 *>(cf + 768 + c8);
-    const int4 i1 = *reinterpret_cast<const int4 *>(cf + 768 + c8 + 4);
-    am[0] = i0.x; am[1] = i0.y; am[2] = i0.z; am[3] = i0.w;
-    am[4] = i1.x; am[5] = i1.y; am[6] = i1.z; am[7] = i1.w;
+  {
+    float ca[8], cb[8], cg[8];
+    int am[8];
+    lds8(cf + c8, ca);
+    lds8(cf + 256 + c8, cb);
+    lds8(cf + 512 + c8, cg);
+    if constexpr (DYMODE == PCS_PRO_BWD_POOL) {
+      const int4 i0 = *reinterpret_cast<const int4 *>(cf + 768 + c8);
+      const int4 i1 = *reinterpret_cast<const int4 *>(cf + 768 + c8 + 4);
+      am[0] = i0.x; am[1] = i0.y; am[2] = i0.z; am[3] = i0.w;
+      am[4] = i1.x; am[5] = i1.y; am[6] = i1.z; am[7] = i1.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = r0 + 16 * i;
+      const int64_t r = rbase + rl;
+      float y[8], v[8];
+      unpack_chunk(ry[i], y);
+      if constexpr (DYMODE == PCS_PRO_BWD) {
+        unpack_chunk(rz[i], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+      } else if constexpr (DYMODE == PCS_PRO_BNRELU) {   // Gram: (beta, gamma) slots hold (s, t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(y[e], cb[e], cg[e]), 0.f);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = fmaf(cg[e], y[e], cb[e]);
+          if (am[e] == (int)r) x += ca[e];
+          v[e] = x;
+        }
+      }
+      u32x4 o = pack_chunk(v);
+      if (r >= rlast) o = mk_u32x4(0, 0, 0, 0);
+      *reinterpret_cast<u32x4 *>(tA + prow(rl) * ROWB + cc * 16) = o;
+    }
   }
+  float xs[8], xt[8];
   lds8(cf + 1024 + c8, xs);
   lds8(cf + 1280 + c8, xt);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rl = r0 + 16 * i;
-    const int64_t r = rbase + rl;
-    const bool ok = r < rlast;
-    float y[8], v[8];
-    unpack_chunk(ry[i], y);
-    if constexpr (DYMODE == PCS_PRO_BWD) {
-      unpack_chunk(rz[i], v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
-    } else if constexpr (DYMODE == PCS_PRO_BNRELU) {   // Gram: (beta, gamma) slots hold (s, t)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(y[e], cb[e], cg[e]), 0.f);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = fmaf(cg[e], y[e], cb[e]);
-        if (am[e] == (int)r) x += ca[e];
-        v[e] = x;
-      }
-    }
-    u32x4 o = pack_chunk(v);
-    if (!ok) o = mk_u32x4(0, 0, 0, 0);
-    *reinterpret_cast<u32x4 *>(tA + prow(rl) * ROWB + cc * 16) = o;
+    const bool ok = rbase + rl < rlast;
     float w[8];
     unpack_chunk(rx[i], w);
 #pragma unroll
