@@ -22,7 +22,7 @@ def timeit(fn, reps=5):
     return st.elapsed_time(en) / reps
 
 
-def run(name, B, N, K, Nc, stats, store, flags=0):
+def run(name, B, N, K, Nc, stats, store, flags=0, epi=None):
     dev = torch.device("cuda")
     lib = L.load()
     M = B * N
@@ -30,12 +30,15 @@ def run(name, B, N, K, Nc, stats, store, flags=0):
     W = (torch.randn(Nc, K, device=dev) * 0.03).to(torch.bfloat16)
     C = torch.empty(M, Nc, device=dev, dtype=torch.bfloat16)
     s, t = torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev) * 0.1
+    s2, t2 = torch.rand(Nc, device=dev) + 0.5, torch.randn(Nc, device=dev) * 0.1
     a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=Nc, dtype=L.BF16, prologue=L.PRO_BNRELU,
-                   epilogue=L.EPI_FWD, chunks_per_scene=0, flags=flags)
+                   epilogue=L.EPI_FWD if epi is None else epi, chunks_per_scene=0, flags=flags)
     lib.pcs_gemm_geometry(ct.byref(a))
     st = torch.empty(B * a.chunks_per_scene, Nc, 2, device=dev)
     a.A, a.W, a.C, a.pa, a.pb = A.data_ptr(), W.data_ptr(), C.data_ptr() if store else None, L.ptr(s), L.ptr(t)
     a.stats = L.ptr(st) if stats else None
+    if epi == L.EPI_BNRELU:
+        a.es, a.et = L.ptr(s2), L.ptr(t2)
     ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
     gb = M * (K + (Nc if store else 0)) * 2 / 1e9
     print(f"{name:34s} K={K:5d} N={Nc:5d} stats={int(stats)} store={int(store)} gen={flags}: {ms:7.3f} ms "
@@ -45,6 +48,7 @@ def run(name, B, N, K, Nc, stats, store, flags=0):
 
 def main():
     B, N = 4, 128 ** 3
+    run("fwd bnrelu epilogue (conv5)", B, N, 128, 1024, 0, 1, epi=L.EPI_BNRELU)
     for K, Nc in [(128, 1024), (512, 256), (64, 512)]:
         for stats, store in [(1, 1), (0, 1), (0, 0)]:
             run("fwd", B, N, K, Nc, stats, store)
