@@ -19,7 +19,7 @@
 #include "common.h"
 
 #ifndef PCS_DGRAD_BATCH
-#define PCS_DGRAD_BATCH 4   // DGRAD epilogue: rows of Yp (and mask / addend) loaded per batch
+#define PCS_DGRAD_BATCH 16  // DGRAD epilogue: rows of Yp (and mask / addend) loaded per batch (all 16)
 #endif
 
 namespace {
