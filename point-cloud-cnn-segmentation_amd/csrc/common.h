@@ -22,6 +22,18 @@ PCS_DEV u32x4 mk_u32x4(unsigned a, unsigned b, unsigned c, unsigned d) {
   return v;
 }
 
+#ifndef PCS_NT_STORE
+#define PCS_NT_STORE 1   // streamed GEMM outputs stored non-temporal (nt): they outgrow L2 / MALL
+#endif
+// one 16-B store of a streamed activation / gradient row chunk (read back only by a later kernel)
+PCS_DEV void st16(void *p, u32x4 v) {
+#if PCS_NT_STORE
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+#else
+  *reinterpret_cast<u32x4 *>(p) = v;
+#endif
+}
+
 
 // ---------------------------------------------------------------------------------------
 // element traits: T = float (parity path, f32 MFMA) or bf16_t (bench path, bf16 MFMA)

@@ -194,8 +194,8 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
     {
       const int r = tid >> 3, ch = tid & 7;   // 64 rows x 8 chunks of 16 B
       if (m0 + r < hi)
-        *reinterpret_cast<u32x4 *>(dX + (sbase + m0 + r) * CIN + ch * 8) =
-            *reinterpret_cast<const u32x4 *>(lds + OFF_OUT + r * CIN * 2 + ch * 16);
+        st16(dX + (sbase + m0 + r) * CIN + ch * 8,
+             *reinterpret_cast<const u32x4 *>(lds + OFF_OUT + r * CIN * 2 + ch * 16));
     }
     if (st + 1 < nsteps) {
       store_step(m0 + MS);
@@ -482,8 +482,8 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     for (int i = 0; i < F::NCH_P; ++i) {
       const int q = tid + THREADS * i, rl = q / (CB / 8), cc = q % (CB / 8);
       if (m0 + rl < hi)
-        *reinterpret_cast<u32x4 *>(Cg + (sbase + m0 + rl) * CIN + n0 + cc * 8) =
-            *reinterpret_cast<const u32x4 *>(lds + F::OFF_OUT + rl * CB * 2 + cc * 16);
+        st16(Cg + (sbase + m0 + rl) * CIN + n0 + cc * 8,
+             *reinterpret_cast<const u32x4 *>(lds + F::OFF_OUT + rl * CB * 2 + cc * 16));
     }
     if (st + 1 < nsteps) {
       store_step(m0 + MS);

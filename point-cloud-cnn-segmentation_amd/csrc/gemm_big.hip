@@ -350,7 +350,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
         const int rr = er0 + RPP * p;
         if (rr < valid) {
           const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
-          if (Cg) *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) = raw;
+          if (Cg) st16(Cg + (row_base + rr) * Ncols + ecol, raw);
           if (do_stats || do_pool) {
             float v[EPC];
             unpack_chunk(raw, v);
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
               sa[e] += dz;                  // S1
               sb[e] = fmaf(dz, y[e], sb[e]);  // sum dz*y; S2 = rstd*(sum dz*y - mean*S1)
             }
-            *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) = pack_chunk(v);
+            st16(Cg + (row_base + rr) * Ncols + ecol, pack_chunk(v));
           }
         }
       }
@@ -430,8 +430,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       for (int p = 0; p < NPASS; ++p) {
         const int rr = er0 + RPP * p;
         if (rr < valid)
-          *reinterpret_cast<u32x4 *>(Cg + (row_base + rr) * Ncols + ecol) =
-              *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+          st16(Cg + (row_base + rr) * Ncols + ecol, *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16));
       }
     }
     __syncthreads();   // the C tile has been consumed

@@ -373,7 +373,7 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
             float v[EPC];
             unpack_chunk(raw, v);
             if constexpr (EPI == PCS_EPI_FWD) {
-              if (Cg) *reinterpret_cast<u32x4 *>(Cg + goff) = raw;
+              if (Cg) st16(Cg + goff, raw);
               if (a.stats) {
                 st_cnt += 1.f;
                 const float rn = 1.f / st_cnt;
@@ -422,9 +422,9 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
                 st_mean[e] += dz;                                        // S1
                 st_m2[e] = fmaf(dz, (y[e] - em[e]) * er[e], st_m2[e]);   // S2
               }
-              *reinterpret_cast<u32x4 *>(Cg + goff) = pack_chunk(v);
+              st16(Cg + goff, pack_chunk(v));
             } else {  // RAW
-              *reinterpret_cast<u32x4 *>(Cg + goff) = raw;
+              st16(Cg + goff, raw);
             }
           }
         }

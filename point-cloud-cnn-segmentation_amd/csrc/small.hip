@@ -55,7 +55,7 @@ __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int
       v[e] = acc;
     }
     const u32x4 packed = pack_chunk(v);
-    *reinterpret_cast<u32x4 *>(Cg + grow * COLS + c0) = packed;
+    st16(Cg + grow * COLS + c0, packed);
     unpack_chunk(packed, v);  // statistics of the stored (rounded) values
     cnt += 1.f;
     const float rn = 1.f / cnt;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tile
             s1[c + e] += dz;
             s2[c + e] = fmaf(dz, xh[r * HEAD_LD + ch], s2[c + e]);
           }
-          *reinterpret_cast<u32x4 *>(dZ + grow * HEAD_CIN + ch0 + c) = pack_chunk(v);
+          st16(dZ + grow * HEAD_CIN + ch0 + c, pack_chunk(v));
         }
       }
       // phase 4: dW / db partials (each weight or bias entry owned by one thread);
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, in
           float tmp[EPC];
 #pragma unroll
           for (int e = 0; e < EPC; ++e) tmp[e] = dz[k * EPC + e];
-          *reinterpret_cast<u32x4 *>(dZ + row * HEAD_CIN + ch0 + k * EPC) = pack_chunk(tmp);
+          st16(dZ + row * HEAD_CIN + ch0 + k * EPC, pack_chunk(tmp));
         }
       }
     }
