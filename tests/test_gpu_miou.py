@@ -1,0 +1,92 @@
+"""North-star mIoU parity (BASELINE north_star "mIoU within 1e-3 of reference"; SURVEY §0.4,
+§8 c): the HIP path and the reference evaluate the SAME weights on the same synthetic clouds.
+
+* device side: eval-mode forward through the C ABI, then the device confusion matrix
+  (pcs_confusion via ConfusionMeter) and pcs_amd.metrics.miou;
+* reference side: argmax of the logits the reference module itself wrote into the golden
+  fixture (tests/golden/make_golden.py), or of the fp64 numpy oracle (pinned to those
+  fixtures) on inputs no fixture covers, scored with sklearn's jaccard_score(average='macro')
+  (the reference reports sklearn metrics, P:341-346; mIoU itself is build-defined).
+
+Seeded random weights predict one class almost everywhere, which makes mIoU uninformative, so
+the main case first trains the model for a few dozen fused steps on the device (weighted CE,
+P:216) and then scores THOSE weights on both sides.  fp32 and bf16 (the bench dtype) are both
+held to 1e-3."""
+import numpy as np
+import pytest
+import torch
+
+import pointnet_oracle as orc
+from golden_util import inputs, load
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+TOL = 1e-3
+
+
+def _sk_miou(pred, lab):
+    from sklearn.metrics import jaccard_score
+    v = lab >= 0
+    return float(jaccard_score(lab[v], pred[v], average="macro"))
+
+
+def _device_miou(sd, pts, lab, C, dtype):
+    from pcs_amd.metrics import ConfusionMeter
+    from pcs_amd.model import PointNetSegmentation
+    m = PointNetSegmentation(C, compute_dtype=dtype).to(DEV)
+    m.load_state_dict({k: torch.as_tensor(np.array(v)) for k, v in sd.items()})
+    m.eval()
+    meter = ConfusionMeter(C, DEV)
+    with torch.no_grad():
+        meter.update(m(torch.from_numpy(pts).to(DEV)), torch.from_numpy(lab).to(DEV))
+    return meter.compute()["miou"]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_miou_matches_reference_golden(dtype):
+    """eval_c2_bnrand: the logits in the fixture were written by the reference module."""
+    g = load("eval_c2_bnrand")
+    sd, pts, lab, _, _ = inputs(g)
+    ref = _sk_miou(np.asarray(g["logits"]).argmax(-1).reshape(-1), lab.reshape(-1))
+    got = _device_miou(sd, pts, lab, int(g["C"]), dtype)
+    print(f"{dtype}: mIoU {got:.6f} vs reference {ref:.6f}")
+    assert abs(got - ref) <= TOL
+
+
+@pytest.fixture(scope="module")
+def trained():
+    """fp32 weights after 40 fused training steps (Adam, class-weighted CE) on seeded clouds."""
+    import pcs_amd.data as pdata
+    from pcs_amd.model import PointNetSegmentation
+    from pcs_amd.optim import FusedAdam
+    from pcs_amd.train import FusedTrainStep
+    C = 2
+    torch.manual_seed(7)
+    m = PointNetSegmentation(C).to(DEV)
+    pts, lab, _ = pdata.synthetic_batch(11, [4096] * 4, C, grid=32)
+    w = pdata.class_weights([lab[b][lab[b] >= 0] for b in range(lab.shape[0])], num_classes=C)
+    step = FusedTrainStep(m, FusedAdam(m, lr=3e-3), class_weight=w)
+    x, y = torch.from_numpy(pts).to(DEV), torch.from_numpy(lab).to(DEV)
+    for i in range(40):
+        step(x, y, seed=1000 + i)
+    torch.cuda.synchronize()
+    return C, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_miou_of_trained_weights_matches_oracle(trained, dtype):
+    """Ragged val batch (pads labelled -1 enter BN / max-pool as in collate_fn) scored with
+    the trained weights by the device path and by the fp64 oracle."""
+    import pcs_amd.data as pdata
+    C, sd = trained
+    pts, lab, _ = pdata.synthetic_batch(4242, [8192, 6000, 8192, 5000], C, grid=32)
+    logits, _ = orc.forward({k: np.asarray(v, np.float64) if v.dtype.kind == "f" else v
+                             for k, v in sd.items()}, pts, train=False)
+    pred = logits.argmax(-1).reshape(-1)
+    v = lab.reshape(-1) >= 0
+    hist = np.bincount(pred[v], minlength=C)
+    ref = _sk_miou(pred, lab.reshape(-1))
+    got = _device_miou(sd, pts, lab, C, dtype)
+    print(f"trained {dtype}: mIoU {got:.6f} vs oracle {ref:.6f}, oracle prediction histogram {hist}")
+    assert hist.min() > 0.01 * v.sum(), "training left a degenerate (one-class) predictor"
+    assert abs(got - ref) <= TOL
