@@ -38,22 +38,33 @@ LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (
 
 # bench tag -> HIP kernel symbol (as summarised from rocprofv3 in profiles/pmc_<round>.json)
 TAG_KERNEL = {
-    "wgrad:global_feat": "wgrad_big_kernel<1, false>",     # Gram a5^T a5 (upper tiles)
-    "fwd:global_feat": "gemm_glds_kernel<0>",              # LDS-DMA: BN stats + max-pool epilogue
-    "dgrad:global_feat": "gemm_glds_kernel<1>",            # LDS-DMA: folded a5 H, mask, sparse rows
+    "wgrad:global_feat": "wgrad_big_kernel<1, false, true>",   # Gram a5^T a5 (upper tiles)
+    "fwd:global_feat": "gemm_glds_kernel<0>",                  # LDS-DMA: BN stats + max-pool epilogue
+    "dgrad:global_feat": "gemm_glds_kernel<1>",                # LDS-DMA: folded a5 H, mask, sparse rows
 }
-PMC_FILE = os.path.join(REPO, "profiles", "pmc_r01.json")
 GRAM_TILE_FRACTION = 10.0 / 16.0   # upper 256-tiles of the symmetric 1024 x 1024 Gram
 
 
-def pmc_traffic(tag, dtype):
-    """HBM bytes per launch of the kernel behind ``tag`` from the committed PMC summary
-    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/profile_round.sh)."""
-    if dtype != "bf16" or tag not in TAG_KERNEL or not os.path.exists(PMC_FILE):
+def pmc_traffic(tag, dtype, workload, points):
+    """HBM bytes per launch of the kernel behind ``tag``, from a committed PMC summary
+    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/profile_round.sh) whose
+    recorded workload, dtype and points per step match this run; None when no such profile
+    exists (the number would describe a different launch)."""
+    import glob
+    sym = TAG_KERNEL.get(tag)
+    if sym is None:
         return None
-    with open(PMC_FILE) as f:
-        ent = json.load(f).get(TAG_KERNEL[tag], {})
-    return ent.get("hbm_bytes_per_launch")
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        meta = rec.get("meta") if isinstance(rec, dict) else None
+        if not meta or (meta.get("workload"), meta.get("dtype"), meta.get("points_per_step")) != \
+                (workload, dtype, points):
+            continue
+        ent = rec.get("kernels", {}).get(sym, {})
+        if "hbm_bytes_per_launch" in ent:
+            return {"bytes": ent["hbm_bytes_per_launch"], "source": os.path.relpath(path, REPO)}
+    return None
 
 
 def kernel_model(tag, M, ab):
@@ -261,20 +272,22 @@ def main():
         if mdl:
             flops, nbytes = mdl
             ai = flops / nbytes
+            tr = pmc_traffic(dom, args.dtype, args.workload, M)
             ridge = PEAK[args.dtype]["mfma"] * 1e12 / (PEAK[args.dtype]["hbm"] * 1e9)
             if ai >= ridge:
                 ach = flops / avg_s / 1e12
                 roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
                         "peak": PEAK[args.dtype]["mfma"], "unit": "TFLOP/s",
                         "frac": round(ach / PEAK[args.dtype]["mfma"], 4),
-                        "traffic": pmc_traffic(dom, args.dtype), "algorithmic_bytes": nbytes,
+                        "traffic": tr and tr["bytes"], "traffic_source": tr and tr["source"],
+                        "algorithmic_bytes": nbytes,
                         "algorithmic_flops": flops, "avg_ms": round(avg_s * 1e3, 4)}
             else:
                 ach = nbytes / avg_s / 1e9
                 roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
                         "peak": PEAK[args.dtype]["hbm"], "unit": "GB/s",
                         "frac": round(ach / PEAK[args.dtype]["hbm"], 4),
-                        "traffic": pmc_traffic(dom, args.dtype),
+                        "traffic": tr and tr["bytes"], "traffic_source": tr and tr["source"],
                         "algorithmic_bytes": nbytes, "avg_ms": round(avg_s * 1e3, 4)}
         if rank == 0:
             step_ms = el / args.steps * 1e3

@@ -15,7 +15,8 @@
 //   upper halves of every wave's rows and columns), so a region is free as soon as its last
 //   quadrant has read it: A-lo and B-lo after phase 1, B-hi after phase 2, A-hi after
 //   phase 3.  One region is restaged per phase, about four phases ahead of its use, by two
-//   glds per thread; waits are counted (vmcnt(10): five regions stay in flight) and the
+//   glds per thread; waits are counted (vmcnt(10): five regions stay in flight, fewer on the
+//   chunk's last two K-tiles, where nothing more is issued) and the
 //   barriers are raw s_barriers, so the loads stay in flight across them.  The 16-B chunks
 //   of a 128-B LDS row are XOR-swizzled by (row >> 1) & 7; glds writes LDS linearly, so the
 //   swizzle is applied to the SOURCE address and again on the ds_read_b128 side (rule 21).
@@ -196,7 +197,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     for (int h = 0; h < 2; ++h) boff[h][g] = (uint32_t)b_row(h, qrow[g]) * (uint32_t)rowbytes + cbyte[g];
   }
   auto issue = [&](int qseq, int region) {
-    if (qseq >= total) return;   // nothing left to prefetch (the counted waits stay valid)
+    if (qseq >= total) return;   // nothing left to prefetch: the loop's tail waits shrink
+                                 // to match (see the phase waits below)
     const int tl = qseq / nks, kt = qseq - tl * nks;
     char *dst = lds + (qseq & 1) * KBUF + region * REG;
     if (region < 2) {
@@ -310,7 +312,11 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     read_b(buf, 2, 0);
     if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
     issue(qs + 1, 1);
-    wait_vm<10>();
+    // every counted wait assumes the five regions issued after the one it retires are in
+    // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
+    // regions actually issued (phase 1 retires B-hi(qs): newer are A-hi(qs) and, unless qs is
+    // the last K-tile, the four regions of qs+1)
+    if (qs + 1 < total) wait_vm<10>(); else wait_vm<2>();
     wait_lgkm0();
     barrier_raw();
     __builtin_amdgcn_s_setprio(1);
@@ -320,7 +326,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 2: (lo, hi); restage A-lo of K-tile qs+2
     read_b(buf, 3, 2);
     issue(qs + 2, 0);
-    wait_vm<10>();
+    // retires A-hi(qs): newer are the four regions of qs+1 and A-lo(qs+2)
+    if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<8>(); else wait_vm<0>();
     wait_lgkm0();
     barrier_raw();
     __builtin_amdgcn_s_setprio(1);
@@ -339,7 +346,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 4: (hi, hi); restage B-hi of K-tile qs+2
     issue(qs + 2, 3);
-    wait_vm<10>();
+    // retires A-lo(qs+1), B-lo(qs+1): newer are B-hi(qs+1), A-hi(qs+1) and three of qs+2
+    if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();
     barrier_raw();
     __builtin_amdgcn_s_setprio(1);
     mfma_quad(4, 2);

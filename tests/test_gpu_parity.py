@@ -224,11 +224,21 @@ def test_cpu_input_raises():
 
 
 def test_bf16_big_kernel_matches_generic_kernel():
-    """The 256x256 wide-layer kernels (register-staged and LDS-DMA) and the generic 128-row
-    kernel compute the same bf16 GEMMs: conv1-4 and a5 agree to a few bf16 ulps; after the
-    max-pool the paths round at different points (module comments below), which train-mode
-    BN amplifies, so seg_conv1-3, the logits and the gradients are compared by norm / cosine
-    (early-layer gradients ~0.94, the same order as either path against the fp64 oracle)."""
+    """The 256x256 wide-layer kernels (LDS-DMA and register-staged) and the generic 128-row
+    kernel compute the same bf16 step.
+
+    * Two launches of the default (LDS-DMA) path on identical inputs are bitwise identical.
+    * register-staged 256x256 (FLAG_NO_GLDS) vs generic: both take global_feat's BN
+      statistics and max-pool candidates from the bf16-rounded tile, so they differ only by
+      fp32 summation order (measured r02: logits 2.8e-3, seg_conv <= 8.3e-4 norm-rel, cosine
+      >= 0.99995): logits < 1e-2, seg_conv outputs < 1e-2 norm-relative, gradient cosine
+      > 0.999 (tighter than the pre-LDS-DMA 2e-2 / 0.99).
+    * LDS-DMA vs generic: the LDS-DMA kernel takes them from its fp32 accumulators, so the
+      pooled g (and seg_conv1's per-scene bias W_g g) differ by up to one bf16 ulp per
+      channel, which train-mode BN over these two small scenes amplifies through seg_conv1-3
+      (measured r02: logits 2.49e-2, seg_conv 1.2-2.3e-2 norm-rel, cosine >= 0.934); bounds
+      are the measured values plus a stated margin: logits < 4e-2, seg_conv < 4e-2,
+      cosine > 0.92."""
     import pcs_amd._lib as L
     from pcs_amd.data import synthetic_batch
     sd = orc.init_params(3, 17, bn_affine_random=True)
@@ -237,7 +247,7 @@ def test_bf16_big_kernel_matches_generic_kernel():
     bits = _bits(masks)
     x = torch.from_numpy(pts).to(DEV)
     outs = []
-    for flags in (0, L.FLAG_GENERIC):
+    for flags in (0, 0, L.FLAG_NO_GLDS, L.FLAG_GENERIC):
         m = _model(sd, 3, dtype="bf16")
         eng = m._engine()
         eng.flags = flags
@@ -249,29 +259,36 @@ def test_bf16_big_kernel_matches_generic_kernel():
         outs.append((out.detach().float().cpu().numpy(),
                      {k: v.float().cpu().numpy() for k, v in sv.ys.items()},
                      {n: p.grad.detach().cpu().numpy() for n, p in m.named_parameters()}))
-    (o1, y1, g1), (o2, y2, g2) = outs
+    (o1, y1, g1), (o1b, y1b, g1b), (o3, y3, g3), (o2, y2, g2) = outs
+    # two launches of the wide-layer path on identical inputs are bitwise identical (no
+    # atomics on float data; a pipeline race would show up here first)
+    assert np.array_equal(o1, o1b)
     for k in y1:
-        d = np.abs(y1[k] - y2[k])
-        # after the max-pool the two paths differ by more than rounding order: the LDS-DMA
-        # global_feat kernel takes the pool candidates and BN statistics from its fp32
-        # accumulators, the generic kernel from the bf16-rounded tile, so the pooled g (and
-        # seg_conv1's per-scene bias W_g g) differ by up to one bf16 ulp per channel
-        # and train-mode BN amplifies that through seg_conv1-3: compare those by norm
-        if k.startswith("seg_conv"):
-            nrm = float(np.linalg.norm(y1[k] - y2[k]) / np.linalg.norm(y2[k]))
-            print(k, "norm-rel", nrm)
-            assert nrm < 5e-2, (k, nrm)
-        else:
-            assert d.max() <= 4e-2 * np.abs(y2[k]).max() and d.mean() <= 2e-3 * np.abs(y2[k]).mean() + 1e-6, \
-                (k, float(d.max()), float(d.mean()), float(np.abs(y2[k]).mean()))
-    print("logits", rel_err(o1, o2))
-    assert rel_err(o1, o2) < 1e-1
+        assert np.array_equal(y1[k], y1b[k]), k
     for n in g1:
-        # BN-cancelled conv biases are noise; bn_global.bias is nonzero only through pooled
-        # features whose relu sits at ~0 (a one-ulp bf16 difference decides which), so it
-        # is not comparable between two accumulation orders.
-        if (n.endswith(".bias") and not n.startswith(("bn", "seg_conv4"))) or n == "bn_global.bias":
-            continue
-        cs = (g1[n].ravel() @ g2[n].ravel()) / (np.linalg.norm(g1[n]) * np.linalg.norm(g2[n]) + 1e-30)
-        print(n, "cos", cs)
-        assert cs > 0.9 or np.linalg.norm(g2[n]) < 1e-9, (n, cs)
+        assert np.array_equal(g1[n], g1b[n]), n
+
+    def compare(tag, oa, ya, ga, ob, yb, gb, seg_tol, logit_tol, cos_min):
+        for k in ya:
+            d = np.abs(ya[k] - yb[k])
+            if k.startswith("seg_conv"):
+                nrm = float(np.linalg.norm(ya[k] - yb[k]) / np.linalg.norm(yb[k]))
+                print(tag, k, "norm-rel", nrm)
+                assert nrm < seg_tol, (tag, k, nrm)
+            else:   # before the pool: a few bf16 ulps
+                assert d.max() <= 4e-2 * np.abs(yb[k]).max() and d.mean() <= 2e-3 * np.abs(yb[k]).mean() + 1e-6, \
+                    (tag, k, float(d.max()), float(d.mean()), float(np.abs(yb[k]).mean()))
+        print(tag, "logits", rel_err(oa, ob))
+        assert rel_err(oa, ob) < logit_tol, tag
+        for n in ga:
+            # BN-cancelled conv biases are noise; bn_global.bias is nonzero only through pooled
+            # features whose relu sits at ~0 (a one-ulp bf16 difference decides which), so it
+            # is not comparable between two accumulation orders.
+            if (n.endswith(".bias") and not n.startswith(("bn", "seg_conv4"))) or n == "bn_global.bias":
+                continue
+            cs = (ga[n].ravel() @ gb[n].ravel()) / (np.linalg.norm(ga[n]) * np.linalg.norm(gb[n]) + 1e-30)
+            print(tag, n, "cos", cs)
+            assert cs > cos_min or np.linalg.norm(gb[n]) < 1e-9, (tag, n, cs)
+
+    compare("noglds-vs-generic", o3, y3, g3, o2, y2, g2, 1e-2, 1e-2, 0.999)
+    compare("glds-vs-generic", o1, y1, g1, o2, y2, g2, 4e-2, 4e-2, 0.92)
