@@ -113,8 +113,9 @@ typedef struct {
 int64_t pcs_gemm_geometry(pcs_gemm_args *args);
 /* Launch the GEMM. */
 int pcs_gemm(const pcs_gemm_args *args, pcs_stream_t stream);
-/* conv1 (Cin = input_dim = 4, P:70, P:106) forward: A = points f32 [M,4] (RAW), W f32
- * [64,4]; epilogue PCS_EPI_FWD semantics (C in dtype, stats).  Same geometry rules. */
+/* conv1 (Cin = K = input_dim, 1..8; the reference's points carry 4, P:70, P:106) forward:
+ * A = points f32 [M,K] (RAW), W f32 [64,K]; epilogue PCS_EPI_FWD semantics (C in dtype,
+ * stats).  Same geometry rules. */
 int pcs_conv1_fwd(const pcs_gemm_args *args, pcs_stream_t stream);
 
 /*
@@ -145,7 +146,8 @@ typedef struct {
 
 int64_t pcs_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_per_scene */
 int pcs_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream);
-int pcs_conv1_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream); /* X = points f32 */
+int pcs_conv1_wgrad(const pcs_wgrad_args *args, pcs_stream_t stream); /* X = points f32 [M, Cin], Cin 1..8;
+                                                                          partial: B*splits*64*Cin f32 */
 
 /*
  * Fused input + weight gradient of seg_conv1's local half (bf16; Cout 512, Cin 64):
@@ -278,7 +280,7 @@ enum { PCS_HEAD_FWD = 0, PCS_HEAD_CE = 1, PCS_HEAD_BWD = 2 };
 typedef struct {
   int64_t num_scenes, scene_rows;
   int32_t Cin;          /* 128 */
-  int32_t num_classes;  /* C <= 16 */
+  int32_t num_classes;  /* 1 <= C <= 64 */
   int32_t dtype, mode;
   int32_t chunks_per_scene; /* 0 = auto */
   const void *Y;        /* [M, Cin] y_seg3 */
@@ -405,9 +407,11 @@ int pcs_cast_weight(const float *W, int64_t rows, int64_t cols, int64_t ldw, int
 
 /*
  * torch.optim.Adam step with L2 (coupled) weight decay, amsgrad=False (P:217, P:255) on
- * flat fp32 buffers.  g_eff = g * (*grad_scale if non-NULL) + wd * p.
+ * flat fp32 buffers.  g_eff = g * (*grad_scale if non-NULL) + wd * p; with a grad_scale
+ * the scaled gradient g * (*grad_scale) is written back into grad (the data-parallel step
+ * normalises the all-reduced gradient by the global CE weight sum this way).
  */
-int pcs_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+int pcs_adam(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
              const float *grad_scale, float lr, float beta1, float beta2, float eps,
              float weight_decay, int64_t step, pcs_stream_t stream);
 

@@ -6,7 +6,7 @@
 
 namespace {
 
-constexpr int THREADS = 256, CMAX = 32;
+constexpr int THREADS = 256, CMAX = 64;
 
 __global__ __launch_bounds__(THREADS) void confusion_kernel(const float *__restrict__ logits, int64_t ld,
                                                             const int64_t *__restrict__ labels, int64_t M,
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(THREADS) void confusion_kernel(const float *__restr
 extern "C" int pcs_confusion(const float *logits, int64_t ld, const int64_t *labels, int64_t M, int32_t C,
                              int64_t *cm, pcs_stream_t stream) {
   if (!logits || !labels || !cm || M < 0 || C < 1 || C > CMAX || ld < C)
-    return pcs_set_einval("pcs_confusion", "bad arguments (1 <= C <= 32, ld >= C)");
+    return pcs_set_einval("pcs_confusion", "bad arguments (1 <= C <= 64, ld >= C)");
   if (M == 0) return 0;
   const int nb = (int)pcs_min64(2048, (M + THREADS - 1) / THREADS);
   hipLaunchKernelGGL(confusion_kernel, dim3(nb), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),

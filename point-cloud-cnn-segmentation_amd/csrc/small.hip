@@ -11,9 +11,22 @@ constexpr int THREADS = 256;
 constexpr int C1_BM = 128;  // conv1 row tile (same chunk geometry rules as pcs_gemm)
 
 // ---------------------------------------------------------------------------------------
-// conv1 forward: y[m, c] = b[c] + sum_k W[c,k] x[m,k]  (P:70, P:106), K = 4, fp32 math
+// conv1 forward: y[m, c] = b[c] + sum_k W[c,k] x[m,k]  (P:70, P:106), K = input_dim
+// (KD = 1..8; 4 for the reference's x, y, z, e), fp32 math
 // ---------------------------------------------------------------------------------------
-template <typename T>
+// one input row x[m, 0..KD) into registers (one 16-B load for the reference's KD = 4)
+template <int KD>
+PCS_DEV void load_xrow(const float *X, int64_t row, float (&x)[KD]) {
+  if constexpr (KD == 4) {
+    const float4 v = *reinterpret_cast<const float4 *>(X + row * 4);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < KD; ++k) x[k] = X[row * KD + k];
+  }
+}
+
+template <typename T, int KD>
 __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                             int tiles_per_chunk) {
   constexpr int EPC = Elem<T>::EPC;
@@ -29,12 +42,12 @@ __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int
   const float *X = reinterpret_cast<const float *>(a.A);
   const float *W = reinterpret_cast<const float *>(a.W);
   T *Cg = reinterpret_cast<T *>(a.C);
-  float w[EPC][4], bias[EPC];
+  float w[EPC][KD], bias[EPC];
 #pragma unroll
   for (int e = 0; e < EPC; ++e) {
     bias[e] = a.bias ? a.bias[c0 + e] : 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[e][k] = W[(c0 + e) * 4 + k];
+    for (int k = 0; k < KD; ++k) w[e][k] = W[(c0 + e) * KD + k];
   }
   float mean[EPC], m2[EPC], cnt = 0.f;
 #pragma unroll
@@ -43,15 +56,14 @@ __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int
   const int64_t r_end = pcs_min64(r_begin + (int64_t)tiles_per_chunk * C1_BM, N);
   for (int64_t r = r_begin + r0; r < r_end; r += RPP) {
     const int64_t grow = scene * N + r;
-    const float4 x = *reinterpret_cast<const float4 *>(X + grow * 4);
+    float x[KD];
+    load_xrow<KD>(X, grow, x);
     float v[EPC];
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
       float acc = bias[e];
-      acc = fmaf(w[e][0], x.x, acc);
-      acc = fmaf(w[e][1], x.y, acc);
-      acc = fmaf(w[e][2], x.z, acc);
-      acc = fmaf(w[e][3], x.w, acc);
+#pragma unroll
+      for (int k = 0; k < KD; ++k) acc = fmaf(w[e][k], x[k], acc);
       v[e] = acc;
     }
     const u32x4 packed = pack_chunk(v);
@@ -83,13 +95,13 @@ __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int
 // ---------------------------------------------------------------------------------------
 // conv1 weight gradient: dW[c,k] = sum_m dy[m,c] x[m,k]; dy = alpha dz + beta + gamma y
 // ---------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int KD>
 __global__ __launch_bounds__(THREADS) void conv1_wgrad_kernel(pcs_wgrad_args a, int64_t rows_per_split) {
   constexpr int EPC = Elem<T>::EPC;
   constexpr int COLS = 64;
   constexpr int CPR = COLS / EPC;
   constexpr int RPP = THREADS / CPR;
-  __shared__ float red[RPP][COLS * 4];
+  __shared__ float red[RPP][COLS * KD];
   const int tid = threadIdx.x;
   const int sps = a.splits_per_scene;
   const int scene = blockIdx.x / sps, sis = blockIdx.x % sps;
@@ -100,36 +112,35 @@ __global__ __launch_bounds__(THREADS) void conv1_wgrad_kernel(pcs_wgrad_args a, 
   const float *X = reinterpret_cast<const float *>(a.X);
   float ca[EPC], cb[EPC], cg[EPC];
   load_vec<EPC>(a.alpha, c0, ca); load_vec<EPC>(a.beta, c0, cb); load_vec<EPC>(a.gamma, c0, cg);
-  float acc[EPC][4];
+  float acc[EPC][KD];
 #pragma unroll
   for (int e = 0; e < EPC; ++e)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc[e][k] = 0.f;
+    for (int k = 0; k < KD; ++k) acc[e][k] = 0.f;
   const int64_t lo = (int64_t)sis * rows_per_split, hi = pcs_min64(lo + rows_per_split, N);
   for (int64_t r = lo + r0; r < hi; r += RPP) {
     const int64_t grow = scene * N + r;
     float dz[EPC], y[EPC];
     unpack_chunk(*reinterpret_cast<const u32x4 *>(dZ + grow * COLS + c0), dz);
     unpack_chunk(*reinterpret_cast<const u32x4 *>(Y + grow * COLS + c0), y);
-    const float4 x = *reinterpret_cast<const float4 *>(X + grow * 4);
+    float x[KD];
+    load_xrow<KD>(X, grow, x);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
       const float dy = fmaf(ca[e], dz[e], fmaf(cg[e], y[e], cb[e]));
-      acc[e][0] = fmaf(dy, x.x, acc[e][0]);
-      acc[e][1] = fmaf(dy, x.y, acc[e][1]);
-      acc[e][2] = fmaf(dy, x.z, acc[e][2]);
-      acc[e][3] = fmaf(dy, x.w, acc[e][3]);
+#pragma unroll
+      for (int k = 0; k < KD; ++k) acc[e][k] = fmaf(dy, x[k], acc[e][k]);
     }
   }
 #pragma unroll
   for (int e = 0; e < EPC; ++e)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) red[r0][(c0 + e) * 4 + k] = acc[e][k];
+    for (int k = 0; k < KD; ++k) red[r0][(c0 + e) * KD + k] = acc[e][k];
   __syncthreads();
-  for (int i = tid; i < COLS * 4; i += THREADS) {
+  for (int i = tid; i < COLS * KD; i += THREADS) {
     float s = 0.f;
     for (int j = 0; j < RPP; ++j) s += red[j][i];
-    a.partial[(int64_t)blockIdx.x * COLS * 4 + i] = s;
+    a.partial[(int64_t)blockIdx.x * COLS * KD + i] = s;
   }
 }
 
@@ -360,10 +371,10 @@ __global__ __launch_bounds__(256) void pool_bwd_coef_kernel(pcs_pool_bwd_args a)
 // ---------------------------------------------------------------------------------------
 constexpr int HEAD_R = 64;      // rows per tile
 constexpr int HEAD_CIN = 128;
-constexpr int HEAD_MAXC = 16;
+constexpr int HEAD_MAXC = 64;   // classes: <= 16 in the 16-class instantiation (2 WGs / CU), else 64
 constexpr int HEAD_LD = HEAD_CIN + 1;
 
-template <typename T, int MODE>
+template <typename T, int MODE, int HEAD_MAXC>
 __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tiles_per_scene,
                                                        int tiles_per_chunk) {
   constexpr int EPC = Elem<T>::EPC;
@@ -812,14 +823,18 @@ __global__ void cast_weight_kernel(const float *W, int64_t rows, int64_t cols, i
   if (WcT) WcT[(i % cols) * rows + i / cols] = o;
 }
 
-__global__ void adam_kernel(float *p, const float *g, float *m, float *v, int64_t n,
+__global__ void adam_kernel(float *p, float *g, float *m, float *v, int64_t n,
                             const float *gscale, float lr, float b1, float b2, float eps, float wd,
                             float bc1, float bc2_sqrt) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float gs = gscale ? *gscale : 1.f;
   const float pi = p[i];
-  const float gi = fmaf(g[i], gs, 0.f) + wd * pi;
+  float gr = g[i];
+  if (gscale) {   // scaled gradient written back: the caller's grad buffer holds dL/dp
+    gr *= *gscale;
+    g[i] = gr;
+  }
+  const float gi = gr + wd * pi;
   const float mi = b1 * m[i] + (1.f - b1) * gi;
   const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
   m[i] = mi;
@@ -847,19 +862,32 @@ static int64_t chunk_geo(int64_t N, int64_t B, int64_t tile, int32_t *cps_io, in
   return tpc;
 }
 
+namespace {
+constexpr int C1_MAXK = 8;   // input_dim 1..8 (the reference's points carry 4: x, y, z, e)
+#define PCS_C1_SWITCH(KD_, CALL)                                 \
+  switch (KD_) {                                                 \
+    case 1: CALL(1); break; case 2: CALL(2); break;              \
+    case 3: CALL(3); break; case 4: CALL(4); break;              \
+    case 5: CALL(5); break; case 6: CALL(6); break;              \
+    case 7: CALL(7); break; default: CALL(8); break;             \
+  }
+}  // namespace
+
 extern "C" int pcs_conv1_fwd(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (!ap || !ap->A || !ap->W || !ap->C) return pcs_set_einval("pcs_conv1_fwd", "missing operand");
-  if (ap->K != 4 || ap->Ncols != 64) return pcs_set_einval("pcs_conv1_fwd", "conv1 is 4 -> 64");
+  if (ap->K < 1 || ap->K > C1_MAXK || ap->Ncols != 64) return pcs_set_einval("pcs_conv1_fwd", "conv1 is input_dim (1..8) -> 64");
   pcs_gemm_args a = *ap;
   const int64_t tpc = pcs_fill_geometry(&a, C1_BM, 2048, 1) / C1_BM;
   const int tps = (int)((a.scene_rows + C1_BM - 1) / C1_BM);
   const int nb = (int)(a.num_scenes * a.chunks_per_scene);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (a.dtype == PCS_BF16)
-    hipLaunchKernelGGL(conv1_fwd_kernel<bf16_t>, dim3(nb), dim3(THREADS), 0, s, a, tps, (int)tpc);
-  else if (a.dtype == PCS_F32)
-    hipLaunchKernelGGL(conv1_fwd_kernel<float>, dim3(nb), dim3(THREADS), 0, s, a, tps, (int)tpc);
+#define PCS_C1F_BF(KD) hipLaunchKernelGGL((conv1_fwd_kernel<bf16_t, KD>), dim3(nb), dim3(THREADS), 0, s, a, tps, (int)tpc)
+#define PCS_C1F_F32(KD) hipLaunchKernelGGL((conv1_fwd_kernel<float, KD>), dim3(nb), dim3(THREADS), 0, s, a, tps, (int)tpc)
+  if (a.dtype == PCS_BF16) { PCS_C1_SWITCH(a.K, PCS_C1F_BF) }
+  else if (a.dtype == PCS_F32) { PCS_C1_SWITCH(a.K, PCS_C1F_F32) }
   else return pcs_set_einval("pcs_conv1_fwd", "bad dtype");
+#undef PCS_C1F_BF
+#undef PCS_C1F_F32
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -867,7 +895,8 @@ extern "C" int pcs_conv1_fwd(const pcs_gemm_args *ap, pcs_stream_t stream) {
 extern "C" int pcs_conv1_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   if (!ap || !ap->dZ || !ap->Y || !ap->X || !ap->partial || !ap->dW)
     return pcs_set_einval("pcs_conv1_wgrad", "missing operand");
-  if (ap->Cout != 64 || ap->Cin != 4) return pcs_set_einval("pcs_conv1_wgrad", "conv1 is 4 -> 64");
+  if (ap->Cout != 64 || ap->Cin < 1 || ap->Cin > C1_MAXK)
+    return pcs_set_einval("pcs_conv1_wgrad", "conv1 is input_dim (1..8) -> 64");
   pcs_wgrad_args a = *ap;
   if (a.splits_per_scene <= 0) {
     int64_t sps = (1024 + a.num_scenes - 1) / a.num_scenes;
@@ -879,14 +908,17 @@ extern "C" int pcs_conv1_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   const int64_t rps = (a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene;
   const int nb = (int)(a.num_scenes * a.splits_per_scene);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (a.dtype == PCS_BF16)
-    hipLaunchKernelGGL(conv1_wgrad_kernel<bf16_t>, dim3(nb), dim3(THREADS), 0, s, a, rps);
-  else if (a.dtype == PCS_F32)
-    hipLaunchKernelGGL(conv1_wgrad_kernel<float>, dim3(nb), dim3(THREADS), 0, s, a, rps);
+#define PCS_C1W_BF(KD) hipLaunchKernelGGL((conv1_wgrad_kernel<bf16_t, KD>), dim3(nb), dim3(THREADS), 0, s, a, rps)
+#define PCS_C1W_F32(KD) hipLaunchKernelGGL((conv1_wgrad_kernel<float, KD>), dim3(nb), dim3(THREADS), 0, s, a, rps)
+  if (a.dtype == PCS_BF16) { PCS_C1_SWITCH(a.Cin, PCS_C1W_BF) }
+  else if (a.dtype == PCS_F32) { PCS_C1_SWITCH(a.Cin, PCS_C1W_F32) }
   else return pcs_set_einval("pcs_conv1_wgrad", "bad dtype");
+#undef PCS_C1W_BF
+#undef PCS_C1W_F32
   PCS_CHECK_LAUNCH();
-  return pcs_reduce_partials(a.partial, nb, 64 * 4, 1.f, a.dW, a.ldw ? a.ldw : 4, 4, stream);
+  return pcs_reduce_partials(a.partial, nb, 64 * a.Cin, 1.f, a.dW, a.ldw ? a.ldw : a.Cin, a.Cin, stream);
 }
+#undef PCS_C1_SWITCH
 
 extern "C" int pcs_bn_fwd_finalize(const float *stats, int64_t B, int64_t N, int32_t C, int32_t cps,
                                    int64_t rpc, const float *gamma, const float *beta,
@@ -982,7 +1014,7 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
   if (!ap) return pcs_set_einval("pcs_head", "null args");
   pcs_head_args a = *ap;
   if (a.Cin != HEAD_CIN) return pcs_set_einval("pcs_head", "head input must have 128 channels");
-  if (a.num_classes < 1 || a.num_classes > HEAD_MAXC) return pcs_set_einval("pcs_head", "1 <= C <= 16");
+  if (a.num_classes < 1 || a.num_classes > HEAD_MAXC) return pcs_set_einval("pcs_head", "1 <= C <= 64");
   if (!a.Y || !a.s || !a.t || !a.W || !a.bias) return pcs_set_einval("pcs_head", "missing operand");
   if (a.mode == PCS_HEAD_CE && (!a.labels || !a.class_weight || !a.loss_partial))
     return pcs_set_einval("pcs_head", "CE mode needs labels, class_weight, loss_partial");
@@ -1018,8 +1050,13 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
     PCS_CHECK_LAUNCH();
     return 0;
   }
-#define PCS_HEAD_LAUNCH(T, MODE) \
-  hipLaunchKernelGGL((head_kernel<T, MODE>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc)
+#define PCS_HEAD_LAUNCH(T, MODE)                                                                  \
+  do {                                                                                            \
+    if (a.num_classes <= 16)                                                                      \
+      hipLaunchKernelGGL((head_kernel<T, MODE, 16>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc); \
+    else                                                                                          \
+      hipLaunchKernelGGL((head_kernel<T, MODE, 64>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc); \
+  } while (0)
   if (a.dtype == PCS_BF16) {
     if (a.mode == PCS_HEAD_FWD) PCS_HEAD_LAUNCH(bf16_t, PCS_HEAD_FWD);
     else if (a.mode == PCS_HEAD_CE) PCS_HEAD_LAUNCH(bf16_t, PCS_HEAD_CE);
@@ -1099,7 +1136,7 @@ extern "C" int pcs_cast_weight(const float *W, int64_t rows, int64_t cols, int64
   return 0;
 }
 
-extern "C" int pcs_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+extern "C" int pcs_adam(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                         const float *grad_scale, float lr, float beta1, float beta2, float eps,
                         float weight_decay, int64_t step, pcs_stream_t stream) {
   if (!param || !grad || !exp_avg || !exp_avg_sq || step < 1) return pcs_set_einval("pcs_adam", "bad arguments");

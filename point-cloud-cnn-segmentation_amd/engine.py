@@ -27,6 +27,8 @@ import torch
 from . import _lib as L
 
 BN_EPS = 1e-5
+MAX_INPUT_DIM = 8     # conv1 kernels (csrc/small.hip) are instantiated for K = 1..8
+MAX_CLASSES = 64      # head kernel (csrc/small.hip: 16- and 64-class instantiations)
 BN_MOMENTUM = 0.1
 DROPOUT_P = 0.3
 
@@ -56,6 +58,57 @@ def param_layout(num_classes: int, input_dim: int = 4):
     for bn, c in BNS:
         out += [(f"{bn}.weight", (c,)), (f"{bn}.bias", (c,))]
     return out
+
+
+# Flat fp32 buffers (parameters / gradients, optim.flatten_parameters): the parameters are
+# grouped by when the backward finishes their gradients, so each all-reduce bucket (§8 e) is
+# one contiguous range issued as soon as the backward has written it:
+#   "seg"    seg_conv1..seg_conv4 + the EXTRA tail (loss numerator, CE weight sum, valid
+#            count): ready once seg_conv1's local input/weight gradient has run;
+#   "global" global_feat: ready after the Gram-form weight gradient (mid-backward);
+#   "tail"   the 9 BatchNorms and conv1..conv5: ready at the end.
+FLAT_EXTRA = 4
+_SEG = ("seg_conv1", "seg_conv2", "seg_conv3", "seg_conv4")
+_EARLY_CONVS = ("conv1", "conv2", "conv3", "conv4", "conv5")
+
+
+def flat_layout(num_classes: int, input_dim: int = 4):
+    """[(name, shape)] in flat-buffer order (see above); registration order is param_layout."""
+    reg = dict(param_layout(num_classes, input_dim))
+    names = [f"{bn}.{w}" for bn, _ in BNS for w in ("weight", "bias")]
+    for conv in _EARLY_CONVS + ("global_feat",) + _SEG:
+        names += [f"{conv}.weight", f"{conv}.bias"]
+    return [(n, reg[n]) for n in names]
+
+
+def flat_offsets(num_classes: int, input_dim: int = 4):
+    """name -> element offset in the flat buffers; the EXTRA tail starts at the total."""
+    offs, off = {}, 0
+    for n, shape in flat_layout(num_classes, input_dim):
+        offs[n] = off
+        off += int(torch.Size(shape).numel())
+    return offs, off
+
+
+def bucket_ranges(num_classes: int, input_dim: int = 4):
+    """Gradient all-reduce buckets: name -> [lo, hi) element range of the flat gradient
+    buffer (which carries FLAT_EXTRA scalars after the parameters)."""
+    offs, total = flat_offsets(num_classes, input_dim)
+    return {"seg": (offs["seg_conv1.weight"], total + FLAT_EXTRA),
+            "global": (offs["global_feat.weight"], offs["seg_conv1.weight"]),
+            "tail": (0, offs["global_feat.weight"])}
+
+
+def check_dims(num_classes: int, input_dim: int):
+    """The reference accepts any input_dim / num_classes (P:66-83; num_classes comes from the
+    data, P:153); the kernels cover input_dim 1..8 (conv1 is unrolled over K) and 1..64
+    classes (the head keeps a row's logits in registers and seg_conv4 in LDS)."""
+    if not 1 <= int(input_dim) <= MAX_INPUT_DIM:
+        raise ValueError(f"pcs_amd supports input_dim 1..{MAX_INPUT_DIM} (the reference's points carry "
+                         f"4: x, y, z, e); got {input_dim}")
+    if not 1 <= int(num_classes) <= MAX_CLASSES:
+        raise ValueError(f"pcs_amd supports 1..{MAX_CLASSES} classes (seg_conv4 + CE head kernel); "
+                         f"got {num_classes}")
 
 
 def _dt(dtype: str):
@@ -98,21 +151,15 @@ class Engine:
     """Launches the PointNetSegmentation kernels for one compute dtype and device."""
 
     def __init__(self, num_classes: int, dtype: str = "fp32", input_dim: int = 4):
-        if input_dim != 4:
-            raise NotImplementedError("the conv1 kernel is specialised for input_dim=4 (x,y,z,e)")
-        if not 1 <= num_classes <= 16:
-            raise NotImplementedError("the fused head supports 1..16 classes")
+        check_dims(num_classes, input_dim)
+        self.input_dim = input_dim
         self.C = num_classes
         self.dtype = dtype
         self.dt, self.tdt = _dt(dtype)
-        self.layout = param_layout(num_classes, input_dim)
+        self.layout = param_layout(num_classes, input_dim)          # registration order
         self.numel = {n: int(torch.Size(s).numel()) for n, s in self.layout}
-        self.offsets = {}
-        off = 0
-        for n, _ in self.layout:
-            self.offsets[n] = off
-            off += self.numel[n]
-        self.total_params = off
+        self.offsets, self.total_params = flat_offsets(num_classes, input_dim)   # flat order
+        self.buckets = bucket_ranges(num_classes, input_dim)
         self._geo = {}
         self.flags = 0       # L.FLAG_GENERIC forces the generic GEMM (cross-checks)
         self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
@@ -197,7 +244,7 @@ class Engine:
             setattr(a, k, L.ptr(v))
         self._launch(tag, "pcs_gemm", ct.byref(a), self._stream())
 
-    def _wgrad(self, B, N, cout, cin, dy_mode, x_mode, dW, ldw=0, **kw):
+    def _wgrad(self, B, N, cout, cin, dy_mode, x_mode, dW, ldw=0, conv1=False, **kw):
         tag = kw.pop("tag", None)
         a = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=cout, Cin=cin, dtype=self.dt,
                         splits_per_scene=0, dy_mode=dy_mode, x_mode=x_mode,
@@ -205,8 +252,8 @@ class Engine:
                         flags=self.flags)
         for k, v in kw.items():
             setattr(a, k, L.ptr(v))
-        fn = "pcs_conv1_wgrad" if cin == 4 else "pcs_wgrad"
-        if cin == 4:
+        fn = "pcs_conv1_wgrad" if conv1 else "pcs_wgrad"
+        if conv1:
             a.splits_per_scene = max(1, min((1024 + B - 1) // B, (N + 255) // 256))
             nbytes = B * a.splits_per_scene * cout * cin * 4
         else:
@@ -250,6 +297,8 @@ class Engine:
             raise RuntimeError("pcs_amd runs on a HIP device only (no CPU fallback)")
         dev = x.device
         B, N, D = x.shape
+        if D != self.input_dim:
+            raise ValueError(f"expected x of shape (B, N, {self.input_dim}), got {tuple(x.shape)}")
         M = B * N
         s = self._stream()
         x = x.contiguous().float()
@@ -271,12 +320,12 @@ class Engine:
         # shifts running_mean), which keeps them centred: full precision in fp32/bf16.
         # conv1 (K=4)
         y1 = self._empty(M, 64, device=dev)
-        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=4, Ncols=64, dtype=L.F32, chunks_per_scene=0,
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=D, Ncols=64, dtype=L.F32, chunks_per_scene=0,
                        flags=L.FLAG_GENERIC)
         rpc = L.load().pcs_gemm_geometry(ct.byref(a))    # conv1: generic 128-row geometry
         cps = a.chunks_per_scene
         st = torch.empty(B * cps, 64, 2, dtype=torch.float32, device=dev) if train else None
-        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=4, Ncols=64, dtype=self.dt,
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=D, Ncols=64, dtype=self.dt,
                        chunks_per_scene=cps, A=L.ptr(x), W=L.ptr(P["conv1.weight"]),
                        C=L.ptr(y1), bias=None, stats=L.ptr(st))
         self._launch("fwd:conv1", "pcs_conv1_fwd", ct.byref(a), s)
@@ -351,6 +400,13 @@ class Engine:
         if train:
             if masks is not None:
                 m1, m2 = masks
+                # the kernels read M x 512 / M x 256 keep bits: a mask for another batch
+                # shape (e.g. a DataParallel replica's chunk) would be read out of bounds
+                if (tuple(m1.shape) != (M, 64) or tuple(m2.shape) != (M, 32) or m1.dtype != torch.uint8
+                        or m2.dtype != torch.uint8 or m1.device != dev or m2.device != dev):
+                    raise ValueError(f"dropout masks must be uint8 [{M}, 64] and [{M}, 32] on {dev}, got "
+                                     f"{tuple(m1.shape)} {m1.dtype} and {tuple(m2.shape)} {m2.dtype}")
+                m1, m2 = m1.contiguous(), m2.contiguous()
             else:
                 m1 = torch.empty(M, 64, dtype=torch.uint8, device=dev)
                 m2 = torch.empty(M, 32, dtype=torch.uint8, device=dev)
@@ -412,10 +468,13 @@ class Engine:
         return hb
 
     # ------------------------------------------------------------------ backward
-    def backward(self, P, sv, gflat, dlogits=None):
+    def backward(self, P, sv, gflat, dlogits=None, on_bucket=None):
         """Backward pass: every parameter gradient is written into the flat fp32 buffer
-        ``gflat`` (registration order, see param_layout).  Uses the head buffers of a
-        fused CE forward, or runs the head backward on caller-supplied ``dlogits``."""
+        ``gflat`` (flat order, see flat_layout).  Uses the head buffers of a fused CE
+        forward, or runs the head backward on caller-supplied ``dlogits``.  ``on_bucket(name)``
+        is called as soon as the kernels writing gradient bucket ``name`` (bucket_ranges)
+        have been enqueued, so a data-parallel caller can start its all-reduce there."""
+        bucket = on_bucket or (lambda name: None)
         if not sv.train:
             raise RuntimeError("backward needs a train-mode forward (BatchNorm batch statistics)")
         B, N = sv.B, sv.N
@@ -557,6 +616,8 @@ class Engine:
                        A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
             wgrad("seg_conv1", "bn_seg1", 64, 512, dz_s1, ys["seg_conv1"], "conv2", "bn2", ldw=Ws1.shape[1])
 
+        bucket("seg")
+
         # global_feat input gradient in folded form (P:113 at P:254): with dy_g = beta_g +
         # gamma_g * y_g + (max-pool rows) and y_g = a5 Wg^T,
         #   dA5 = a5 H + 1 c^T + sum_b sp[b, c] Wg[c, :] at the row am[b, c],
@@ -594,6 +655,7 @@ class Engine:
                      L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.dt, None, None,
                      L.ptr(G("global_feat.weight")), 1024, s)
         keepalive.append((Hg, cvec, ones, zeros, gram, colsum, ws, Wg_r))
+        bucket("global")
 
         # conv5 (128 -> 1024): R = dz5^T a4 gives bn5's S2 (y5 = a4 W5^T is not stored) and
         # the alpha-term of dW5; then the folded input gradient and the Gram-form dW5:
@@ -639,7 +701,8 @@ class Engine:
         bn_bwd("bn1", "conv1", st, cps)
         dz1 = bufB
         al, be, ga = coefs["bn1"]
-        keepalive.append(self._wgrad(B, N, 64, 4, L.PRO_BWD, L.PRO_RAW, G("conv1.weight"), ldw=4,
-                                     tag="wgrad:conv1",
+        keepalive.append(self._wgrad(B, N, 64, self.input_dim, L.PRO_BWD, L.PRO_RAW, G("conv1.weight"),
+                                     ldw=self.input_dim, conv1=True, tag="wgrad:conv1",
                                      dZ=dz1, Y=ys["conv1"], alpha=al, beta=be, gamma=ga, X=sv.x))
+        bucket("tail")
         return hb

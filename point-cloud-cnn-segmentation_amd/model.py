@@ -13,11 +13,37 @@ works unchanged).  There is no CPU path: calling the model on a CPU tensor raise
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .engine import BNS, Engine
+from .engine import BNS, FLAT_EXTRA, Engine, check_dims, flat_offsets, param_layout
+
+
+class _DropoutState:
+    """Per-module (per-replica) dropout state: replayed keep masks and the Philox seed stream.
+
+    nn.DataParallel (P:209-211) replicates the module every forward by shallow-copying its
+    ``__dict__`` (torch/nn/parallel/replicate.py) and runs the replicas in one thread per GPU
+    (parallel_apply.py), so anything mutable on the module would be shared between threads.
+    ``PointNetSegmentation._replicate_for_data_parallel`` gives every replica its own state,
+    seeded from the base module's stream (under its lock, in replica order)."""
+
+    def __init__(self, seed: int):
+        self.lock = threading.Lock()
+        self.gen = torch.Generator().manual_seed(seed)
+        self.masks = None
+
+    def next_seed(self) -> int:
+        with self.lock:
+            return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
+
+    def take_masks(self):
+        with self.lock:
+            m, self.masks = self.masks, None
+            return m
 
 
 class _PointNetFunction(torch.autograd.Function):
@@ -85,9 +111,12 @@ class PointNetSegmentation(nn.Module):
         self.num_classes = num_classes
         self.input_dim = input_dim
         self.compute_dtype = compute_dtype
+        check_dims(num_classes, input_dim)   # fail at construction, not at the first forward
+        # created lazily (it loads libpcs.so); it holds no per-call state (only a geometry
+        # cache), so DataParallel replicas may share it
         self._eng = None
-        self._masks = None
-        self._seed_gen = torch.Generator().manual_seed(0x5eed)
+        self._dstate = _DropoutState(0x5eed)
+        self._pnames = [n for n, _ in param_layout(num_classes, input_dim)]
 
     # ---------------------------------------------------------------- internals
     def _engine(self) -> Engine:
@@ -95,14 +124,35 @@ class PointNetSegmentation(nn.Module):
             self._eng = Engine(self.num_classes, self.compute_dtype, self.input_dim)
         return self._eng
 
+    def _params(self):
+        """The parameters in registration order, by attribute: on a DataParallel replica they
+        are the broadcast copies that replicate() sets as plain attributes (its
+        ``_parameters`` is empty), so named_parameters() would see none of them."""
+        out = []
+        for n in self._pnames:
+            mod, attr = n.split(".")
+            out.append(getattr(getattr(self, mod), attr))
+        return out
+
     def _param_dict(self):
-        return {n: p for n, p in self.named_parameters()}
+        return dict(zip(self._pnames, self._params()))
+
+    _flat_extra = FLAT_EXTRA   # gradient-buffer tail used by the fused data-parallel step
+
+    def _flat_offsets(self):
+        """Parameter offsets in the flat fp32 buffers (engine.flat_layout: bucket order)."""
+        return flat_offsets(self.num_classes, self.input_dim)[0]
 
     def _buffer_dict(self):
         return {n: b for n, b in self.named_buffers()}
 
     def _next_seed(self):
-        return int(torch.randint(0, 2 ** 62, (1,), generator=self._seed_gen).item())
+        return self._dstate.next_seed()
+
+    def _replicate_for_data_parallel(self):
+        replica = super()._replicate_for_data_parallel()
+        replica._dstate = _DropoutState(self._next_seed())
+        return replica
 
     def set_dropout_masks(self, bits1, bits2):
         """Replay dropout keep masks in the next train forward (tests / reference parity).
@@ -110,14 +160,15 @@ class PointNetSegmentation(nn.Module):
         bits1: uint8 [B*N, 64] (512 channels after bn_seg1, P:124), bits2: uint8 [B*N, 32]
         (256 channels after bn_seg2, P:126); bit i of byte j = channel 8j+i.
         """
-        self._masks = (bits1.contiguous(), bits2.contiguous())
+        with self._dstate.lock:
+            self._dstate.masks = (bits1.contiguous(), bits2.contiguous())
 
     def _take_dropout_masks(self):
-        m, self._masks = self._masks, None
-        return m
+        return self._dstate.take_masks()
 
     def seed_dropout(self, seed: int):
-        self._seed_gen.manual_seed(seed)
+        with self._dstate.lock:
+            self._dstate.gen.manual_seed(seed)
 
     # ---------------------------------------------------------------- API
     def forward(self, x):
@@ -127,7 +178,7 @@ class PointNetSegmentation(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("pcs_amd.PointNetSegmentation runs on a HIP device only; "
                                "move the model and inputs with .to('cuda')")
-        return _PointNetFunction.apply(x, self, *self.parameters())
+        return _PointNetFunction.apply(x, self, *self._params())
 
 
 def load_reference_checkpoint(path, map_location="cpu"):

@@ -13,21 +13,33 @@ import torch
 from . import _lib as L
 
 
+def param_slices(module: torch.nn.Module):
+    """[(param, offset, numel)] in registration order.  Offsets follow the module's flat
+    layout when it defines one (PointNetSegmentation: gradient-bucket order, engine.flat_layout)
+    and registration order otherwise."""
+    named = list(module.named_parameters())
+    offs = module._flat_offsets() if hasattr(module, "_flat_offsets") else None
+    out, off = [], 0
+    for name, p in named:
+        k = p.numel()
+        out.append((p, offs[name] if offs is not None else off, k))
+        off += k
+    return out
+
+
 def flatten_parameters(module: torch.nn.Module):
     """Re-home every parameter of ``module`` as a view into one contiguous fp32 buffer
-    (and give each a gradient view into one flat grad buffer).  Returns (pflat, gflat)."""
-    params = list(module.parameters())
-    dev = params[0].device
-    n = sum(p.numel() for p in params)
+    (and give each a gradient view into one flat grad buffer, which carries the module's
+    ``_flat_extra`` scalars after the parameters).  Returns (pflat, gflat)."""
+    sl = param_slices(module)
+    dev = sl[0][0].device
+    n = sum(k for _, _, k in sl)
     pflat = torch.empty(n, dtype=torch.float32, device=dev)
-    gflat = torch.zeros(n, dtype=torch.float32, device=dev)
-    off = 0
-    for p in params:
-        k = p.numel()
+    gflat = torch.zeros(n + getattr(module, "_flat_extra", 0), dtype=torch.float32, device=dev)
+    for p, off, k in sl:
         pflat[off:off + k].copy_(p.data.reshape(-1))
         p.data = pflat[off:off + k].view_as(p)
         p.grad = gflat[off:off + k].view_as(p)
-        off += k
     module._pcs_flat = (pflat, gflat)
     return pflat, gflat
 
@@ -38,15 +50,12 @@ def flat_buffers(module):
     flat = getattr(module, "_pcs_flat", None)
     if flat is not None:
         pflat, gflat = flat
-        off = 0
         ok = True
-        for p in module.parameters():
-            k = p.numel()
+        for p, off, k in param_slices(module):
             if (p.data_ptr() != pflat[off:].data_ptr() or p.grad is None
                     or p.grad.data_ptr() != gflat[off:].data_ptr()):
                 ok = False
                 break
-            off += k
         if ok:
             return pflat, gflat
     return flatten_parameters(module)
@@ -67,7 +76,9 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg = torch.zeros_like(pflat)
         self.exp_avg_sq = torch.zeros_like(pflat)
         self.step_count = 0
-        self.grad_scale = None   # optional device scalar multiplying every gradient
+        # optional device scalar multiplying every gradient; the kernel writes the scaled
+        # gradient back, so p.grad holds it after the step (data-parallel normalisation)
+        self.grad_scale = None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -89,26 +100,20 @@ class FusedAdam(torch.optim.Optimizer):
     def state_dict(self):
         """torch.optim.Adam-compatible layout (per-parameter step/exp_avg/exp_avg_sq)."""
         state = {}
-        off = 0
-        for i, p in enumerate(self.module.parameters()):
-            k = p.numel()
+        for i, (p, off, k) in enumerate(param_slices(self.module)):
             state[i] = {"step": torch.tensor(float(self.step_count)),
                         "exp_avg": self.exp_avg[off:off + k].view_as(p).clone(),
                         "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p).clone()}
-            off += k
         groups = [dict(g, params=list(range(len(g["params"])))) for g in self.param_groups]
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
-        off = 0
-        for i, p in enumerate(self.module.parameters()):
-            k = p.numel()
+        for i, (p, off, k) in enumerate(param_slices(self.module)):
             st = sd["state"].get(i) or sd["state"].get(str(i))
             if st is not None:
                 self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
                 self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
                 self.step_count = int(float(st["step"]))
-            off += k
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             for key in ("lr", "betas", "eps", "weight_decay"):
                 if key in sg:

@@ -7,9 +7,11 @@ and replica 0 shares the base module's running buffers.  ``tests/golden/train_c3
 records exactly that, computed by the reference module itself (make_golden.make_dp_case).
 
 ``pcs_amd.FusedTrainStep`` implements it as one process per GPU: each rank runs its own
-scenes, ``allreduce_ce_denominator`` makes the CE denominator global before the head and
-``allreduce_gradients`` sums the flat gradient buffer.  Here the per-rank compute is the
-oracle (fp64) and the collectives are the product's own helpers over gloo.
+scenes and computes its un-normalised gradient; the flat gradient buffer (engine.flat_layout
+order, with the loss numerator and CE weight sum in its tail) is summed in the three
+``engine.bucket_ranges`` buckets by ``train.GradientBuckets``, then scaled by 1 / the global
+weight sum.  Here the per-rank compute is the oracle (fp64) and the buckets / collectives are
+the product's own over gloo.
 """
 import os
 import socket
@@ -48,23 +50,31 @@ def _rank_share(g, rank, world, denom=None):
 
 
 def _dp_worker(rank, world, port, out):
-    from pcs_amd.train import allreduce_ce_denominator, allreduce_gradients
+    from pcs_amd.engine import bucket_ranges, flat_layout
+    from pcs_amd.train import GradientBuckets
     torch.set_num_threads(2)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     try:
         g = load(CASE)
-        names = [str(n) for n in g["param_names"]]
-        wsum = torch.tensor([_rank_share(g, rank, world), 0.0, 0.0], dtype=torch.float64)
-        allreduce_ce_denominator(wsum)
-        loss, logits, grads, cache = _rank_share(g, rank, world, denom=float(wsum[0]))
-        gflat = torch.from_numpy(np.concatenate([grads[n].reshape(-1) for n in names]))
-        loss_num = torch.tensor([loss * float(wsum[0])], dtype=torch.float64)
-        allreduce_gradients(gflat, loss_num)
+        C = int(g["C"])
+        wloc = _rank_share(g, rank, world)
+        # un-normalised share (denominator 1): the loss is linear in 1 / sum_w
+        loss, logits, grads, cache = _rank_share(g, rank, world, denom=1.0)
+        names = [n for n, _ in flat_layout(C)]
+        gflat = torch.from_numpy(np.concatenate([grads[n].reshape(-1) for n in names]
+                                                + [np.array([loss, wloc, 0.0, 0.0])]))
+        b = GradientBuckets(gflat, bucket_ranges(C))
+        for name in ("seg", "global", "tail"):   # the order the backward finishes them
+            b.issue(name)
+        b.wait()
+        nparam = gflat.numel() - 4
+        wsum = float(gflat[nparam + 1])
+        grads_flat = gflat[:nparam] / wsum
         sd = inputs(g)[0]
         run = orc.update_running_stats(sd, cache)
-        np.savez(os.path.join(out, f"rank{rank}.npz"), gflat=gflat.numpy(),
-                 loss=float(loss_num[0] / wsum[0]), logits=logits,
+        np.savez(os.path.join(out, f"rank{rank}.npz"), gflat=grads_flat.numpy(),
+                 loss=float(gflat[nparam] / wsum), logits=logits,
                  **{f"buf/{k}": np.asarray(v) for k, v in run.items()
                     if "running" in k or "num_batches" in k})
     finally:
@@ -72,14 +82,27 @@ def _dp_worker(rank, world, port, out):
 
 
 def _unflatten(g, flat):
+    from pcs_amd.engine import flat_layout
     sd = inputs(g)[0]
     out, o = {}, 0
-    for n in [str(n) for n in g["param_names"]]:
+    for n, _ in flat_layout(int(g["C"])):
         k = sd[n].size
         out[n] = flat[o:o + k].reshape(sd[n].shape)
         o += k
     assert o == flat.size
     return out
+
+
+def test_bucket_ranges_cover_the_flat_buffer():
+    from pcs_amd.engine import FLAT_EXTRA, bucket_ranges, flat_offsets, param_layout
+    for C, D in ((2, 4), (3, 4), (20, 3)):
+        offs, total = flat_offsets(C, D)
+        assert sorted(offs) == sorted(n for n, _ in param_layout(C, D))
+        r = sorted(bucket_ranges(C, D).values())
+        assert r[0][0] == 0 and r[-1][1] == total + FLAT_EXTRA
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        # seg_conv4's weight and bias are adjacent (the head writes them as one block)
+        assert offs["seg_conv4.bias"] == offs["seg_conv4.weight"] + C * 128
 
 
 @pytest.mark.parametrize("B", [1, 2, 3, 4, 5, 7, 8])

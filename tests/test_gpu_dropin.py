@@ -1,0 +1,178 @@
+"""The drop-in module under the reference's own callers (SURVEY §8 b):
+
+* nn.DataParallel wrapping (P:209-211) running the reference's inner loop P:236-255 with
+  torch.optim.Adam + StepLR, checkpointed as model.module.state_dict() (P:375);
+* DataParallel's replica path (torch.nn.parallel.replicate + parallel_apply, one thread per
+  replica, P:244): replicas share the Engine but own their dropout state, and gradients
+  flow back to the base parameters through Broadcast's reduce-add;
+* num_classes / input_dim beyond the reference defaults (P:66-83; num_classes is
+  len(set(labels)), P:153): fp32 parity with the oracle at C = 20 and input_dim = 3.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import pointnet_oracle as orc
+from golden_util import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _pair(C=3, seed=5, dtype="fp32"):
+    from pcs_amd.model import PointNetSegmentation
+    sd = orc.init_params(C, seed, bn_affine_random=True)
+    ms = []
+    for _ in range(2):
+        m = PointNetSegmentation(C, compute_dtype=dtype).to(DEV)
+        m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in sd.items()})
+        ms.append(m)
+    return ms
+
+
+def _batches(C, n=2):
+    from pcs_amd.data import synthetic_batch
+    out = []
+    for i in range(n):
+        pts, lab, msk = synthetic_batch(300 + i, [1500, 1100, 1500], C, grid=32)
+        out.append((torch.from_numpy(pts), torch.from_numpy(lab), torch.from_numpy(msk)))
+    return out
+
+
+def _reference_loop(model, batches, C, weight):
+    """P:236-255 verbatim in structure (criterion P:216, Adam P:217, StepLR P:218)."""
+    criterion = nn.CrossEntropyLoss(ignore_index=-1, weight=weight)
+    optimizer = torch.optim.Adam(model.parameters(), lr=0.001, weight_decay=1e-4)
+    scheduler = torch.optim.lr_scheduler.StepLR(optimizer, step_size=20, gamma=0.5)
+    model.train()
+    losses = []
+    for points, labels, masks in batches:
+        points, labels, masks = points.to(DEV), labels.to(DEV), masks.to(DEV)
+        optimizer.zero_grad()
+        outputs = model(points)
+        outputs = outputs.contiguous().view(-1, C)
+        labels = labels.view(-1)
+        loss = criterion(outputs, labels)
+        loss.backward()
+        optimizer.step()
+        losses.append(loss.item())
+        _, predicted = torch.max(outputs.view(points.shape[0], -1, C), 2)   # P:261
+    scheduler.step()
+    return losses
+
+
+def test_dataparallel_reference_loop():
+    from pcs_amd.model import load_reference_checkpoint
+    C = 3
+    base, plain = _pair(C)
+    dp = nn.DataParallel(base, device_ids=[0])
+    w = torch.tensor([0.5, 1.0, 1.5], device=DEV)
+    b = _batches(C)
+    l_dp = _reference_loop(dp, b, C, w)
+    l_plain = _reference_loop(plain, b, C, w)
+    assert l_dp == l_plain   # identical kernels, seeds and Adam: bitwise
+    for (k1, v1), (k2, v2) in zip(dp.module.state_dict().items(), plain.state_dict().items()):
+        assert k1 == k2 and torch.equal(v1, v2), k1
+    # P:375 saves model.module.state_dict(): the 65 reference keys, no prefix
+    keys = list(dp.module.state_dict().keys())
+    assert keys == orc.state_dict_keys(C) and len(keys) == 65
+    assert all(k.startswith("module.") for k in dp.state_dict())
+    assert int(dp.module.bn1.num_batches_tracked) == 2
+
+
+def test_dataparallel_checkpoint_prefix_roundtrip(tmp_path):
+    from pcs_amd.model import PointNetSegmentation, load_reference_checkpoint
+    base, _ = _pair(2)
+    dp = nn.DataParallel(base, device_ids=[0])
+    path = tmp_path / "best_model.pth"
+    torch.save({"model_state_dict": dp.state_dict(), "num_classes": 2}, path)   # prefixed
+    sd, ck = load_reference_checkpoint(path)
+    m = PointNetSegmentation(2).to(DEV)
+    m.load_state_dict(sd)
+    for k, v in base.state_dict().items():
+        assert torch.equal(m.state_dict()[k], v), k
+
+
+def test_replicas_in_threads_match_sequential():
+    """Two replicas (replicate() twice, as DataParallel does per device) run concurrently in
+    parallel_apply's threads == the same replicas run one after the other; gradients reach
+    the base parameters (Broadcast backward) and every replica drew its own dropout seed."""
+    from torch.nn.parallel import parallel_apply, replicate
+    C = 3
+    b = _batches(C, 2)
+    res = []
+    for threaded in (True, False):
+        base, _ = _pair(C)
+        base.train()
+        reps = [replicate(base, [0])[0] for _ in range(2)]
+        assert reps[0]._dstate is not reps[1]._dstate and reps[0]._dstate is not base._dstate
+        xs = [(bb[0].to(DEV),) for bb in b]
+        if threaded:
+            outs = parallel_apply(reps, xs, devices=[0, 0])
+        else:
+            outs = [r(*x) for r, x in zip(reps, xs)]
+        crit = nn.CrossEntropyLoss(ignore_index=-1)
+        loss = sum(crit(o.contiguous().view(-1, C), bb[1].to(DEV).view(-1)) for o, bb in zip(outs, b))
+        loss.backward()
+        res.append(([o.detach().cpu() for o in outs], {n: p.grad.detach().cpu().clone() for n, p in base.named_parameters()}))
+    (o1, g1), (o2, g2) = res
+    for a, c in zip(o1, o2):
+        assert torch.equal(a, c)
+    assert not torch.equal(o1[0][:1000], o1[1][:1000])   # different inputs / masks
+    for n in g1:
+        assert torch.equal(g1[n], g2[n]), n
+        assert torch.isfinite(g1[n]).all()
+    assert float(g1["global_feat.weight"].abs().sum()) > 0
+
+
+@pytest.mark.parametrize("C,D", [(20, 4), (3, 3), (64, 4)])
+def test_classes_and_input_dim_fp32_parity(C, D):
+    """Non-default num_classes / input_dim against the fp64 oracle (the oracle is generic in
+    both; parity unpinned by reference fixtures for these shapes)."""
+    from pcs_amd.data import synthetic_batch
+    from pcs_amd.model import PointNetSegmentation
+    sd = orc.init_params(C, 41 + C, input_dim=D, bn_affine_random=True)
+    pts, lab, _ = synthetic_batch(42, [900, 700], 2, grid=16)
+    rng = np.random.default_rng(C)
+    lab = np.where(lab >= 0, rng.integers(0, C, lab.shape), -1)
+    pts = np.ascontiguousarray(pts[..., :D]) if D <= 4 else pts
+    masks = orc.dropout_masks(3, pts.shape[0] * pts.shape[1])
+    w = (np.arange(C) % 3 + 1).astype(np.float32) / 2
+    m = PointNetSegmentation(C, input_dim=D).to(DEV)
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in sd.items()})
+    m.train()
+    m.set_dropout_masks(*(torch.from_numpy(np.packbits(k, axis=1, bitorder="little")).to(DEV) for k in masks))
+    out = m(torch.from_numpy(pts).to(DEV))
+    crit = nn.CrossEntropyLoss(ignore_index=-1, weight=torch.from_numpy(w).to(DEV))
+    loss = crit(out.contiguous().view(-1, C), torch.from_numpy(lab).to(DEV).view(-1))
+    loss.backward()
+    rloss, rlogits, grads, _ = orc.train_step(sd, pts, lab, w, masks=masks)
+    assert rel_err(out.detach().cpu().numpy(), rlogits) < 1e-4
+    assert abs(loss.item() - rloss) < 1e-5 * max(1.0, abs(rloss))
+    # gradients: random labels over many classes on 1,600 train-mode points make this step
+    # far more rounding-sensitive than the golden cases (ReLU-boundary flips): a plain fp32
+    # restatement (the oracle in fp32, as the reference computes) is 0.8-2.4 % off fp64
+    # here.  Bound: as accurate as that fp32 computation, and never looser than it needs
+    # (the 2e-3 of the golden cases); measured r02: <= 6e-3 at C = 20 / 64, 9e-4 at D = 3.
+    g32 = orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32)[2]
+    gmax = max(np.linalg.norm(v) for v in grads.values())
+    errs, bound = {}, {}
+    for n, p in m.named_parameters():
+        noisy = n.endswith(".bias") and not n.startswith(("bn", "seg_conv4"))
+        ref = grads[n].reshape(-1)
+        scale = 1e-3 * gmax if noisy else max(np.linalg.norm(ref), 1e-3 * gmax)
+        errs[n] = float(np.linalg.norm(p.grad.detach().cpu().numpy().reshape(-1) - ref) / scale)
+        bound[n] = max(2e-3, float(np.linalg.norm(g32[n].reshape(-1) - ref) / scale))
+    print(C, D, errs)
+    bad = {k: (v, bound[k]) for k, v in errs.items() if v > bound[k]}
+    assert not bad, bad
+
+
+def test_mask_shape_mismatch_raises():
+    base, _ = _pair(2)
+    base.train()
+    bits = (torch.zeros(10, 64, dtype=torch.uint8, device=DEV), torch.zeros(10, 32, dtype=torch.uint8, device=DEV))
+    base.set_dropout_masks(*bits)
+    with pytest.raises(ValueError):
+        base(torch.zeros(1, 16, 4, device=DEV))
