@@ -1,0 +1,254 @@
+"""bf16-storage emulation of the PointNetSegmentation training step (numpy float32).
+
+TEST / ANALYSIS INFRASTRUCTURE ONLY (same rule as pointnet_oracle.py: never imported by the
+product path).  It answers one question about the bf16 bench path: is its gradient error at
+large scenes a property of storing activations and gradients in bf16, or of a kernel?
+
+``train_step(sd, x, labels, weight, masks, store)`` runs the reference step (forward P:98-133,
+weighted CE P:216/251, backward P:254) in float32 arithmetic.  With ``store="fp32"`` nothing
+is rounded (a plain fp32 restatement).  With ``store="bf16"`` every tensor the HIP bf16 path
+keeps in bf16 is rounded to bf16 (round-to-nearest-even) at the point the HIP path rounds it
+(point-cloud-cnn-segmentation_amd/engine.py), everything else stays fp32:
+
+* forward: GEMM weights (conv2..conv5, global_feat, seg_conv1's local half, seg_conv2/3;
+  conv1, seg_conv4 and seg_conv1's global half stay fp32); every stored pre-BN output Y_l
+  (BN statistics from the stored values, as the GEMM epilogues compute them); every GEMM
+  input activation a_l = relu(bn(Y_l)) [* dropout]; a5 = relu(bn5(y5)) (conv5's statistics
+  and global_feat's statistics / max-pool from fp32 accumulators, as the Gram-derived bn5
+  statistics and the LDS-DMA epilogue do); the head works in fp32;
+* backward: every stored dZ_l (the BN-output gradient after ReLU / dropout; its sums S1 / S2
+  from the fp32 values, as the producing epilogues form them); every GEMM operand dy_l; the
+  folded global_feat / conv5 operands H and diag(alpha) W (the Gram-form weight gradients,
+  the pool rows and the per-scene sums csum_b stay fp32).
+
+Memory is kept to the tensors the backward needs (about 9 KB per point plus a few [M, 1024]
+temporaries), so 4 scenes x 64^3 points run on a 64 GB host.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from pointnet_oracle import BN_EPS, DROPOUT_P, _w
+
+F32 = np.float32
+
+
+def round_bf16(a):
+    """float32 -> nearest-even bf16, returned as float32 (finite inputs)."""
+    a = np.ascontiguousarray(a, dtype=F32)
+    u = a.view(np.uint32)
+    r = (u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) & np.uint32(0xFFFF0000)
+    return r.view(F32)
+
+
+def _stats(Y):
+    """Batch mean and biased variance per column, fp64 accumulation (the HIP finalisation
+    merges fp32 partials in fp64)."""
+    mean = Y.mean(axis=0, dtype=np.float64)
+    var = np.zeros(Y.shape[1], np.float64)
+    step = 1 << 18
+    for i in range(0, Y.shape[0], step):
+        d = Y[i:i + step].astype(np.float64) - mean
+        var += (d * d).sum(axis=0)
+    return mean, var / Y.shape[0]
+
+
+def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P):
+    """One reference training step (without the optimizer).  Returns (loss, grads) with
+    grads keyed by state-dict parameter name (float64 arrays); conv biases that BN cancels
+    are returned as zeros (analytically ~0 in every path)."""
+    R = round_bf16 if store == "bf16" else (lambda a: np.ascontiguousarray(a, dtype=F32))
+    B, N, D = x.shape
+    M = B * N
+    X = x.reshape(M, D).astype(F32)
+    W = {n: _w(sd, n, F32) for n in ("conv1", "conv2", "conv3", "conv4", "conv5", "global_feat",
+                                    "seg_conv1", "seg_conv2", "seg_conv3", "seg_conv4")}
+    Wr = {n: R(W[n]) for n in ("conv2", "conv3", "conv4", "conv5", "global_feat", "seg_conv2", "seg_conv3")}
+    Wr["seg_conv1_l"] = R(W["seg_conv1"][:, :64])
+    Wg1 = np.ascontiguousarray(W["seg_conv1"][:, 64:])     # global half: fp32 (pcs_scene_gemv)
+    gam = {bn: sd[f"{bn}.weight"].astype(np.float64) for bn in
+           ("bn1", "bn2", "bn3", "bn4", "bn5", "bn_global", "bn_seg1", "bn_seg2", "bn_seg3")}
+    bet = {bn: sd[f"{bn}.bias"].astype(np.float64) for bn in gam}
+    keep = 1.0 / (1.0 - p)
+    k1 = masks[0].astype(F32) * F32(keep)
+    k2 = masks[1].astype(F32) * F32(keep)
+    cache = {}
+
+    def bn_coef(bn, mean, var):
+        rstd = 1.0 / np.sqrt(var + BN_EPS)
+        scale = gam[bn] * rstd
+        shift = bet[bn] - mean * scale
+        cache[bn] = (mean, rstd)
+        return scale.astype(F32), shift.astype(F32)
+
+    def act(Y, bn, k=None):
+        s, t = cache[bn + "_st"]
+        a = np.maximum(Y * s + t, F32(0))
+        return a * k if k is not None else a
+
+    def layer(A, bn, Wt):
+        Y = R(A @ Wt.T)                                  # stored pre-BN (bias cancels in BN)
+        cache[bn + "_st"] = bn_coef(bn, *_stats(Y))
+        return Y
+
+    # ---------------- forward (P:103-131)
+    Y1 = R(X @ W["conv1"].T)
+    cache["bn1_st"] = bn_coef("bn1", *_stats(Y1))
+    Y2 = layer(R(act(Y1, "bn1")), "bn2", Wr["conv2"])
+    A2 = R(act(Y2, "bn2"))                               # point_feat (conv3 / seg_conv1 input)
+    Y3 = layer(A2, "bn3", Wr["conv3"])
+    A3 = R(act(Y3, "bn3"))
+    Y4 = layer(A3, "bn4", Wr["conv4"])
+    A4 = R(act(Y4, "bn4"))
+    y5 = A4 @ Wr["conv5"].T                              # fp32 accumulators
+    cache["bn5_st"] = bn_coef("bn5", *_stats(y5))
+    a5 = R(act(y5, "bn5"))
+    del y5
+    yg = a5 @ Wr["global_feat"].T
+    mg, vg = _stats(yg)
+    sg, tg = bn_coef("bn_global", mg, vg)
+    cache["bn_global_st"] = (sg, tg)
+    zg = (yg * sg + tg).reshape(B, N, -1)
+    idx = zg.argmax(axis=1)                              # first max of relu(bn(y)) (P:114)
+    g = np.maximum(np.take_along_axis(zg, idx[:, None, :], 1)[:, 0, :], 0).astype(np.float64)
+    ysel = np.take_along_axis(yg.reshape(B, N, -1), idx[:, None, :], 1)[:, 0, :].astype(np.float64)
+    del yg, zg
+    sb = g @ Wg1.T.astype(np.float64)                    # per-scene bias (P:117-123), centred
+    sb -= sb.mean(axis=0)
+    Ys1 = R((A2 @ Wr["seg_conv1_l"].T).reshape(B, N, -1) + sb[:, None, :].astype(F32)).reshape(M, -1)
+    cache["bn_seg1_st"] = bn_coef("bn_seg1", *_stats(Ys1))
+    As1 = R(act(Ys1, "bn_seg1", k1))
+    Ys2 = layer(As1, "bn_seg2", Wr["seg_conv2"])
+    As2 = R(act(Ys2, "bn_seg2", k2))
+    Ys3 = layer(As2, "bn_seg3", Wr["seg_conv3"])
+    as3 = act(Ys3, "bn_seg3")                            # head: fp32
+    logits = as3 @ W["seg_conv4"].T + sd["seg_conv4.bias"].astype(F32)
+
+    # ---------------- weighted CE (P:216, P:251)
+    y = labels.reshape(-1)
+    valid = y >= 0
+    ys = np.where(valid, y, 0)
+    z = logits.astype(np.float64)
+    mx = z.max(axis=1, keepdims=True)
+    e = np.exp(z - mx)
+    se = e.sum(axis=1, keepdims=True)
+    wv = np.where(valid, np.asarray(weight, np.float64)[ys], 0.0)
+    den = wv.sum()
+    loss = float((wv * (mx[:, 0] + np.log(se[:, 0]) - z[np.arange(M), ys])).sum() / den)
+    dl = e / se
+    dl[np.arange(M), ys] -= 1.0
+    dl = (dl * (wv / den)[:, None]).astype(F32)
+    del e, z
+
+    # ---------------- backward (P:254)
+    grads = {}
+    grads["seg_conv4.weight"] = (dl.T.astype(np.float64) @ as3)[:, :, None]
+    grads["seg_conv4.bias"] = dl.sum(axis=0, dtype=np.float64)
+    dA = dl @ W["seg_conv4"]
+
+    def bn_back(dA, Y, bn, k=None):
+        """dZ after ReLU (and dropout) -> stored R(dZ); S1/S2 from fp32; dy = R(alpha dZ + beta
+        + gamma Y) in the GEMM operand dtype.  Also returns dy before rounding (pool sums)."""
+        mean, rstd = cache[bn]
+        s, t = cache[bn + "_st"]
+        pos = (Y * s + t) > 0
+        dz = np.where(pos, dA * k if k is not None else dA, F32(0))
+        xh = ((Y.astype(np.float64) - mean) * rstd)
+        S1 = dz.sum(axis=0, dtype=np.float64)
+        S2 = (dz * xh).sum(axis=0)
+        grads[f"{bn}.weight"], grads[f"{bn}.bias"] = S2, S1
+        al = gam[bn] * rstd
+        dy = (al * (R(dz).astype(np.float64) - S1 / M - xh * (S2 / M))).astype(F32)
+        return dy, S1, S2
+
+    def conv_back(conv, dy, Ain, Wt, need_dx=True):
+        dyr = R(dy)
+        grads[f"{conv}.weight"] = (dyr.T.astype(np.float64) @ Ain)[:, :, None]
+        grads[f"{conv}.bias"] = np.zeros(dy.shape[1])
+        return dyr @ Wt if need_dx else None
+
+    dy, _, _ = bn_back(dA, Ys3, "bn_seg3")
+    dA = conv_back("seg_conv3", dy, As2, Wr["seg_conv3"])
+    dy, _, _ = bn_back(dA, Ys2, "bn_seg2", k2)
+    dA = conv_back("seg_conv2", dy, As1, Wr["seg_conv2"])
+    dys1, _, _ = bn_back(dA, Ys1, "bn_seg1", k1)
+    del dA
+    # seg_conv1 = local GEMM + per-scene global GEMV: dW = [dy^T A2 | sum_b csum_b g_b^T]
+    dyr = R(dys1)
+    dWl = dyr.T.astype(np.float64) @ A2
+    csum = dys1.reshape(B, N, -1).sum(axis=1, dtype=np.float64)    # fp32 sums (pcs_pool_bwd)
+    grads["seg_conv1.weight"] = np.concatenate([dWl, csum.T @ g], axis=1)[:, :, None]
+    grads["seg_conv1.bias"] = np.zeros(dys1.shape[1])
+    dA2 = R(dyr @ Wr["seg_conv1_l"])                                  # stored (conv3 addend)
+    del dys1, dyr
+    # max-pool + bn_global backward (sparse rows), folded dA5 = a5 H + c + sparse
+    dg = csum @ Wg1.astype(np.float64)                                # [B, 1024]
+    mean, rstd = cache["bn_global"]
+    sgl, tgl = cache["bn_global_st"]
+    dzs = np.where(ysel * sgl + tgl > 0, dg, 0.0)
+    xs = (ysel - mean) * rstd
+    S1 = dzs.sum(axis=0)
+    S2 = (dzs * xs).sum(axis=0)
+    grads["bn_global.weight"], grads["bn_global.bias"] = S2, S1
+    al = gam["bn_global"] * rstd
+    gc = -al * rstd * S2 / M
+    bc = -al * S1 / M - gc * mean
+    Wgr = Wr["global_feat"].astype(np.float64)
+    H = R((Wgr.T * gc) @ Wgr)
+    cvec = (Wgr.T @ bc).astype(F32)
+    dA5 = a5 @ H + cvec
+    rows = idx + (np.arange(B) * N)[:, None]
+    sp = al * dzs                                                     # [B, 1024]
+    Wg32 = W["global_feat"].astype(np.float64)
+    for b in range(B):
+        np.add.at(dA5, rows[b], (sp[b][:, None] * Wg32).astype(F32))
+    dz5 = np.where(a5 > 0, dA5, F32(0))
+    del dA5
+    S1_5 = dz5.sum(axis=0, dtype=np.float64)
+    DZ5 = R(dz5)
+    del dz5
+    G5 = (a5.T @ a5).astype(np.float64)                               # fp32 accumulation
+    S5 = a5.sum(axis=0, dtype=np.float64)
+    dWg = np.outer(bc, S5) + (gc[:, None] * Wgr) @ G5
+    for b in range(B):                                                # the max-pool rows
+        dWg += sp[b][:, None] * a5[rows[b]].astype(np.float64)
+    grads["global_feat.weight"] = dWg[:, :, None]
+    grads["global_feat.bias"] = np.zeros(1024)
+    del G5
+    # conv5 folded backward (R = dz5^T a4 gives S2 and the alpha term of dW5)
+    mean, rstd = cache["bn5"]
+    Rm = DZ5.T.astype(np.float64) @ A4                                 # [1024, 128]
+    W5r = Wr["conv5"].astype(np.float64)
+    mu_y = mean
+    S2_5 = rstd * ((W5r * Rm).sum(axis=1) - mu_y * S1_5)
+    grads["bn5.weight"], grads["bn5.bias"] = S2_5, S1_5
+    al5 = gam["bn5"] * rstd
+    ga5 = -al5 * rstd * S2_5 / M
+    be5 = -al5 * S1_5 / M - ga5 * mean
+    Ws = R(al5[:, None] * W5r)
+    h4 = R((W5r.T * ga5) @ W5r)
+    c5 = (W5r.T @ be5).astype(F32)
+    dA4 = R(DZ5 @ Ws + c5) + A4 @ h4
+    del DZ5
+    G4 = A4.T.astype(np.float64) @ A4
+    S4 = A4.sum(axis=0, dtype=np.float64)
+    grads["conv5.weight"] = (al5[:, None] * Rm + np.outer(be5, S4) + (ga5[:, None] * W5r) @ G4)[:, :, None]
+    grads["conv5.bias"] = np.zeros(1024)
+    dy, _, _ = bn_back(dA4, Y4, "bn4")
+    dA = conv_back("conv4", dy, A3, Wr["conv4"])
+    dy, _, _ = bn_back(dA, Y3, "bn3")
+    dA = conv_back("conv3", dy, A2, Wr["conv3"]) + dA2
+    dy, _, _ = bn_back(dA, Y2, "bn2")
+    A1 = R(act(Y1, "bn1"))
+    dA = conv_back("conv2", dy, A1, Wr["conv2"])
+    mean, rstd = cache["bn1"]
+    s, t = cache["bn1_st"]
+    dz = np.where((Y1 * s + t) > 0, dA, F32(0))
+    xh = (Y1.astype(np.float64) - mean) * rstd
+    S1 = dz.sum(axis=0, dtype=np.float64)
+    S2 = (dz * xh).sum(axis=0)
+    grads["bn1.weight"], grads["bn1.bias"] = S2, S1
+    dy = gam["bn1"] * rstd * (R(dz).astype(np.float64) - S1 / M - xh * (S2 / M))   # conv1 wgrad: fp32 dy
+    grads["conv1.weight"] = (dy.T @ X.astype(np.float64))[:, :, None]
+    grads["conv1.bias"] = np.zeros(64)
+    return loss, grads

@@ -289,6 +289,14 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                                                                          acc[i0 + i][j0 + j], 0, 0, 0);
   };
 
+  // A/B experiment knob (flags bits 8..15): delay workgroup L's start by ((7 L) mod 16) x
+  // knob x 512 cycles, spreading the workgroups' epilogues (and their store bursts) over a
+  // row tile's K-loop instead of all landing at once
+  if (const int stag = (a.flags >> 8) & 0xff) {
+    const int slot = (L * 7) & 15;
+    for (int i = 0; i < slot * stag; ++i) __builtin_amdgcn_s_sleep(8);
+  }
+
   // ---- prologue: K-tile 0 landed; A-lo, B-lo, B-hi of K-tile 1 in flight
   issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
   issue(1, 0); issue(1, 2); issue(1, 3);
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
     read_a(buf, 0);
     read_b(buf, 2, 0);
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
+    if (MODE == MODE_DGRAD && !(a.flags & (1 << 17)) && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
     issue(qs + 1, 1);
     // every counted wait assumes the five regions issued after the one it retires are in
     // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
@@ -336,7 +344,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
+    if (MODE == MODE_DGRAD && !(a.flags & (1 << 17)) && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
     issue(qs + 2, 2);
     wait_lgkm0();
     barrier_raw();
@@ -530,7 +538,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
             pk[2 * q][h] = sw[0];
             pk[2 * q + 1][h] = sw[1];
           }
-          if (ok)
+          if (ok && !(a.flags & (1 << 16)))
             // plain store: dz5 is re-read right away by conv5's backward (nt measured 1 ms slower)
             *reinterpret_cast<u32x4 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + scol + 32 * q) =
                 mk_u32x4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);

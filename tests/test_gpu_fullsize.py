@@ -6,13 +6,16 @@ the oracle at small sizes (test_gpu_parity) -- through size-independent properti
 * logits: argmax agreement > 95 % and norm-relative error < 0.1 (the bf16 bound of
   test_gpu_parity's bf16 case);
 * one training step (same weights, same Philox dropout seed): losses within 1e-2, BN running
-  statistics within 2e-2, and per-tensor gradient cosine similarity > 0.95 for every layer
-  after the max-pool (seg_conv1..4, bn_seg1..3).  Layers before the pool are only required
-  to stay positively correlated (1 - cos < 0.6): their gradient reaches them through
-  per-scene sums of the dense BN-backward of seg_conv1 (and the sparse pool rows), which
-  cancel to O(pool rows / points) of their size, so bf16 storage noise (2^-9 per element,
-  growing ~sqrt(N)) dominates at 2M points per scene (1 - cos 0.2-0.5 measured at cfg2,
-  0.1 at 4K points; tools/bf16_scaling.py).  bn_global.bias is skipped: its
+  statistics within 2e-2, and per-tensor gradient cosine similarity for every layer
+  after the max-pool (seg_conv1..4, bn_seg1..3; 1 - cos <= 0.03, measured r02 0.0218).
+  Layers before the pool get their gradient through per-scene sums of the dense
+  BN-backward of seg_conv1 (and the sparse pool rows), which cancel to O(pool rows / points)
+  of their size, so bf16 storage noise (2^-9 per element, growing ~sqrt(N)) dominates at
+  2M points per scene: 1 - cos measured r02 up to 0.496 (conv2).  That this is what bf16
+  storage costs and not a kernel error is shown at 4K-262K points per scene, where a numpy
+  bf16-storage emulation can run: the HIP error / emulated error ratio is 0.88-1.11 for
+  every tensor (test_gpu_bf16_storage.py, profiles/bf16_emulation_r02.md).  Bound: the
+  measured value times 1.13, the top of that ratio spread: 1 - cos <= 0.56.  bn_global.bias is skipped: its
   gradient is W^T sum_b csum_b with sum_b csum_b = 0 (BN input gradients sum to zero),
   i.e. analytically ~0 like the BN-cancelled conv biases;
 * the 2^21-row scenes exercise the chunk geometry, the 256-row tiles and the fused kernels at
@@ -96,7 +99,7 @@ def test_cfg2_bf16_train_step_tracks_fp32(cfg2_batch):
         worst[n] = 1 - float(a @ b / (a.norm() * b.norm() + 1e-30))
     print("cfg2 bf16 gradient 1-cos:", {k: round(v, 4) for k, v in worst.items()})
     post_pool = ("seg_conv", "bn_seg")
-    bad = {k: v for k, v in worst.items() if v > (0.05 if k.startswith(post_pool) else 0.6)}
+    bad = {k: v for k, v in worst.items() if v > (0.03 if k.startswith(post_pool) else 0.56)}
     assert not bad, bad
     for n in b32:
         e = float((b16[n] - b32[n]).norm() / b32[n].norm())

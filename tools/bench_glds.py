@@ -53,7 +53,8 @@ def main():
             keep["pool"] = torch.empty(nch, Nc, 4, device=dev)
         kw.update(keep)
         a.A, a.W = A.data_ptr(), W.data_ptr()
-        a.C = kw.pop("C").data_ptr() if "C" in kw else None
+        cc = kw.pop("C", None)
+        a.C = cc.data_ptr() if cc is not None else None
         if kw.pop("sparse", False):
             a.pool_idx, a.pool_coef, a.pool_w, a.pool_ldw, a.pool_c = am.data_ptr(), sp.data_ptr(), Wsp.data_ptr(), Nc, K
         for k, v in kw.items():
@@ -61,6 +62,23 @@ def main():
         ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
         print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
 
+    if os.environ.get("GLDS_PARTS"):   # dgrad epilogue parts (experiment flag bits 16/17)
+        for rep in range(2):
+            run("[dgrad] full", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True, sparse=True)
+            run("[dgrad] no stores", L.EPI_DGRAD, 1 << 16, C=C, Yp=A, bias=c, stats=True, sparse=True)
+            run("[dgrad] no mask extraction", L.EPI_DGRAD, 1 << 17, C=C, Yp=A, bias=c, stats=True, sparse=True)
+            run("[dgrad] neither", L.EPI_DGRAD, 3 << 16, C=C, Yp=A, bias=c, stats=True, sparse=True)
+            run("[dgrad] neither, no S1/sparse", L.EPI_DGRAD, 3 << 16, C=C, Yp=A)
+            run("[fwd] no epilogue work", L.EPI_FWD, 0, es=gsign)
+        return
+    if os.environ.get("GLDS_STAGGER"):   # A/B of the start-stagger knob, interleaved, one process
+        for rep in range(3):
+            for st in (0, 3, 7, 14):
+                fl = st << 8
+                run(f"[stagger {st:2d}] fwd, no epilogue work", L.EPI_FWD, fl, es=gsign)
+                run(f"[stagger {st:2d}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True, es=gsign)
+                run(f"[stagger {st:2d}] dgrad full", L.EPI_DGRAD, fl, C=C, Yp=A, bias=c, stats=True, sparse=True)
+        return
     for fl, tag in ((0, "glds"), (L.FLAG_NO_GLDS, "big ")):
         run(f"[{tag}] fwd, no epilogue work", L.EPI_FWD, fl, es=gsign)
         run(f"[{tag}] fwd + stats", L.EPI_FWD, fl, stats=True, es=gsign)
