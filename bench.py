@@ -38,7 +38,7 @@ LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (
 
 # bench tag -> HIP kernel symbol (as summarised from rocprofv3 in profiles/pmc_<round>.json)
 TAG_KERNEL = {
-    "wgrad:global_feat": "wgrad_big_kernel<1, false, true>",   # Gram a5^T a5 (upper tiles)
+    "wgrad:global_feat": "gram_glds_kernel",                   # LDS-DMA Gram a5^T a5 (upper tiles)
     "fwd:global_feat": "gemm_glds_kernel<0>",                  # LDS-DMA: BN stats + max-pool epilogue
     "dgrad:global_feat": "gemm_glds_kernel<1>",                # LDS-DMA: folded a5 H, mask, sparse rows
 }

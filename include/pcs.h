@@ -57,7 +57,9 @@ enum {
                         S1 = sum dz, S2 = sum dz*(Yp-mean)*rstd (0 when erstd is NULL)      */
   PCS_EPI_RAW = 2,   /* store acc                                                          */
   PCS_EPI_BNRELU = 3 /* y = acc + bias; store relu(y*es + et): the BN+ReLU of this layer
-                        applied on the way out, from a finished statistics pass (P:106-110) */
+                        applied on the way out, from a finished statistics pass (P:106-110);
+                        with stats (bf16 256-wide kernel only): per-chunk column sums of the
+                        stored output as (sum, 0) pairs                                     */
 };
 
 /*
@@ -326,6 +328,17 @@ int64_t pcs_gram_workspace(int64_t num_scenes, int64_t scene_rows, int32_t C, in
 int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, int64_t scene_rows,
              int32_t C, int32_t dtype, int32_t splits_per_scene, float *workspace, float *G,
              float *colsum, pcs_stream_t stream);
+
+/*
+ * Gram G = A^T A [C, C] of a stored bf16 activation A [M, C] (C % 256 == 0) on the LDS-DMA
+ * pipeline (csrc/gram_glds.hip): upper 256-tiles, persistent one-workgroup-per-CU grid over
+ * equal (tile, 64-row step) ranges, fp32 partial tiles summed in a fixed order, lower tiles
+ * mirrored.  No column sums (the bf16 path takes them from conv5's BN+ReLU epilogue).
+ * pcs_gram_raw_workspace returns the fp32 workspace bytes (2 tiles per CU).
+ */
+int64_t pcs_gram_raw_workspace(int64_t M, int32_t C);
+int pcs_gram_raw(const void *A, int64_t M, int32_t C, float *workspace, int64_t workspace_bytes, float *G,
+                 pcs_stream_t stream);
 
 /*
  * Weight gradient of a BN-fed layer from the Gram of its input a (G, S from pcs_gram):

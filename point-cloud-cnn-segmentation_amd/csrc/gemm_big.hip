@@ -44,7 +44,7 @@ template <int PRO, int EPI> struct Lay {
   static constexpr int BITS = COEF + NC * KMAX * 4;
   static constexpr int ECOEF = BITS + (PRO == PCS_PRO_BWD_POOL ? 32 : 0);
   static constexpr int RUN = ECOEF + (EPI == PCS_EPI_DGRAD ? 4 * BN * 4 : 0);
-  static constexpr int BYTES = RUN + (EPI == PCS_EPI_FWD ? 6 * BN * 4 : EPI == PCS_EPI_DGRAD ? 2 * BN * 4 : 0);
+  static constexpr int BYTES = RUN + (EPI == PCS_EPI_FWD ? 6 * BN * 4 : (EPI == PCS_EPI_DGRAD || EPI == PCS_EPI_BNRELU) ? 2 * BN * 4 : 0);
   static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   float *cf = reinterpret_cast<float *>(lds + LY::COEF);
   uint32_t *tbits = reinterpret_cast<uint32_t *>(lds + LY::BITS);
   float *ecf = reinterpret_cast<float *>(lds + LY::ECOEF);   // DGRAD: es | et | emean | erstd
-  float *run = reinterpret_cast<float *>(lds + LY::RUN);     // mean|m2|max|maxi|min|mini or S1|S2
+  float *run = reinterpret_cast<float *>(lds + LY::RUN);     // mean|m2|max|maxi|min|mini, S1|S2 or colsum
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -123,6 +123,8 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       run[tid] = 0.f; run[BN + tid] = 0.f;
       run[2 * BN + tid] = -__builtin_huge_valf(); run[3 * BN + tid] = __int_as_float(0x7fffffff);
       run[4 * BN + tid] = __builtin_huge_valf(); run[5 * BN + tid] = __int_as_float(0x7fffffff);
+    } else if constexpr (EPI == PCS_EPI_BNRELU) {
+      run[tid] = 0.f; run[BN + tid] = 0.f;
     }
   }
   float run_n = 0.f;   // rows merged into the running statistics so far (uniform)
@@ -425,19 +427,29 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
           }
         }
       }
-    } else {  // RAW
+    } else {  // RAW / BNRELU
 #pragma unroll 4
       for (int p = 0; p < NPASS; ++p) {
         const int rr = er0 + RPP * p;
-        if (rr < valid)
-          st16(Cg + (row_base + rr) * Ncols + ecol, *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16));
+        if (rr < valid) {
+          const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
+          st16(Cg + (row_base + rr) * Ncols + ecol, raw);
+          if constexpr (EPI == PCS_EPI_BNRELU) {
+            if (do_stats) {   // column sums of the stored (bf16-rounded) activation
+              float v[EPC];
+              unpack_chunk(raw, v);
+#pragma unroll
+              for (int e = 0; e < EPC; ++e) sa[e] += v[e];
+            }
+          }
+        }
       }
     }
     __syncthreads();   // the C tile has been consumed
 
     // per-tile merge of the per-thread partials into the running per-column accumulators
-    if ((EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD) && (do_stats || do_pool)) {
-      float2 *ps = reinterpret_cast<float2 *>(lds);                 // [RPP][BN] stats / S1,S2
+    if ((EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD || EPI == PCS_EPI_BNRELU) && (do_stats || do_pool)) {
+      float2 *ps = reinterpret_cast<float2 *>(lds);                 // [RPP][BN] stats / S1,S2 / colsum
       float4 *pp = reinterpret_cast<float4 *>(lds + RPP * BN * 8);  // [RPP][BN] pool
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
@@ -492,7 +504,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
   }
 
   // chunk end: this workgroup's per-column partials (same layout as gemm_nt)
-  if ((EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD) && tid < BN) {
+  if ((EPI == PCS_EPI_FWD || EPI == PCS_EPI_DGRAD || EPI == PCS_EPI_BNRELU) && tid < BN) {
     const int64_t o = (int64_t)chunk * Ncols + n0 + tid;
     if (do_stats) {
       float s2 = run[BN + tid];

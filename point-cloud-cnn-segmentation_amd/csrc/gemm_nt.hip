@@ -588,8 +588,11 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (a.epilogue < PCS_EPI_FWD || a.epilogue > PCS_EPI_BNRELU) return pcs_set_einval("pcs_gemm", "bad epilogue");
   if (a.epilogue == PCS_EPI_DGRAD && (!a.Yp || !a.C || !a.es != !a.et || (a.erstd && !a.emean)))
     return pcs_set_einval("pcs_gemm", "EPI_DGRAD needs Yp and C (es/et both or neither, emean with erstd)");
-  if (a.epilogue == PCS_EPI_BNRELU && (!a.es || !a.et || !a.C || a.stats || a.pool))
-    return pcs_set_einval("pcs_gemm", "EPI_BNRELU needs es, et and C (no statistics)");
+  if (a.epilogue == PCS_EPI_BNRELU && (!a.es || !a.et || !a.C || a.pool))
+    return pcs_set_einval("pcs_gemm", "EPI_BNRELU needs es, et and C (no pool)");
+  // EPI_BNRELU statistics = per-chunk column sums of the stored output (bf16 256-wide kernel)
+  if (a.epilogue == PCS_EPI_BNRELU && a.stats && !(wide_class(a) && pcs_gemm_big_applicable(a)))
+    return pcs_set_einval("pcs_gemm", "EPI_BNRELU column sums need the bf16 256-wide kernel (Ncols % 256 == 0)");
   if (a.pool && a.epilogue != PCS_EPI_FWD) return pcs_set_einval("pcs_gemm", "pool needs EPI_FWD");
   if (a.pool_w && (a.epilogue != PCS_EPI_DGRAD || a.prologue != PCS_PRO_RAW || !a.pool_idx || !a.pool_coef ||
                    a.pool_c <= 0 || a.pool_c > 1024 || a.pool_ldw < a.Ncols))

@@ -145,6 +145,7 @@ class Saved:
     logits: torch.Tensor = None
     wc: dict = None                               # cast weights used by this pass
     gram4: tuple = None                           # (G, S) of a4 when the forward computed it
+    a5_colsum: torch.Tensor = None                # bf16: per-chunk column sums of a5 (conv5 epilogue)
 
 
 class Engine:
@@ -263,6 +264,11 @@ class Engine:
         self._launch(tag, fn, ct.byref(a), self._stream())
         return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
+    def _raw_gram(self):
+        """bf16 wide-layer path: a5 is stored post-ReLU, so global_feat's Gram reads it raw
+        on the LDS-DMA kernel (pcs_gram_raw) with column sums from conv5's epilogue."""
+        return self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC)
+
     def _rounded(self, W):
         """fp32 copy of W as the forward's compute-dtype GEMM saw it (pcs_round_weight)."""
         if self.dt == L.F32:
@@ -366,8 +372,14 @@ class Engine:
                                          offset=P["conv5.bias"])
         a5 = self._empty(M, 1024, device=dev)
         c5 = sv.bn["bn5"]
+        # bf16: the epilogue also sums a5's columns per chunk (S of global_feat's Gram-form
+        # weight gradient; the LDS-DMA Gram kernel computes G only)
+        sv.a5_colsum = None
+        if train and self._raw_gram():
+            cps5c, _ = self.geometry(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU)
+            sv.a5_colsum = torch.empty(B * cps5c, 1024, 2, dtype=torch.float32, device=dev)
         self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU, sv.ys["conv4"], wc["conv5"][0], a5,
-                   es=c5.scale, et=c5.shift, tag="fwd:conv5", **bnrelu("bn4"))
+                   es=c5.scale, et=c5.shift, stats=sv.a5_colsum, tag="fwd:conv5", **bnrelu("bn4"))
         sv.ys["a5"] = a5
 
         # global_feat (P:113-114): a5 W^T with BN statistics and max-pool partials in the
@@ -642,14 +654,24 @@ class Engine:
         ones = torch.ones(1024, dtype=torch.float32, device=dev)
         zeros = torch.zeros(1024, dtype=torch.float32, device=dev)
         gram = torch.empty(1024, 1024, dtype=torch.float32, device=dev)
-        colsum = torch.empty(1024, dtype=torch.float32, device=dev)
-        sps = ct.c_int32(0)
-        nbytes = L.load().pcs_gram_workspace(B, N, 1024, self.dt, ct.byref(sps))
-        ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
-        raw = self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC)   # a5 is the activation itself
-        self._launch("wgrad:global_feat", "pcs_gram", L.ptr(a5), None if raw else L.ptr(ones),
-                     None if raw else L.ptr(zeros), B, N, 1024, self.dt, sps.value, L.ptr(ws), L.ptr(gram),
-                     L.ptr(colsum), s)
+        if self._raw_gram() and sv.a5_colsum is not None:
+            # a5 is the activation itself: LDS-DMA Gram; S from conv5's per-chunk column sums
+            nbytes = L.load().pcs_gram_raw_workspace(M, 1024)
+            if nbytes < 0:
+                raise L.PcsError(L.load().pcs_last_error().decode())
+            ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            self._launch("wgrad:global_feat", "pcs_gram_raw", L.ptr(a5), M, 1024, L.ptr(ws), nbytes, L.ptr(gram), s)
+            cs2 = torch.empty(1024, 2, dtype=torch.float32, device=dev)
+            L.call("pcs_reduce_partials", L.ptr(sv.a5_colsum), sv.a5_colsum.shape[0], 2048, 1.0, L.ptr(cs2),
+                   2048, 2048, s)
+            colsum = cs2[:, 0].contiguous()
+        else:
+            colsum = torch.empty(1024, dtype=torch.float32, device=dev)
+            sps = ct.c_int32(0)
+            nbytes = L.load().pcs_gram_workspace(B, N, 1024, self.dt, ct.byref(sps))
+            ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
+            self._launch("wgrad:global_feat", "pcs_gram", L.ptr(a5), L.ptr(ones), L.ptr(zeros), B, N, 1024,
+                         self.dt, sps.value, L.ptr(ws), L.ptr(gram), L.ptr(colsum), s)
         self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg_r),
                      Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(a5),
                      L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.dt, None, None,

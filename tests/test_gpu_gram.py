@@ -93,3 +93,33 @@ def test_raw_gram_of_stored_activations(B, N, C):
     with pytest.raises(L.PcsError):   # the identity form needs the 256x256 kernel
         L.call("pcs_gram", L.ptr(A), None, None, B, N, 128, L.BF16, sps.value, L.ptr(ws), L.ptr(G),
                L.ptr(S), L.stream_ptr())
+
+
+@pytest.mark.parametrize("M", [8 * 128 ** 2 + 37, 1000, 64 * 3])
+def test_gram_raw_lds_dma_matches_torch(M):
+    """pcs_gram_raw (csrc/gram_glds.hip): the LDS-DMA Gram of a stored bf16 activation, over
+    balanced (tile, 64-row step) ranges (ranges spanning two tiles, fewer steps than
+    workgroups, a tail of M % 64 rows), is a^T a of the bf16 values; repeated launches are
+    bitwise identical."""
+    import pcs_amd._lib as L
+    C = 1024
+    g = torch.Generator().manual_seed(M)
+    A = torch.relu(torch.randn(M, C, generator=g)).to(torch.bfloat16).to(DEV)
+    A[:, 5] = 0   # an all-zero column
+    nbytes = L.load().pcs_gram_raw_workspace(M, C)
+    assert nbytes > 0
+    ws = torch.empty(nbytes // 4, device=DEV)
+    outs = []
+    for _ in range(3):
+        G = torch.full((C, C), float("nan"), device=DEV)
+        L.call("pcs_gram_raw", L.ptr(A), M, C, L.ptr(ws), nbytes, L.ptr(G), L.stream_ptr())
+        outs.append(G)
+    torch.cuda.synchronize()
+    ref = A.double().T @ A.double()
+    G = outs[0]
+    assert torch.isfinite(G).all()
+    err = float((G.double() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
+    assert torch.equal(G, G.T)
+    for o in outs[1:]:
+        assert torch.equal(o, G)

@@ -71,6 +71,25 @@ def main():
             run("[dgrad] neither, no S1/sparse", L.EPI_DGRAD, 3 << 16, C=C, Yp=A)
             run("[fwd] no epilogue work", L.EPI_FWD, 0, es=gsign)
         return
+    if os.environ.get("GLDS_GRAM"):   # Gram of a5: register-staged 256x256 vs LDS-DMA persistent
+        sps = ct.c_int32(0)
+        nb = lib.pcs_gram_workspace(B, N, K, L.BF16, ct.byref(sps))
+        ws = torch.empty(nb // 4, device=dev)
+        G = torch.empty(K, K, device=dev)
+        S = torch.empty(K, device=dev)
+        nb2 = lib.pcs_gram_raw_workspace(M, K)
+        ws2 = torch.empty(nb2 // 4, device=dev)
+        G2 = torch.empty(K, K, device=dev)
+        gfl = flops * 10 / 16
+        for rep in range(3):
+            ms = timeit(lambda: L.call("pcs_gram", L.ptr(A), None, None, B, N, K, L.BF16, sps.value, L.ptr(ws),
+                                       L.ptr(G), L.ptr(S), L.stream_ptr()))
+            print(f"[gram] register-staged (pcs_gram)                {ms:8.3f} ms  {gfl / ms / 1e9:8.1f} TF/s", flush=True)
+            ms = timeit(lambda: L.call("pcs_gram_raw", L.ptr(A), M, K, L.ptr(ws2), nb2, L.ptr(G2), L.stream_ptr()))
+            print(f"[gram] LDS-DMA persistent (pcs_gram_raw)         {ms:8.3f} ms  {gfl / ms / 1e9:8.1f} TF/s", flush=True)
+        torch.cuda.synchronize()
+        print("max |G - G2| / max |G|:", float((G - G2).abs().max() / G.abs().max()))
+        return
     if os.environ.get("GLDS_STAGGER"):   # A/B of the start-stagger knob, interleaved, one process
         for rep in range(3):
             for st in (0, 3, 7, 14):
