@@ -330,6 +330,17 @@ int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, 
              float *colsum, pcs_stream_t stream);
 
 /*
+ * The max-pool rows' term of global_feat's folded input gradient (autograd of P:114 at P:254),
+ * applied after a PCS_EPI_DGRAD pcs_gemm that ran without pool_w (the LDS-DMA kernel):
+ *   dz[m, n] += (Yp[m, n] > 0) * sum_{c : pool_idx[b, c] == m} pool_coef[b, c] pool_w[c, n]
+ * for every distinct argmax row m (global row index) of scene b; the same term is added to
+ * S1 (stats[.].x) of the scene's first chunk.  pool_idx / pool_coef: [B, pool_c].
+ */
+int pcs_pool_rows_add(void *dz, const void *Yp, int32_t dtype, int64_t num_scenes, int64_t scene_rows, int32_t Ncols,
+                      const int32_t *pool_idx, const float *pool_coef, const float *pool_w, int64_t pool_ldw,
+                      int32_t pool_c, float *stats, int32_t chunks_per_scene, pcs_stream_t stream);
+
+/*
  * Gram G = A^T A [C, C] of a stored bf16 activation A [M, C] (C % 256 == 0) on the LDS-DMA
  * pipeline (csrc/gram_glds.hip): upper 256-tiles, persistent one-workgroup-per-CU grid over
  * equal (tile, 64-row step) ranges, fp32 partial tiles summed in a fixed order, lower tiles

@@ -116,6 +116,7 @@ SIGNATURES = [
     ("pcs_abi_version", ct.c_int, []),
     ("pcs_gram_workspace", _i64, [_i64, _i64, _i32, _i32, ct.POINTER(_i32)]),
     ("pcs_gram", ct.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    ("pcs_pool_rows_add", ct.c_int, [_vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i32, _vp]),
     ("pcs_gram_raw_workspace", _i64, [_i64, _i32]),
     ("pcs_gram_raw", ct.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     ("pcs_gram_wgrad", ct.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,

@@ -3,9 +3,11 @@
 // the materialised a5 = relu(bn5(y5)) (no prologue transform, so the operand goes
 // HBM -> LDS without passing through registers):
 //   forward   y_g = a5 Wg^T            epilogue: BN statistics + max-pool partials (P:113-114)
-//   backward  dA5 = a5 H + c + sparse  with H = Wg^T diag(gamma_g) Wg, c = Wg^T beta_g
-//             (pcs_bn_fold), the max-pool rows added sparsely, the ReLU mask of bn5 read
-//             from the operand itself, S1 = sum dz per column (autograd of P:110-114, P:254)
+//   backward  dA5 = a5 H + c  with H = Wg^T diag(gamma_g) Wg, c = Wg^T beta_g (pcs_bn_fold),
+//             the ReLU mask of bn5 read from the operand itself, S1 = sum dz per column
+//             (autograd of P:110-114, P:254); the max-pool rows' sparse term is added after
+//             the kernel by pcs_pool_rows_add: an ordinary global load in this epilogue makes
+//             hipcc wait vmcnt(0), draining the LDS-DMA prefetch at every tile
 //
 // Structure (cdna_hip_programming.md §5, "The 256² 8-phase template"):
 // * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 outputs = 8 x 4 accumulators of
@@ -25,6 +27,8 @@
 //   LDS outside the staging area), so the next tile's first K-tiles load while it runs.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int THREADS = 512;
@@ -35,16 +39,12 @@ constexpr int STAGE_BYTES = 2 * KBUF;              // 128 KB
 constexpr int OFF_RUN = STAGE_BYTES;               // [2 wm][256] float2: (mean, m2) | (S1, 0)
 constexpr int OFF_BIAS = OFF_RUN + 2 * 256 * 8;    // [256] f32
 constexpr int OFF_RUNN = OFF_BIAS + 256 * 4;       // [2] f32: rows merged per wave half
-constexpr int OFF_SPI = OFF_RUNN + 16;             // [1024] i32: sparse rows, sorted (max-pool argmax)
-constexpr int OFF_SPC = OFF_SPI + 1024 * 4;        // [1024] f32: their coefficients
-constexpr int OFF_SPK = OFF_SPC + 1024 * 4;        // [1024] u16: their channel (row of pool_w)
-constexpr int OFF_UNI = OFF_SPK + 1024 * 2;        // 16 KB, per mode:
+constexpr int OFF_UNI = OFF_RUNN + 16;             // 16 KB, per mode:
 constexpr int OFF_POOL = OFF_UNI;                  //   FWD: [2][256] float4 max, argmax, min, argmin
 constexpr int OFF_SGN = OFF_UNI + 2 * 256 * 16;    //        [256] f32 +1 / -1 (pool keeps max / min)
 constexpr int OFF_MASK = OFF_UNI;                  //   DGRAD: 2 x [256 rows][8 words] ReLU mask bits
 constexpr int LDS_BYTES = OFF_UNI + 2 * 256 * 8 * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-constexpr int SPMAX = 1024;
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1 };
 
@@ -119,9 +119,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   float4 *runp = reinterpret_cast<float4 *>(lds + OFF_POOL);
   float *lbias = reinterpret_cast<float *>(lds + OFF_BIAS);
   float *runn = reinterpret_cast<float *>(lds + OFF_RUNN);
-  int *spi = reinterpret_cast<int *>(lds + OFF_SPI);
-  float *spc = reinterpret_cast<float *>(lds + OFF_SPC);
-  uint16_t *spk = reinterpret_cast<uint16_t *>(lds + OFF_SPK);
   float *lsgn = reinterpret_cast<float *>(lds + OFF_SGN);
   uint32_t *mbits = reinterpret_cast<uint32_t *>(lds + OFF_MASK);
 
@@ -150,7 +147,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first glds)
   const bool do_stats = a.stats != nullptr;
   const bool do_pool = MODE == MODE_FWD && a.pool != nullptr;
-  const bool sparse = MODE == MODE_DGRAD && a.pool_w != nullptr;
   if (tid < BN) {
     lbias[tid] = a.bias ? a.bias[n0 + tid] : 0.f;
 #pragma unroll
@@ -164,24 +160,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     }
   }
   if (tid < 2) runn[tid] = 0.f;
-  int nsp = 0, sp_next = 0;   // sparse (DGRAD): max-pool rows, first one not yet passed
-  if (sparse) {   // the scene's max-pool rows sorted by row (rank sort; staging LDS is free here)
-    nsp = a.pool_c;
-    int *tr = reinterpret_cast<int *>(lds);
-    for (int c = tid; c < nsp; c += THREADS) tr[c] = a.pool_idx[(int64_t)scene * nsp + c];
-    __syncthreads();
-    for (int c = tid; c < nsp; c += THREADS) {
-      const int r = tr[c];
-      int rank = 0;
-      for (int q = 0; q < nsp; ++q) {
-        const int rq = tr[q];
-        rank += rq < r || (rq == r && q < c);
-      }
-      spi[rank] = r;
-      spc[rank] = a.pool_coef[(int64_t)scene * nsp + c];
-      spk[rank] = (uint16_t)c;
-    }
-  }
   __syncthreads();
 
   // ---- glds: piece g of wave w covers region rows (2w+g)*8 .. +8; lane -> row +lane/8,
@@ -289,14 +267,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                                                                          acc[i0 + i][j0 + j], 0, 0, 0);
   };
 
-  // A/B experiment knob (flags bits 8..15): delay workgroup L's start by ((7 L) mod 16) x
-  // knob x 512 cycles, spreading the workgroups' epilogues (and their store bursts) over a
-  // row tile's K-loop instead of all landing at once
-  if (const int stag = (a.flags >> 8) & 0xff) {
-    const int slot = (L * 7) & 15;
-    for (int i = 0; i < slot * stag; ++i) __builtin_amdgcn_s_sleep(8);
-  }
-
   // ---- prologue: K-tile 0 landed; A-lo, B-lo, B-hi of K-tile 1 in flight
   issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
   issue(1, 0); issue(1, 2); issue(1, 3);
@@ -318,7 +288,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
     read_a(buf, 0);
     read_b(buf, 2, 0);
-    if (MODE == MODE_DGRAD && !(a.flags & (1 << 17)) && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
     issue(qs + 1, 1);
     // every counted wait assumes the five regions issued after the one it retires are in
     // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
@@ -344,7 +314,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
-    if (MODE == MODE_DGRAD && !(a.flags & (1 << 17)) && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
     issue(qs + 2, 2);
     wait_lgkm0();
     barrier_raw();
@@ -476,30 +446,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         run_n += (float)nvw;
       }
     } else {   // MODE_DGRAD
-      if (sparse) {   // the tile's max-pool rows (rare): tiles ascend, so a running pointer
-        while (sp_next < nsp && (int64_t)spi[sp_next] < rb) ++sp_next;
-        int p = sp_next;
-        for (; p < nsp && (int64_t)spi[p] < rb + valid; ++p) {
-          const int m = (int)((int64_t)spi[p] - rb) - wm * 128;   // row within this wave's half
-          if (m < 0 || m >= 128 || (m & 15) != lr) continue;
-          const float w = spc[p];
-          const float *wr = a.pool_w + (int64_t)spk[p] * a.pool_ldw + n0 + wn * 64 + 4 * lg;
-          float4 q[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(wr + j * 16);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (i != (m >> 4)) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              acc[i][j][0] = fmaf(w, q[j].x, acc[i][j][0]);
-              acc[i][j][1] = fmaf(w, q[j].y, acc[i][j][1]);
-              acc[i][j][2] = fmaf(w, q[j].z, acc[i][j][2]);
-              acc[i][j][3] = fmaf(w, q[j].w, acc[i][j][3]);
-            }
-          }
-        }
-      }
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
       const uint32_t *mrow = mbits + ((qs / nks) & 1) * 2048 + wn * 2;
       const bool full = valid == BM;   // uniform: only a scene's last tile is partial
@@ -513,6 +459,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       // 2h and 2h+1 leaves each lane 8 consecutive columns of tile j + (lg & 1), so every
       // store instruction writes 16 rows x 64 contiguous bytes instead of 16 x 32.
       const int scol = n0 + wn * 64 + 16 * (lg & 1) + 8 * (lg >> 1);
+      // masking: v = acc & (0 - bit) (v_bfe_i32 sign-extends the keep bit to a full mask)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const bool ok = full || ((rowok >> i) & 1u);
@@ -520,11 +467,12 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         uint32_t pk[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint32_t word = (j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg);
+          const int word = (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg));
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            v[r] = ((word >> r) & 1u) ? acc[i][j][r] : 0.f;
+            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
+            v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
             s1[j][r] += ok ? v[r] : 0.f;
           }
           pk[j][0] = pack2bf(v[0], v[1]);
@@ -538,7 +486,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
             pk[2 * q][h] = sw[0];
             pk[2 * q + 1][h] = sw[1];
           }
-          if (ok && !(a.flags & (1 << 16)))
+          if (ok)
             // plain store: dz5 is re-read right away by conv5's backward (nt measured 1 ms slower)
             *reinterpret_cast<u32x4 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + scol + 32 * q) =
                 mk_u32x4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
@@ -600,7 +548,7 @@ bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
   if (a.epilogue == PCS_EPI_FWD) return a.C == nullptr && a.scene_bias == nullptr && (!a.pool || a.es);
   if (a.epilogue == PCS_EPI_DGRAD)   // mask read from the operand itself, no S2, no addend
     return a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask &&
-           (!a.pool_w || a.pool_c <= SPMAX);
+           !a.pool_w;
   return false;
 }
 
@@ -611,6 +559,84 @@ int pcs_gemm_glds_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s
     hipLaunchKernelGGL((gemm_glds_kernel<MODE_FWD>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb);
   else
     hipLaunchKernelGGL((gemm_glds_kernel<MODE_DGRAD>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// pcs_pool_rows_add: the max-pool rows' term of global_feat's folded input gradient, after
+// the LDS-DMA kernel (which leaves it out, see the top of this file):
+//   dz[m, n] += (Yp[m, n] > 0) * sum_{c : idx[b, c] == m} coef[b, c] * Wp[c, n]
+// for every distinct argmax row m of scene b, and the same term summed into S1 of the scene's
+// first chunk.  One block per (scene, 256 columns), thread = column; the scene's (row,
+// channel) pairs are rank-sorted in LDS so equal rows are applied once, in a fixed order.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+constexpr int PR_MAXC = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, const T *__restrict__ Yp, int64_t N,
+                                                            int Ncols, const int32_t *__restrict__ idx,
+                                                            const float *__restrict__ coef, const float *__restrict__ Wp,
+                                                            int64_t ldw, int P, float *__restrict__ stats, int cps) {
+  __shared__ int rows[PR_MAXC], srow[PR_MAXC];
+  __shared__ int sch[PR_MAXC];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int n = blockIdx.x * 256 + tid;
+  for (int c = tid; c < P; c += 256) rows[c] = idx[(int64_t)b * P + c];
+  __syncthreads();
+  for (int c = tid; c < P; c += 256) {   // stable rank sort by row
+    const int r = rows[c];
+    int rank = 0;
+    for (int q = 0; q < P; ++q) {
+      const int rq = rows[q];
+      rank += rq < r || (rq == r && q < c);
+    }
+    srow[rank] = r;
+    sch[rank] = c;
+  }
+  __syncthreads();
+  if (n >= Ncols) return;
+  float ds1 = 0.f, v = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const int c = sch[p];
+    v = fmaf(coef[(int64_t)b * P + c], Wp[(int64_t)c * ldw + n], v);
+    if (p + 1 == P || srow[p + 1] != srow[p]) {   // last pair of this row: apply
+      const int64_t o = (int64_t)srow[p] * Ncols + n;
+      if (load_elem(Yp, o) > 0.f) {
+        const float d = load_elem(dz, o) + v;
+        if constexpr (sizeof(T) == 2) dz[o] = (T)(pack2bf(d, 0.f) & 0xffffu);
+        else dz[o] = d;
+        ds1 += v;
+      }
+      v = 0.f;
+    }
+  }
+  if (stats) stats[((int64_t)b * cps * Ncols + n) * 2] += ds1;
+}
+
+}  // namespace
+
+extern "C" int pcs_pool_rows_add(void *dz, const void *Yp, int32_t dtype, int64_t num_scenes, int64_t scene_rows,
+                                 int32_t Ncols, const int32_t *pool_idx, const float *pool_coef, const float *pool_w,
+                                 int64_t pool_ldw, int32_t pool_c, float *stats, int32_t chunks_per_scene,
+                                 pcs_stream_t stream) {
+  if (!dz || !Yp || !pool_idx || !pool_coef || !pool_w || num_scenes <= 0 || scene_rows <= 0 || Ncols <= 0 ||
+      pool_c <= 0 || pool_c > PR_MAXC || pool_ldw < Ncols || (stats && chunks_per_scene <= 0))
+    return pcs_set_einval("pcs_pool_rows_add", "bad arguments (0 < pool_c <= 1024, pool_ldw >= Ncols)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((Ncols + 255) / 256, (unsigned)num_scenes);
+  if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(pool_rows_add_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<bf16_t *>(dz),
+                       static_cast<const bf16_t *>(Yp), scene_rows, (int)Ncols, pool_idx, pool_coef, pool_w, pool_ldw,
+                       (int)pool_c, stats, (int)chunks_per_scene);
+  else if (dtype == PCS_F32)
+    hipLaunchKernelGGL(pool_rows_add_kernel<float>, grid, dim3(256), 0, s, static_cast<float *>(dz),
+                       static_cast<const float *>(Yp), scene_rows, (int)Ncols, pool_idx, pool_coef, pool_w, pool_ldw,
+                       (int)pool_c, stats, (int)chunks_per_scene);
+  else
+    return pcs_set_einval("pcs_pool_rows_add", "bad dtype");
   PCS_CHECK_LAUNCH();
   return 0;
 }

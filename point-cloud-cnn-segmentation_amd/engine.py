@@ -645,9 +645,17 @@ class Engine:
         pc5 = sv.bn["bn5"]
         cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD)
         st5 = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
-        self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
-                   pool_idx=sv.am, pool_coef=sp, pool_w=Wg, pool_ldw=Wg.shape[1], pool_c=1024,
-                   stats=st5, tag="dgrad:global_feat")
+        if self.dt == L.BF16 and not (self.flags & (L.FLAG_GENERIC | L.FLAG_NO_GLDS)):
+            # LDS-DMA kernel without the max-pool rows (no ordinary global loads in its
+            # epilogue), then their sparse term (pcs_pool_rows_add)
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
+                       stats=st5, tag="dgrad:global_feat")
+            L.call("pcs_pool_rows_add", L.ptr(bufB), L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am), L.ptr(sp),
+                   L.ptr(Wg), Wg.shape[1], 1024, L.ptr(st5), cps5, s)
+        else:
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
+                       pool_idx=sv.am, pool_coef=sp, pool_w=Wg, pool_ldw=Wg.shape[1], pool_c=1024,
+                       stats=st5, tag="dgrad:global_feat")
         dz5 = bufB
         # global_feat weight gradient from the Gram of a5: the symmetric a5^T a5 (upper tiles)
         # + an O(C^3) assemble instead of the M x 1024 x 1024 GEMM

@@ -106,9 +106,15 @@ def test_folded_dgrad_sparse_mask_s1(variant, B, N, cps):
     st = torch.empty(nch, K, 2, device=DEV)
     out = torch.empty(B * N, K, dtype=tdt, device=DEV)
     a.A, a.W, a.C, a.Yp, a.bias = A.data_ptr(), H.data_ptr(), out.data_ptr(), A.data_ptr(), c.data_ptr()
-    a.pool_idx, a.pool_coef, a.pool_w, a.pool_ldw, a.pool_c = am.data_ptr(), sp.data_ptr(), Wsp.data_ptr(), K, Pc
     a.stats = st.data_ptr()
-    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    if variant == "glds":
+        # the LDS-DMA kernel leaves the max-pool rows to pcs_pool_rows_add
+        L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+        L.call("pcs_pool_rows_add", L.ptr(out), L.ptr(A), dt, B, N, K, L.ptr(am), L.ptr(sp), L.ptr(Wsp), K, Pc,
+               L.ptr(st), a.chunks_per_scene, L.stream_ptr())
+    else:
+        a.pool_idx, a.pool_coef, a.pool_w, a.pool_ldw, a.pool_c = am.data_ptr(), sp.data_ptr(), Wsp.data_ptr(), K, Pc
+        L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
     torch.cuda.synchronize()
     v = A.double() @ H.double().T + c.double()
     for b in range(B):

@@ -62,15 +62,6 @@ def main():
         ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
         print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
 
-    if os.environ.get("GLDS_PARTS"):   # dgrad epilogue parts (experiment flag bits 16/17)
-        for rep in range(2):
-            run("[dgrad] full", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True, sparse=True)
-            run("[dgrad] no stores", L.EPI_DGRAD, 1 << 16, C=C, Yp=A, bias=c, stats=True, sparse=True)
-            run("[dgrad] no mask extraction", L.EPI_DGRAD, 1 << 17, C=C, Yp=A, bias=c, stats=True, sparse=True)
-            run("[dgrad] neither", L.EPI_DGRAD, 3 << 16, C=C, Yp=A, bias=c, stats=True, sparse=True)
-            run("[dgrad] neither, no S1/sparse", L.EPI_DGRAD, 3 << 16, C=C, Yp=A)
-            run("[fwd] no epilogue work", L.EPI_FWD, 0, es=gsign)
-        return
     if os.environ.get("GLDS_GRAM"):   # Gram of a5: register-staged 256x256 vs LDS-DMA persistent
         sps = ct.c_int32(0)
         nb = lib.pcs_gram_workspace(B, N, K, L.BF16, ct.byref(sps))
@@ -90,21 +81,12 @@ def main():
         torch.cuda.synchronize()
         print("max |G - G2| / max |G|:", float((G - G2).abs().max() / G.abs().max()))
         return
-    if os.environ.get("GLDS_STAGGER"):   # A/B of the start-stagger knob, interleaved, one process
-        for rep in range(3):
-            for st in (0, 3, 7, 14):
-                fl = st << 8
-                run(f"[stagger {st:2d}] fwd, no epilogue work", L.EPI_FWD, fl, es=gsign)
-                run(f"[stagger {st:2d}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True, es=gsign)
-                run(f"[stagger {st:2d}] dgrad full", L.EPI_DGRAD, fl, C=C, Yp=A, bias=c, stats=True, sparse=True)
-        return
     for fl, tag in ((0, "glds"), (L.FLAG_NO_GLDS, "big ")):
         run(f"[{tag}] fwd, no epilogue work", L.EPI_FWD, fl, es=gsign)
         run(f"[{tag}] fwd + stats", L.EPI_FWD, fl, stats=True, es=gsign)
         run(f"[{tag}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True, es=gsign)
     run("[glds] dgrad: mask + store", L.EPI_DGRAD, 0, C=C, Yp=A)
     run("[glds] dgrad: mask + store + bias + S1", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True)
-    run("[glds] dgrad: + sparse rows", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True, sparse=True)
     run("[gen ] dgrad (generic kernel, FLAG_NO_GLDS)", L.EPI_DGRAD, L.FLAG_NO_GLDS, C=C, Yp=A, bias=c, stats=True,
         sparse=True)
 
