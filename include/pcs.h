@@ -30,12 +30,17 @@ extern "C" {
 
 typedef struct ihipStream_t *pcs_stream_t; /* == hipStream_t */
 
-enum { PCS_F32 = 0, PCS_BF16 = 1 };
+enum { PCS_F32 = 0, PCS_BF16 = 1, PCS_FP8 = 2 /* OCP e4m3fn, 1 byte (wide-layer operands only) */ };
 enum { PCS_OK = 0, PCS_EINVAL = -1000 };
 /* pcs_gemm_args.flags */
 enum {
   PCS_FLAG_GENERIC = 1, /* force the generic 128x{64,128} kernel (cross-checks)            */
-  PCS_FLAG_NO_GLDS = 2  /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
+  PCS_FLAG_NO_GLDS = 2, /* never pick the LDS-DMA 256x256 kernel (A/B timing, cross-checks) */
+  PCS_FLAG_AW_FP8 = 4,  /* A (and Yp) and W are fp8 e4m3 (dtype still names C, stats in fp32):
+                           W rows carry E8M0 scales in w_scale, A is unscaled; the LDS-DMA
+                           kernel runs v_mfma_scale_f32_16x16x128_f8f6f4 (K % 256 == 0; RAW
+                           prologue; FWD statistics / pool or DGRAD)                         */
+  PCS_FLAG_C_FP8 = 8    /* EPI_BNRELU of the bf16 256-wide kernel stores C as fp8 e4m3      */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
@@ -107,6 +112,7 @@ typedef struct {
   const float *pool_w;
   int64_t pool_ldw;
   int32_t pool_c;
+  const uint8_t *w_scale; /* [Ncols] E8M0 scale of each W row (PCS_FLAG_AW_FP8) */
 } pcs_gemm_args;
 
 /* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error.  The
@@ -330,26 +336,38 @@ int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, 
              float *colsum, pcs_stream_t stream);
 
 /*
+ * fp8 e4m3 (OCP) rows with one E8M0 scale per row, for the fp8 wide layer (MX-scaled MFMA
+ * operands whose 32-element blocks share the row's scale):
+ *   scale[r] = 127 + ceil(log2(max_k |W[r, k]| / 448)) (clamped to [1, 254]; 127 for a zero row)
+ *   Wq[r, k] = e4m3(W[r, k] * 2^(127 - scale[r]))   (round to nearest even, saturating)
+ * deq (optional, [rows, cols] fp32): the values the MFMA sees, Wq[r, k] * 2^(scale[r] - 127).
+ */
+int pcs_quant_fp8_rows(const float *W, int64_t rows, int64_t cols, int64_t ldw, uint8_t *Wq, uint8_t *scale,
+                       float *deq, pcs_stream_t stream);
+
+/*
  * The max-pool rows' term of global_feat's folded input gradient (autograd of P:114 at P:254),
  * applied after a PCS_EPI_DGRAD pcs_gemm that ran without pool_w (the LDS-DMA kernel):
  *   dz[m, n] += (Yp[m, n] > 0) * sum_{c : pool_idx[b, c] == m} pool_coef[b, c] pool_w[c, n]
  * for every distinct argmax row m (global row index) of scene b; the same term is added to
  * S1 (stats[.].x) of the scene's first chunk.  pool_idx / pool_coef: [B, pool_c].
  */
-int pcs_pool_rows_add(void *dz, const void *Yp, int32_t dtype, int64_t num_scenes, int64_t scene_rows, int32_t Ncols,
-                      const int32_t *pool_idx, const float *pool_coef, const float *pool_w, int64_t pool_ldw,
-                      int32_t pool_c, float *stats, int32_t chunks_per_scene, pcs_stream_t stream);
+int pcs_pool_rows_add(void *dz, int32_t dz_dtype, const void *Yp, int32_t yp_dtype, int64_t num_scenes,
+                      int64_t scene_rows, int32_t Ncols, const int32_t *pool_idx, const float *pool_coef,
+                      const float *pool_w, int64_t pool_ldw, int32_t pool_c, float *stats, int32_t chunks_per_scene,
+                      pcs_stream_t stream);
 
 /*
- * Gram G = A^T A [C, C] of a stored bf16 activation A [M, C] (C % 256 == 0) on the LDS-DMA
- * pipeline (csrc/gram_glds.hip): upper 256-tiles, persistent one-workgroup-per-CU grid over
- * equal (tile, 64-row step) ranges, fp32 partial tiles summed in a fixed order, lower tiles
- * mirrored.  No column sums (the bf16 path takes them from conv5's BN+ReLU epilogue).
- * pcs_gram_raw_workspace returns the fp32 workspace bytes (2 tiles per CU).
+ * Gram G = A^T A [C, C] of a stored activation A [M, C] (C % 256 == 0; dtype PCS_BF16, or
+ * PCS_FP8 for the e4m3 a5 of the fp8 path) on the LDS-DMA pipeline (csrc/gram_glds.hip):
+ * upper 256-tiles x row splits in one wave of workgroups (a split's tiles share its rows
+ * through one XCD's L2), fp32 partial tiles summed in a fixed order, lower tiles mirrored.
+ * Products are exact in fp32 for both dtypes.  No column sums (they come from conv5's BN+ReLU
+ * epilogue).  pcs_gram_raw_workspace returns the fp32 workspace bytes (one tile per workgroup).
  */
 int64_t pcs_gram_raw_workspace(int64_t M, int32_t C);
-int pcs_gram_raw(const void *A, int64_t M, int32_t C, float *workspace, int64_t workspace_bytes, float *G,
-                 pcs_stream_t stream);
+int pcs_gram_raw(const void *A, int64_t M, int32_t C, int32_t dtype, float *workspace, int64_t workspace_bytes,
+                 float *G, pcs_stream_t stream);
 
 /*
  * Weight gradient of a BN-fed layer from the Gram of its input a (G, S from pcs_gram):
@@ -359,7 +377,8 @@ int pcs_gram_raw(const void *A, int64_t M, int32_t C, float *workspace, int64_t 
  * reading y.  global_feat (P:113): R = NULL, dy from the max-pool (sp/am: pcs_pool_bwd /
  * pcs_pool_finalize; Y/s/t: stored conv5 output and bn5 scale/shift, a recomputed at the
  * argmax rows).  conv5 (P:110): R = dz^T a (pcs_wgrad with dy_mode RAW), sp = NULL.
- * W: fp32 [Cout, Cin] with row stride ldw_in; dW row stride ldw (multiple of 4).
+ * W: fp32 [Cout, Cin] with row stride ldw_in; dW row stride ldw (multiple of 4).  dtype names
+ * Y's storage (PCS_F32, PCS_BF16, or PCS_FP8 for the fp8 path's e4m3 a5).
  */
 int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_in,
                    const float *beta, const float *gamma, const float *sp, const int32_t *am,

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (loads torch's HIP runtime before libpcs.so)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "csrc", "libpcs.so")
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 PRO_RAW, PRO_BNRELU, PRO_BWD, PRO_BWD_POOL = 0, 1, 2, 3
 EPI_FWD, EPI_DGRAD, EPI_RAW, EPI_BNRELU = 0, 1, 2, 3
 HEAD_FWD, HEAD_CE, HEAD_BWD = 0, 1, 2
@@ -37,12 +37,14 @@ class GemmArgs(ct.Structure):
         ("c_mask", _vp), ("c_keep_scale", _f),
         ("Yp", _vp), ("es", _vp), ("et", _vp), ("emean", _vp), ("erstd", _vp),
         ("stats", _vp), ("pool", _vp), ("flags", _i32),
-        ("pool_w", _vp), ("pool_ldw", _i64), ("pool_c", _i32),
+        ("pool_w", _vp), ("pool_ldw", _i64), ("pool_c", _i32), ("w_scale", _vp),
     ]
 
 
 FLAG_GENERIC = 1
 FLAG_NO_GLDS = 2
+FLAG_AW_FP8 = 4
+FLAG_C_FP8 = 8
 
 
 class WgradArgs(ct.Structure):
@@ -116,9 +118,11 @@ SIGNATURES = [
     ("pcs_abi_version", ct.c_int, []),
     ("pcs_gram_workspace", _i64, [_i64, _i64, _i32, _i32, ct.POINTER(_i32)]),
     ("pcs_gram", ct.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
-    ("pcs_pool_rows_add", ct.c_int, [_vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i32, _vp]),
+    ("pcs_pool_rows_add", ct.c_int, [_vp, _i32, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i32,
+                                     _vp]),
+    ("pcs_quant_fp8_rows", ct.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     ("pcs_gram_raw_workspace", _i64, [_i64, _i32]),
-    ("pcs_gram_raw", ct.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+    ("pcs_gram_raw", ct.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp]),
     ("pcs_gram_wgrad", ct.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
                                   _i32, _vp, _vp, _vp, _i64, _vp]),
     ("pcs_bn_fold", ct.c_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),

@@ -80,6 +80,17 @@ PCS_DEV u32x4 pack_chunk(const float (&v)[8]) {
 PCS_DEV float load_elem(const float *p, int64_t i) { return p[i]; }
 PCS_DEV float load_elem(const bf16_t *p, int64_t i) { return bf2f(p[i]); }
 
+// fp8 e4m3 (OCP e4m3fn on gfx950): one storage byte
+typedef unsigned char fp8_t;
+PCS_DEV float fp82f(uint32_t byte) { return __builtin_amdgcn_cvt_f32_fp8((int)byte, 0); }
+PCS_DEV float load_elem(const fp8_t *p, int64_t i) { return fp82f(p[i]); }
+// four floats -> four e4m3 bytes (round to nearest even; the hardware conversion saturates)
+PCS_DEV uint32_t pack4fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
 // load EPC floats of a small per-channel coefficient vector (L1/L2 resident)
 template <int EPC>
 PCS_DEV void load_vec(const float *__restrict__ p, int k, float (&v)[EPC]) {

@@ -68,13 +68,15 @@ PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
 // LDS (staged once per workgroup: a workgroup's row chunk never leaves its scene), and rows
 // past the end of a scene are clamped rather than branched around (their outputs are never
 // stored), so the k-loop carries no exec-mask branches and no early vmcnt(0).
-// MASK: dropout keep bits of A (FWD prologue) or of C (DGRAD epilogue); ADD: DGRAD addend
+// MASK: dropout keep bits of A (FWD prologue) or of C (DGRAD epilogue); ADD: DGRAD addend,
+// or (BNRELU epilogue) an fp8 e4m3 output (PCS_FLAG_C_FP8)
 template <int PRO, int EPI, bool MASK, bool ADD>
 __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                            int tiles_per_chunk, int ncb) {
   constexpr int EPC = 8;
   constexpr bool AMASK = MASK && PRO == PCS_PRO_BNRELU;   // dropout bits of the A operand
   constexpr bool CMASK = MASK && EPI == PCS_EPI_DGRAD;    // dropout bits of the dgrad output
+  constexpr bool C8 = ADD && EPI == PCS_EPI_BNRELU;       // fp8 activation store
   typedef Lay<PRO, EPI> LY;
   __shared__ __attribute__((aligned(16))) char lds[LY::BYTES];
   float *cf = reinterpret_cast<float *>(lds + LY::COEF);
@@ -433,13 +435,29 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
         const int rr = er0 + RPP * p;
         if (rr < valid) {
           const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
-          st16(Cg + (row_base + rr) * Ncols + ecol, raw);
-          if constexpr (EPI == PCS_EPI_BNRELU) {
-            if (do_stats) {   // column sums of the stored (bf16-rounded) activation
-              float v[EPC];
-              unpack_chunk(raw, v);
+          if constexpr (C8) {   // fp8 e4m3 activation (8 B)
+            float v[EPC];
+            unpack_chunk(raw, v);
+            const uint32_t lo = pack4fp8(v[0], v[1], v[2], v[3]), hi = pack4fp8(v[4], v[5], v[6], v[7]);
+            __builtin_nontemporal_store((uint64_t)hi << 32 | lo,
+                                        reinterpret_cast<uint64_t *>(reinterpret_cast<fp8_t *>(a.C) +
+                                                                     (row_base + rr) * Ncols + ecol));
+            if (do_stats) {   // column sums of the stored (fp8-rounded) activation
 #pragma unroll
-              for (int e = 0; e < EPC; ++e) sa[e] += v[e];
+              for (int e = 0; e < 4; ++e) {
+                sa[e] += fp82f((lo >> (8 * e)) & 255u);
+                sa[4 + e] += fp82f((hi >> (8 * e)) & 255u);
+              }
+            }
+          } else {
+            st16(Cg + (row_base + rr) * Ncols + ecol, raw);
+            if constexpr (EPI == PCS_EPI_BNRELU) {
+              if (do_stats) {   // column sums of the stored (bf16-rounded) activation
+                float v[EPC];
+                unpack_chunk(raw, v);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) sa[e] += v[e];
+              }
             }
           }
         }
@@ -550,6 +568,7 @@ int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
     case PCS_EPI_BNRELU:
       if (g.prologue == PCS_PRO_RAW) return launch<PCS_PRO_RAW, PCS_EPI_BNRELU, false>(g, tps, tpc, s);
+      if (g.flags & PCS_FLAG_C_FP8) return launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, false, true>(g, tps, tpc, s);
       return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, true>(g, tps, tpc, s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, false>(g, tps, tpc, s);
     case PCS_EPI_DGRAD:

@@ -111,9 +111,17 @@ PCS_DEV int a_row(int hi, int q) { return (q & 63) + ((q >> 6) << 7) + (hi ? 64 
 PCS_DEV int b_row(int hi, int q) { return (q & 31) + ((q >> 5) << 6) + (hi ? 32 : 0); }
 PCS_DEV int swz(int q, int chunk) { return chunk ^ ((q >> 1) & 7); }
 
-template <int MODE>
+// FP8 (PCS_FLAG_AW_FP8): A and W are e4m3 bytes, a K-tile is 128 elements (the same 128-B
+// rows), one v_mfma_scale_f32_16x16x128_f8f6f4 replaces the two bf16 16x16x32 of a (i, j)
+// pair (2x the MFMA rate); each weight row's E8M0 scale is replicated into the four scale
+// bytes of every lane holding that row (the MX blocks of a row share it), A is unscaled.
+// Both operands use the same lane -> k map (32 consecutive bytes at k = 32 (lane >> 4)), which
+// is all a dot product over k needs.
+template <int MODE, bool FP8>
 __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int tiles_per_scene,
                                                             int tiles_per_chunk, int ncb) {
+  constexpr int ESZ = FP8 ? 1 : 2;
+  constexpr int KT = 128 / ESZ;                    // K per K-tile (128-byte LDS rows)
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   float2 *run = reinterpret_cast<float2 *>(lds + OFF_RUN);
   float4 *runp = reinterpret_cast<float4 *>(lds + OFF_POOL);
@@ -136,13 +144,18 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   const int t_begin = cis * tiles_per_chunk;
   const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
   if (t_begin >= t_end) return;   // uniform across the workgroup
-  const int nks = K / BK;
+  const int nks = K / KT;
   const int total = (t_end - t_begin) * nks;
   const int64_t row0 = (int64_t)scene * N + (int64_t)t_begin * BM;
   const int64_t scene_end = (int64_t)(scene + 1) * N;
   const char *Ab = reinterpret_cast<const char *>(a.A);
-  const char *Wb = reinterpret_cast<const char *>(a.W) + (int64_t)n0 * K * 2;
-  const int64_t rowbytes = (int64_t)K * 2;
+  const char *Wb = reinterpret_cast<const char *>(a.W) + (int64_t)n0 * K * ESZ;
+  const int64_t rowbytes = (int64_t)K * ESZ;
+  int wsc[4] = {0, 0, 0, 0};   // FP8: this lane's weight-row scales (rows wn*64 + j*16 + lr)
+  if constexpr (FP8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wsc[j] = (int)a.w_scale[n0 + wn * 64 + j * 16 + lr] * 0x01010101;
+  }
 
   // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first glds)
   const bool do_stats = a.stats != nullptr;
@@ -196,16 +209,29 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     }
   };
 
-  // ---- fragment reads (ds_read_b128 of the swizzled 16-B chunks)
-  bf16x8 af[4][2], bfr[4][2];
+  // ---- fragment reads (ds_read_b128 of the swizzled 16-B chunks): bf16 16x16x32 takes
+  // chunk kk*4 + lg for k-step kk; fp8 16x16x128 takes chunks 2 lg, 2 lg + 1 (32 bytes)
+  // bf16: two 4-dword fragments per (i) / (j), one per k-step; fp8: one 8-dword fragment
+  typedef int v8i __attribute__((ext_vector_type(8)));
+  u32x4 af[4][2], bfr[4][2];
+  v8i af8[4], bf8[4];
+  auto frag8 = [&](const char *p0, const char *p1) {
+    const u32x4 lo = *reinterpret_cast<const u32x4 *>(p0), hi = *reinterpret_cast<const u32x4 *>(p1);
+    return v8i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  auto chunk_of = [&](int kk) { return FP8 ? 2 * lg + kk : kk * 4 + lg; };
   auto read_a = [&](int buf, int region) {
     const char *base = lds + buf * KBUF + region * REG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = wm * 64 + i * 16 + lr;
+      if constexpr (FP8) {
+        af8[i] = frag8(base + q * 128 + swz(q, chunk_of(0)) * 16, base + q * 128 + swz(q, chunk_of(1)) * 16);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        af[i][kk] = *reinterpret_cast<const bf16x8 *>(base + q * 128 + swz(q, kk * 4 + lg) * 16);
+        for (int kk = 0; kk < 2; ++kk)
+          af[i][kk] = *reinterpret_cast<const u32x4 *>(base + q * 128 + swz(q, chunk_of(kk)) * 16);
+      }
     }
   };
   auto read_b = [&](int buf, int region, int j0) {
@@ -213,9 +239,13 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int q = wn * 32 + j * 16 + lr;
+      if constexpr (FP8) {
+        bf8[j0 + j] = frag8(base + q * 128 + swz(q, chunk_of(0)) * 16, base + q * 128 + swz(q, chunk_of(1)) * 16);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        bfr[j0 + j][kk] = *reinterpret_cast<const bf16x8 *>(base + q * 128 + swz(q, kk * 4 + lg) * 16);
+        for (int kk = 0; kk < 2; ++kk)
+          bfr[j0 + j][kk] = *reinterpret_cast<const u32x4 *>(base + q * 128 + swz(q, chunk_of(kk)) * 16);
+      }
     }
   };
   // DGRAD: the ReLU mask of bn5 comes from the operand (Yp == A, K == Ncols): the tile's
@@ -230,6 +260,21 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     const int t = a_row(region, q);
     const char *base = lds + buf * KBUF + region * REG + q * 128;
     uint32_t w = 0;
+    if constexpr (FP8) {   // 32 columns (bytes) per thread: x > 0 <=> sign clear, 7 low bits nonzero
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t x = v[d];
+          const uint32_t pos = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) & ~x & 0x80808080u;
+          const uint32_t nib = ((pos >> 7) & 1u) | ((pos >> 14) & 2u) | ((pos >> 21) & 4u) | ((pos >> 28) & 8u);
+          w |= nib << (c * 16 + d * 4);
+        }
+      }
+      mbits[par * 2048 + t * 8 + kq * 4 + h] = w;
+      return;
+    }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
@@ -260,11 +305,18 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (FP8) {
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              bf8[j0 + j], af8[i], acc[i0 + i][j0 + j], 0, 0, 0, wsc[j0 + j], 0, 0x7f7f7f7f);
+        } else {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j0 + j][kk], af[i][kk],
-                                                                         acc[i0 + i][j0 + j], 0, 0, 0);
+          for (int kk = 0; kk < 2; ++kk)
+            acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, bfr[j0 + j][kk]), __builtin_bit_cast(bf16x8, af[i][kk]),
+                acc[i0 + i][j0 + j], 0, 0, 0);
+        }
+      }
   };
 
   // ---- prologue: K-tile 0 landed; A-lo, B-lo, B-hi of K-tile 1 in flight
@@ -273,7 +325,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   wait_vm<6>();
   barrier_raw();
 
-  const int kq0 = n0 >> 6;          // DGRAD: first K-tile holding this tile's mask columns
+  const int kq0 = n0 / KT;          // DGRAD: first K-tile holding this tile's mask columns
+  constexpr unsigned NKQ = 256 / KT;  // DGRAD: K-tiles holding them (4 bf16, 2 fp8)
   float run_n = 0.f;                // rows of this wave's half merged so far (uniform)
   // The two wave halves run one barrier apart (the template's stagger): while the waves of
   // one half issue their MFMAs, the other half's ds_reads / glds / waits proceed, so each
@@ -288,7 +341,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
     read_a(buf, 0);
     read_b(buf, 2, 0);
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
     issue(qs + 1, 1);
     // every counted wait assumes the five regions issued after the one it retires are in
     // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
@@ -314,7 +367,6 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < 4u) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
     issue(qs + 2, 2);
     wait_lgkm0();
     barrier_raw();
@@ -322,7 +374,10 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     mfma_quad(4, 0);
     __builtin_amdgcn_s_setprio(0);
     barrier_raw();
-    // phase 4: (hi, hi); restage B-hi of K-tile qs+2
+    // phase 4: (hi, hi); restage B-hi of K-tile qs+2.  A-hi's mask bits are taken here, not
+    // in phase 3: B-lo's fragments are dead by now, which keeps the extraction's registers
+    // out of the accumulators' way (A-hi(qs) is restaged only in phase 1 of qs+1)
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
     issue(qs + 2, 3);
     // retires A-lo(qs+1), B-lo(qs+1): newer are B-hi(qs+1), A-hi(qs+1) and three of qs+2
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();
@@ -449,57 +504,58 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
       const uint32_t *mrow = mbits + ((qs / nks) & 1) * 2048 + wn * 2;
       const bool full = valid == BM;   // uniform: only a scene's last tile is partial
-      float s1[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s1[j][r] = 0.f;
+      // masking: v = acc & (0 - bit) (v_bfe_i32 sign-extends the keep bit to a full mask).
       // Stores widened to 16 B (cdna_hip_programming.md T21 with v_permlane16_swap): a lane
       // holds 4 columns (8 B) of tile j; swapping tile j with tile j+1 between lane groups
       // 2h and 2h+1 leaves each lane 8 consecutive columns of tile j + (lg & 1), so every
-      // store instruction writes 16 rows x 64 contiguous bytes instead of 16 x 32.
+      // store instruction writes 16 rows x 64 contiguous bytes instead of 16 x 32.  One tile
+      // pair (q) at a time: 8 column sums and one mask word live, not 16 and two.
       const int scol = n0 + wn * 64 + 16 * (lg & 1) + 8 * (lg >> 1);
-      // masking: v = acc & (0 - bit) (v_bfe_i32 sign-extends the keep bit to a full mask)
+      float S1 = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bool ok = full || ((rowok >> i) & 1u);
-        const uint2 mw = *reinterpret_cast<const uint2 *>(mrow + (wm * 128 + i * 16 + lr) * 8);
-        uint32_t pk[4][2];
+      for (int q = 0; q < 2; ++q) {
+        float s1[2][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int word = (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg));
-          float v[4];
+        for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
-            v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
-            s1[j][r] += ok ? v[r] : 0.f;
+          for (int r = 0; r < 4; ++r) s1[jj][r] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool ok = full || ((rowok >> i) & 1u);
+          const uint32_t mw = mrow[(wm * 128 + i * 16 + lr) * 8 + q];
+          uint32_t pk[2][2];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int word = (int)(mw >> (jj * 16 + 4 * lg));
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
+              v[r] = __uint_as_float(__float_as_uint(acc[i][2 * q + jj][r]) & keep);
+              s1[jj][r] += ok ? v[r] : 0.f;
+            }
+            pk[jj][0] = pack2bf(v[0], v[1]);
+            pk[jj][1] = pack2bf(v[2], v[3]);
           }
-          pk[j][0] = pack2bf(v[0], v[1]);
-          pk[j][1] = pack2bf(v[2], v[3]);
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const auto sw = __builtin_amdgcn_permlane16_swap(pk[2 * q][h], pk[2 * q + 1][h], false, false);
-            pk[2 * q][h] = sw[0];
-            pk[2 * q + 1][h] = sw[1];
+            const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+            pk[0][h] = sw[0];
+            pk[1][h] = sw[1];
           }
           if (ok)
             // plain store: dz5 is re-read right away by conv5's backward (nt measured 1 ms slower)
             *reinterpret_cast<u32x4 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + scol + 32 * q) =
-                mk_u32x4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
+                mk_u32x4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
         }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t = row_sum(s1[jj][r]);
+            if (lr == (2 * q + jj) * 4 + r) S1 = t;
+          }
       }
-      float S1 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float t = row_sum(s1[j][r]);
-          if (lr == j * 4 + r) S1 = t;
-        }
       if (do_stats) run[cme].x += S1;
       // The stores count in vmcnt but are not waited for here: the next counted wait
       // (vmcnt(10), phase 1) only relies on the LOADS completing in order among themselves
@@ -542,7 +598,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 
 bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS))) return false;
-  if (a.prologue != PCS_PRO_RAW || a.K % (2 * BK) != 0 || a.Ncols % BN != 0) return false;
+  const bool fp8 = a.flags & PCS_FLAG_AW_FP8;
+  if (fp8 && !a.w_scale) return false;
+  if (a.prologue != PCS_PRO_RAW || a.K % (fp8 ? 256 : 2 * BK) != 0 || a.Ncols % BN != 0) return false;
   // forward: statistics / max-pool only (nothing stored); the pool keeps one extremum per
   // column, chosen by sign(es), so a pool needs es
   if (a.epilogue == PCS_EPI_FWD) return a.C == nullptr && a.scene_bias == nullptr && (!a.pool || a.es);
@@ -555,10 +613,14 @@ bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
 int pcs_gemm_glds_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s) {
   const int ncb = g.Ncols / BN;
   const int nb = ncb * (int)(g.num_scenes * g.chunks_per_scene);
-  if (g.epilogue == PCS_EPI_FWD)
-    hipLaunchKernelGGL((gemm_glds_kernel<MODE_FWD>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb);
-  else
-    hipLaunchKernelGGL((gemm_glds_kernel<MODE_DGRAD>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb);
+  const bool fp8 = g.flags & PCS_FLAG_AW_FP8;
+#define PCS_GL(M, F) hipLaunchKernelGGL((gemm_glds_kernel<M, F>), dim3(nb), dim3(THREADS), 0, s, g, tps, tpc, ncb)
+  if (g.epilogue == PCS_EPI_FWD) {
+    if (fp8) PCS_GL(MODE_FWD, true); else PCS_GL(MODE_FWD, false);
+  } else {
+    if (fp8) PCS_GL(MODE_DGRAD, true); else PCS_GL(MODE_DGRAD, false);
+  }
+#undef PCS_GL
   PCS_CHECK_LAUNCH();
   return 0;
 }
@@ -575,8 +637,8 @@ namespace {
 
 constexpr int PR_MAXC = 1024;
 
-template <typename T>
-__global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, const T *__restrict__ Yp, int64_t N,
+template <typename T, typename TY>
+__global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, const TY *__restrict__ Yp, int64_t N,
                                                             int Ncols, const int32_t *__restrict__ idx,
                                                             const float *__restrict__ coef, const float *__restrict__ Wp,
                                                             int64_t ldw, int P, float *__restrict__ stats, int cps) {
@@ -618,25 +680,69 @@ __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, 
 
 }  // namespace
 
-extern "C" int pcs_pool_rows_add(void *dz, const void *Yp, int32_t dtype, int64_t num_scenes, int64_t scene_rows,
-                                 int32_t Ncols, const int32_t *pool_idx, const float *pool_coef, const float *pool_w,
-                                 int64_t pool_ldw, int32_t pool_c, float *stats, int32_t chunks_per_scene,
-                                 pcs_stream_t stream) {
+extern "C" int pcs_pool_rows_add(void *dz, int32_t dz_dtype, const void *Yp, int32_t yp_dtype, int64_t num_scenes,
+                                 int64_t scene_rows, int32_t Ncols, const int32_t *pool_idx, const float *pool_coef,
+                                 const float *pool_w, int64_t pool_ldw, int32_t pool_c, float *stats,
+                                 int32_t chunks_per_scene, pcs_stream_t stream) {
   if (!dz || !Yp || !pool_idx || !pool_coef || !pool_w || num_scenes <= 0 || scene_rows <= 0 || Ncols <= 0 ||
       pool_c <= 0 || pool_c > PR_MAXC || pool_ldw < Ncols || (stats && chunks_per_scene <= 0))
     return pcs_set_einval("pcs_pool_rows_add", "bad arguments (0 < pool_c <= 1024, pool_ldw >= Ncols)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((Ncols + 255) / 256, (unsigned)num_scenes);
-  if (dtype == PCS_BF16)
-    hipLaunchKernelGGL(pool_rows_add_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<bf16_t *>(dz),
-                       static_cast<const bf16_t *>(Yp), scene_rows, (int)Ncols, pool_idx, pool_coef, pool_w, pool_ldw,
-                       (int)pool_c, stats, (int)chunks_per_scene);
-  else if (dtype == PCS_F32)
-    hipLaunchKernelGGL(pool_rows_add_kernel<float>, grid, dim3(256), 0, s, static_cast<float *>(dz),
-                       static_cast<const float *>(Yp), scene_rows, (int)Ncols, pool_idx, pool_coef, pool_w, pool_ldw,
-                       (int)pool_c, stats, (int)chunks_per_scene);
-  else
-    return pcs_set_einval("pcs_pool_rows_add", "bad dtype");
+#define PCS_PRA(T, TY)                                                                                          \
+  hipLaunchKernelGGL((pool_rows_add_kernel<T, TY>), grid, dim3(256), 0, s, static_cast<T *>(dz),                 \
+                     static_cast<const TY *>(Yp), scene_rows, (int)Ncols, pool_idx, pool_coef, pool_w, pool_ldw, \
+                     (int)pool_c, stats, (int)chunks_per_scene)
+  if (dz_dtype == PCS_BF16 && yp_dtype == PCS_BF16) PCS_PRA(bf16_t, bf16_t);
+  else if (dz_dtype == PCS_BF16 && yp_dtype == PCS_FP8) PCS_PRA(bf16_t, fp8_t);
+  else if (dz_dtype == PCS_F32 && yp_dtype == PCS_F32) PCS_PRA(float, float);
+  else return pcs_set_einval("pcs_pool_rows_add", "dtypes: (bf16, bf16), (bf16, fp8) or (f32, f32)");
+#undef PCS_PRA
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// pcs_quant_fp8_rows: per-row E8M0-scaled e4m3 copy of a weight matrix (one block per row)
+// ---------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const float *__restrict__ W, int64_t cols, int64_t ldw,
+                                                             fp8_t *__restrict__ Wq, uint8_t *__restrict__ scale,
+                                                             float *__restrict__ deq) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const float *w = W + r * ldw;
+  float mx = 0.f;
+  for (int64_t k = threadIdx.x; k < cols; k += 256) mx = fmaxf(mx, fabsf(w[k]));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 0;
+  if (mx > 0.f) {
+    e = (int)ceilf(log2f(mx / 448.f));
+    e = e < -126 ? -126 : (e > 127 ? 127 : e);
+  }
+  if (threadIdx.x == 0) scale[r] = (uint8_t)(127 + e);
+  const float inv = ldexpf(1.f, -e);
+  for (int64_t k = threadIdx.x * 4; k < cols; k += 1024) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = k + q < cols ? w[k + q] * inv : 0.f;
+    const uint32_t b = pack4fp8(v[0], v[1], v[2], v[3]);
+    for (int q = 0; q < 4 && k + q < cols; ++q) {
+      Wq[r * cols + k + q] = (fp8_t)(b >> (8 * q));
+      if (deq) deq[r * cols + k + q] = ldexpf(fp82f((b >> (8 * q)) & 255u), e);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int pcs_quant_fp8_rows(const float *W, int64_t rows, int64_t cols, int64_t ldw, uint8_t *Wq, uint8_t *scale,
+                                  float *deq, pcs_stream_t stream) {
+  if (!W || !Wq || !scale || rows <= 0 || cols <= 0 || ldw < cols) return pcs_set_einval("pcs_quant_fp8_rows", "bad arguments");
+  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((unsigned)rows), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), W,
+                     cols, ldw, Wq, scale, deq);
   PCS_CHECK_LAUNCH();
   return 0;
 }

@@ -601,6 +601,12 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31)
     return pcs_set_einval("pcs_gemm", "M must be < 2^31 rows");
   if (a.K > KMAX) return pcs_set_einval("pcs_gemm", "K must be <= 1024");
+  if ((a.flags & PCS_FLAG_AW_FP8) && !(wide_class(a) && pcs_gemm_glds_applicable(a)))
+    return pcs_set_einval("pcs_gemm", "fp8 operands (PCS_FLAG_AW_FP8) need the LDS-DMA kernel: bf16 C, RAW prologue, "
+                                      "K % 256 == 0, Ncols % 256 == 0, w_scale, FWD (no C) or folded DGRAD");
+  if ((a.flags & PCS_FLAG_C_FP8) && !(a.epilogue == PCS_EPI_BNRELU && a.prologue == PCS_PRO_BNRELU && !a.a_mask &&
+                                      wide_class(a) && pcs_gemm_big_applicable(a)))
+    return pcs_set_einval("pcs_gemm", "fp8 output (PCS_FLAG_C_FP8) needs PRO_BNRELU (no dropout) + EPI_BNRELU on the bf16 256-wide kernel");
   if (a.a_mask && a.prologue != PCS_PRO_BNRELU)
     return pcs_set_einval("pcs_gemm", "a_mask applies to the BNRELU prologue only");
   const int64_t rpc = pcs_gemm_geometry(&a);

@@ -98,6 +98,10 @@ extern "C" int pcs_gram_wgrad(const float *G, const float *S, const float *W, in
     hipLaunchKernelGGL(gram_wgrad_kernel<float>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
                        sp, am, reinterpret_cast<const float *>(Y), s, t, (int)num_scenes, Cout, Cin, R, alpha,
                        dW, ldw);
+  else if (dtype == PCS_FP8)   // the fp8 path's e4m3 a5 (max-pool rows' term)
+    hipLaunchKernelGGL(gram_wgrad_kernel<fp8_t>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
+                       sp, am, reinterpret_cast<const fp8_t *>(Y), s, t, (int)num_scenes, Cout, Cin, R, alpha,
+                       dW, ldw);
   else
     return pcs_set_einval("pcs_gram_wgrad", "bad dtype");
   PCS_CHECK_LAUNCH();

@@ -22,20 +22,34 @@
 //   since the DMA writes LDS linearly), so the 8 rows each half-wave reads land in 8 distinct
 //   bank groups.
 // * The final M % 64 rows are left to pcs_gram_raw's tail kernel.
+// * fp8 (the cfg5 path, a5 stored as e4m3 by conv5's epilogue): a K-step is 128 rows of 128-B
+//   region rows (the same 16 KB regions), one unit-scaled v_mfma_scale_f32_16x16x128_f8f6f4
+//   per (i, j) pair.  A lane's 32 k-values of one column are four ds_read_b64_tr_b8 of 8 rows
+//   (rows 32 t + 8 (lane >> 4) .. + 8, t = 0..3), the same lane -> k map for both operands;
+//   the 16-B granules of row r are XOR-swizzled by (r >> 1) & 7, so the 16 rows a half-wave
+//   reads fill all 64 banks.  Products of e4m3 values are exact in the fp32 accumulators: G is
+//   the Gram of the stored activation, as in bf16.
 #include "common.h"
 
 namespace {
 
 constexpr int THREADS = 512;
-constexpr int TN = 256, MS = 64;
-constexpr int ROWB = 256;                     // region row: 128 columns x 2 B
-constexpr int REG = MS * ROWB;                // 16 KB
+constexpr int TN = 256;
+constexpr int REG = 16384;                    // region: 64 rows x 256 B (bf16) | 128 x 128 B (fp8)
 constexpr int KBUF = 4 * REG;                 // A-lo | A-hi | B-lo | B-hi
 constexpr int LDS_BYTES = 2 * KBUF;           // 128 KB
+template <bool FP8> struct GCfg {
+  static constexpr int ESZ = FP8 ? 1 : 2;
+  static constexpr int MS = FP8 ? 128 : 64;   // rows per K-step
+  static constexpr int ROWB = 128 * ESZ;      // region row: 128 columns
+};
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v2i lds_v2i;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 PCS_DEV void sbar() { __builtin_amdgcn_sched_barrier(0); }
@@ -63,9 +77,11 @@ PCS_DEV void wait_lgkm0() {
   sbar();
 }
 
-PCS_DEV int gsw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }   // granule swizzle of row r
+PCS_DEV int gsw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }   // bf16: 32-B granule swizzle of row r
+PCS_DEV int gsw8(int r) { return (r >> 1) & 7; }                     // fp8: 16-B granule swizzle
 // byte offset of (row, byte-in-row) in a region
-PCS_DEV int roff(int r, int byte) { return r * ROWB + ((((byte >> 5) ^ gsw(r)) << 5) | (byte & 31)); }
+PCS_DEV int roff(int r, int byte) { return r * 256 + ((((byte >> 5) ^ gsw(r)) << 5) | (byte & 31)); }
+PCS_DEV int roff8(int r, int byte) { return r * 128 + ((((byte >> 4) ^ gsw8(r)) << 4) | (byte & 15)); }
 
 // tile index t (0 .. nt(nt+1)/2 - 1) -> (block row, block col) of the upper triangle
 PCS_DEV void tile_rc(int t, int nt, int &br, int &bc) {
@@ -74,6 +90,17 @@ PCS_DEV void tile_rc(int t, int nt, int &br, int &bc) {
   bc = br + t;
 }
 
+// fp8: 32 k-values (rows 32 t + r0 .. + 8, t = 0..3) of one column per lane
+PCS_DEV v8i tr_frag8(const char *region, int r0, int byte) {
+  v8i v;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const v2i x = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i *)(region + roff8(32 * t + r0, byte)));
+    v[2 * t] = x[0];
+    v[2 * t + 1] = x[1];
+  }
+  return v;
+}
 PCS_DEV bf16x8 tr_frag(const char *region, int r0, int r1, int byte) {
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(region + roff(r0, byte)));
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(region + roff(r1, byte)));
@@ -88,8 +115,11 @@ PCS_DEV int xcd_remap(int bid, int nb) {
 
 // Workgroup L = split * ntile + tile: steps [split * steps / nsplit, (split + 1) * steps / nsplit)
 // of tile `tile`, partial slot L.
-__global__ __launch_bounds__(THREADS) void gram_glds_kernel(const bf16_t *__restrict__ A, int C, int64_t steps,
+template <bool FP8>
+__global__ __launch_bounds__(THREADS) void gram_glds_kernel(const void *__restrict__ A, int C, int64_t steps,
                                                             int ntile, float *__restrict__ part) {
+  typedef GCfg<FP8> CF;
+  constexpr int MS = CF::MS;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -103,26 +133,37 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const bf16_t *__rest
   const int nt = C / TN;
   int br, bc;
   tile_rc(tile, nt, br, bc);
-  const int64_t rowbytes = (int64_t)C * 2;
+  const int64_t rowbytes = (int64_t)C * CF::ESZ;
   const char *Ab = reinterpret_cast<const char *>(A);
 
-  // ---- DMA: piece g (0, 1) of wave w covers region rows (2w + g) * 4 .. + 4; lane -> row
-  // + lane / 16, LDS slot lane % 16 (16 B), which holds logical chunk c of the row:
-  // granule (slot / 2) ^ f(row), half slot % 2
+  // ---- DMA, bf16: piece g (0, 1) of wave w covers region rows (2w + g) * 4 .. + 4; lane ->
+  // row + lane / 16, LDS slot lane % 16 (16 B), which holds logical chunk c of the row:
+  // granule (slot / 2) ^ f(row), half slot % 2.
+  //   A regions (n columns): chunk c -> tile column (c & 7) * 8 + (c >> 3) * 128 + hi * 64
+  //   B regions (k columns): chunk c -> tile column (c >> 2) * 64 + (c & 3) * 8 + hi * 32
+  // fp8: rows (2w + g) * 8 + lane / 8, slot lane % 8 holds granule c = slot ^ f8(row) (16 columns)
+  //   A: c -> (c & 3) * 16 + (c >> 2) * 128 + hi * 64;  B: c -> (c >> 1) * 64 + (c & 1) * 16 + hi * 32
   int prow[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) prow[g] = (2 * wid + g) * 4 + (lane >> 4);
-  // A regions (n columns): region chunk c -> tile column (c & 7) * 8 + (c >> 3) * 128 + hi * 64
-  // B regions (k columns): region chunk c -> tile column (c >> 2) * 64 + (c & 3) * 8 + hi * 32
   uint32_t acol[2][2], bcol[2][2];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    const int slot = lane & 15;
-    const int c = ((((slot >> 1) ^ gsw(prow[g])) << 1) | (slot & 1));
+    if constexpr (FP8) {
+      prow[g] = (2 * wid + g) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ gsw8(prow[g]);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      acol[h][g] = (uint32_t)(((c & 7) * 8 + (c >> 3) * 128 + h * 64) * 2);
-      bcol[h][g] = (uint32_t)(((c >> 2) * 64 + (c & 3) * 8 + h * 32) * 2);
+      for (int h = 0; h < 2; ++h) {
+        acol[h][g] = (uint32_t)((c & 3) * 16 + (c >> 2) * 128 + h * 64);
+        bcol[h][g] = (uint32_t)((c >> 1) * 64 + (c & 1) * 16 + h * 32);
+      }
+    } else {
+      prow[g] = (2 * wid + g) * 4 + (lane >> 4);
+      const int slot = lane & 15;
+      const int c = ((((slot >> 1) ^ gsw(prow[g])) << 1) | (slot & 1));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acol[h][g] = (uint32_t)(((c & 7) * 8 + (c >> 3) * 128 + h * 64) * 2);
+        bcol[h][g] = (uint32_t)(((c >> 2) * 64 + (c & 3) * 8 + h * 32) * 2);
+      }
     }
   }
 
@@ -130,7 +171,7 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const bf16_t *__rest
     if (qseq >= total) return;   // nothing left: the tail waits below shrink to match
     const int hi = region & 1;
     const int col0 = (region < 2 ? br : bc) * TN;
-    const char *sb = Ab + (s0 + qseq) * MS * rowbytes + (int64_t)col0 * 2;
+    const char *sb = Ab + (s0 + qseq) * MS * rowbytes + (int64_t)col0 * CF::ESZ;
     char *dst = lds + (qseq & 1) * KBUF + region * REG;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -139,29 +180,43 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const bf16_t *__rest
     }
   };
 
-  // fragments: lane (q = (lane >> 2) & 3, p = lane & 3, g = lane >> 4) reads rows
-  // 32 kk + 8 g + q (+4) of column base + 4 p, transposed
+  // fragments, bf16: lane (q = (lane >> 2) & 3, p = lane & 3, g = lane >> 4) reads rows
+  // 32 kk + 8 g + q (+4) of column base + 4 p, transposed.  fp8: in each 16-lane group lane i
+  // reads row 8 g + i / 2 (+ 32 t), bytes 8 (i & 1) .. of the group's 16 columns, and ends
+  // with column i of the 8 rows
   const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int r8 = 8 * fg + ((lane & 15) >> 1), c8 = 8 * (lane & 1);
   bf16x8 af[4][2], bfr[4][2];
+  v8i af8[4], bf8[4];
   auto read_a = [&](int buf, int hi) {   // n columns wm*128 + (hi*4 + i)*16 .. -> region col wm*64 + i*16
     const char *base = lds + buf * KBUF + hi * REG;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (FP8) {
+        af8[i] = tr_frag8(base, r8, wm * 64 + i * 16 + c8);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int r0 = 32 * kk + 8 * fg + fq;
-        af[i][kk] = tr_frag(base, r0, r0 + 4, (wm * 64 + i * 16 + 4 * fp) * 2);
+        for (int kk = 0; kk < 2; ++kk) {
+          const int r0 = 32 * kk + 8 * fg + fq;
+          af[i][kk] = tr_frag(base, r0, r0 + 4, (wm * 64 + i * 16 + 4 * fp) * 2);
+        }
       }
+    }
   };
   auto read_b = [&](int buf, int hi, int j0) {   // k columns wn*64 + (hi*2 + j)*16 -> region col wn*32 + j*16
     const char *base = lds + buf * KBUF + (2 + hi) * REG;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (FP8) {
+        bf8[j0 + j] = tr_frag8(base, r8, wn * 32 + j * 16 + c8);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int r0 = 32 * kk + 8 * fg + fq;
-        bfr[j0 + j][kk] = tr_frag(base, r0, r0 + 4, (wn * 32 + j * 16 + 4 * fp) * 2);
+        for (int kk = 0; kk < 2; ++kk) {
+          const int r0 = 32 * kk + 8 * fg + fq;
+          bfr[j0 + j][kk] = tr_frag(base, r0, r0 + 4, (wn * 32 + j * 16 + 4 * fp) * 2);
+        }
       }
+    }
   };
 
   f32x4 acc[8][4];
@@ -176,11 +231,17 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const bf16_t *__rest
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (FP8) {
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              bf8[j0 + j], af8[i], acc[i0 + i][j0 + j], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+        } else {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j0 + j][kk], af[i][kk],
-                                                                         acc[i0 + i][j0 + j], 0, 0, 0);
+          for (int kk = 0; kk < 2; ++kk)
+            acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j0 + j][kk], af[i][kk],
+                                                                           acc[i0 + i][j0 + j], 0, 0, 0);
+        }
+      }
   };
 
   // ---- prologue: step 0 landed; A-lo, B-lo, B-hi of step 1 in flight
@@ -250,8 +311,9 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const bf16_t *__rest
 }
 
 // sum the nsplit partial slots of each upper tile into G (fixed order) and add the Gram of
-// the tail rows [m_tail, M) (fewer than 64); mirror into the lower tiles
-__global__ __launch_bounds__(256) void gram_reduce_kernel(const float *__restrict__ part, const bf16_t *__restrict__ A,
+// the tail rows [m_tail, M) (fewer than one K-step); mirror into the lower tiles
+template <typename T>
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float *__restrict__ part, const T *__restrict__ A,
                                                           int64_t M, int64_t m_tail, int C, int ntile, int nsplit,
                                                           float *__restrict__ G) {
   const int t = blockIdx.y;
@@ -264,7 +326,7 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float *__restric
   for (int sp = 0; sp < nsplit; ++sp) s += part[((int64_t)sp * ntile + t) * TN * TN + e];
   const int gn = br * TN + n, gk = bc * TN + k;
   for (int64_t m = m_tail; m < M; ++m)
-    s = fmaf(bf2f(A[m * C + gn]), bf2f(A[m * C + gk]), s);
+    s = fmaf(load_elem(A, m * C + gn), load_elem(A, m * C + gk), s);
   G[(int64_t)gn * C + gk] = s;
   if (br != bc) G[(int64_t)gk * C + gn] = s;
 }
@@ -288,23 +350,34 @@ extern "C" int64_t pcs_gram_raw_workspace(int64_t M, int32_t C) {
   return (int64_t)gram_splits(C) * ntile * TN * TN * 4;
 }
 
-extern "C" int pcs_gram_raw(const void *A, int64_t M, int32_t C, float *workspace, int64_t workspace_bytes, float *G,
-                            pcs_stream_t stream) {
+extern "C" int pcs_gram_raw(const void *A, int64_t M, int32_t C, int32_t dtype, float *workspace,
+                            int64_t workspace_bytes, float *G, pcs_stream_t stream) {
   if (!A || !workspace || !G || M <= 0 || C <= 0 || C % TN)
     return pcs_set_einval("pcs_gram_raw", "A, workspace, G, M > 0 and C % 256 == 0 required");
+  if (dtype != PCS_BF16 && dtype != PCS_FP8) return pcs_set_einval("pcs_gram_raw", "dtype must be PCS_BF16 or PCS_FP8");
   if (M >= ((int64_t)1 << 31)) return pcs_set_einval("pcs_gram_raw", "M must be < 2^31");
   const int64_t need = pcs_gram_raw_workspace(M, C);
   if (need < 0) return (int)need;
   if (workspace_bytes < need) return pcs_set_einval("pcs_gram_raw", "workspace too small (pcs_gram_raw_workspace)");
   const int nt = C / TN, ntile = nt * (nt + 1) / 2;
   const int nsplit = gram_splits(C);
-  const int64_t steps = M / MS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bf16_t *Ab = static_cast<const bf16_t *>(A);
-  hipLaunchKernelGGL(gram_glds_kernel, dim3(nsplit * ntile), dim3(THREADS), 0, s, Ab, (int)C, steps, ntile, workspace);
-  PCS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(TN * TN / 256, ntile), dim3(256), 0, s, workspace, Ab, M, steps * MS,
-                     (int)C, ntile, nsplit, G);
+  const dim3 rgrid(TN * TN / 256, ntile);
+  if (dtype == PCS_FP8) {
+    const int64_t steps = M / GCfg<true>::MS;
+    hipLaunchKernelGGL(gram_glds_kernel<true>, dim3(nsplit * ntile), dim3(THREADS), 0, s, A, (int)C, steps, ntile,
+                       workspace);
+    PCS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(gram_reduce_kernel<fp8_t>, rgrid, dim3(256), 0, s, workspace, static_cast<const fp8_t *>(A), M,
+                       steps * GCfg<true>::MS, (int)C, ntile, nsplit, G);
+  } else {
+    const int64_t steps = M / GCfg<false>::MS;
+    hipLaunchKernelGGL(gram_glds_kernel<false>, dim3(nsplit * ntile), dim3(THREADS), 0, s, A, (int)C, steps, ntile,
+                       workspace);
+    PCS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(gram_reduce_kernel<bf16_t>, rgrid, dim3(256), 0, s, workspace, static_cast<const bf16_t *>(A),
+                       M, steps * GCfg<false>::MS, (int)C, ntile, nsplit, G);
+  }
   PCS_CHECK_LAUNCH();
   return 0;
 }

@@ -112,11 +112,13 @@ def check_dims(num_classes: int, input_dim: int):
 
 
 def _dt(dtype: str):
+    """(C-ABI dtype, torch dtype) of the stored activations.  "fp8" is the bf16 path with the
+    wide layer (a5 = relu(bn5(y5)) and global_feat's operands) in fp8 e4m3."""
     if dtype == "fp32":
         return L.F32, torch.float32
-    if dtype == "bf16":
+    if dtype in ("bf16", "fp8"):
         return L.BF16, torch.bfloat16
-    raise ValueError(f"compute dtype must be 'fp32' or 'bf16', got {dtype!r}")
+    raise ValueError(f"compute dtype must be 'fp32', 'bf16' or 'fp8', got {dtype!r}")
 
 
 @dataclass
@@ -157,6 +159,10 @@ class Engine:
         self.C = num_classes
         self.dtype = dtype
         self.dt, self.tdt = _dt(dtype)
+        # fp8: conv5 stores a5 as e4m3 and global_feat runs on MX-scaled fp8 MFMA (W rows
+        # quantized with one E8M0 scale each, pcs_quant_fp8_rows), forward and input gradient
+        self.fp8 = dtype == "fp8"
+        self.a5_dt = L.FP8 if self.fp8 else self.dt
         self.layout = param_layout(num_classes, input_dim)          # registration order
         self.numel = {n: int(torch.Size(s).numel()) for n, s in self.layout}
         self.offsets, self.total_params = flat_offsets(num_classes, input_dim)   # flat order
@@ -212,7 +218,20 @@ class Engine:
             WcT = self._empty(cols, rows, device=dev)
             L.call("pcs_cast_weight", L.ptr(W), rows, cols, ld, self.dt, L.ptr(Wc), L.ptr(WcT), s)
             wc[conv] = (Wc, WcT)
+        if self.fp8:
+            wc["global_feat_fp8"] = self._quant_fp8(P["global_feat.weight"])
         return wc
+
+    def _quant_fp8(self, W):
+        """(e4m3 rows, E8M0 row scales, fp32 dequantized copy) of a 2-D fp32 matrix."""
+        rows, cols = W.shape
+        dev = W.device
+        Wq = torch.empty(rows, cols, dtype=torch.uint8, device=dev)
+        sc = torch.empty(rows, dtype=torch.uint8, device=dev)
+        deq = torch.empty(rows, cols, dtype=torch.float32, device=dev)
+        L.call("pcs_quant_fp8_rows", L.ptr(W), rows, cols, W.stride(0), L.ptr(Wq), L.ptr(sc), L.ptr(deq),
+               self._stream())
+        return Wq, sc, deq
 
     def _bn_finalize(self, bnname, stats, B, N, C, cps, rpc, P, bufs, train, dev, offset=None):
         """BN coefficients for stored activations that omit ``offset`` (the conv bias)."""
@@ -236,7 +255,8 @@ class Engine:
         tag = kw.pop("tag", None)
         cps, _ = self.geometry(B, N, K, ncols, pro, epi)
         a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
-                       prologue=pro, epilogue=epi, chunks_per_scene=cps, flags=self.flags,
+                       prologue=pro, epilogue=epi, chunks_per_scene=cps,
+                       flags=self.flags | kw.pop("extra_flags", 0),
                        A=L.ptr(A), W=L.ptr(W), C=L.ptr(C),
                        a_keep_scale=kw.pop("a_keep_scale", 1.0),
                        c_keep_scale=kw.pop("c_keep_scale", 1.0),
@@ -265,8 +285,8 @@ class Engine:
         return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
     def _raw_gram(self):
-        """bf16 wide-layer path: a5 is stored post-ReLU, so global_feat's Gram reads it raw
-        on the LDS-DMA kernel (pcs_gram_raw) with column sums from conv5's epilogue."""
+        """bf16 / fp8 wide-layer path: a5 is stored post-ReLU, so global_feat's Gram reads it
+        raw on the LDS-DMA kernel (pcs_gram_raw) with column sums from conv5's epilogue."""
         return self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC)
 
     def _rounded(self, W):
@@ -370,7 +390,7 @@ class Engine:
                        stats=st, tag="fwd_stats:conv5", **bnrelu("bn4"))
         sv.bn["bn5"] = self._bn_finalize("bn5", st, B, N, 1024, cps, rpc, P, bufs, train, dev,
                                          offset=P["conv5.bias"])
-        a5 = self._empty(M, 1024, device=dev)
+        a5 = self._empty(M, 1024, device=dev, dtype=torch.uint8 if self.fp8 else None)
         c5 = sv.bn["bn5"]
         # bf16: the epilogue also sums a5's columns per chunk (S of global_feat's Gram-form
         # weight gradient; the LDS-DMA Gram kernel computes G only)
@@ -379,7 +399,8 @@ class Engine:
             cps5c, _ = self.geometry(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU)
             sv.a5_colsum = torch.empty(B * cps5c, 1024, 2, dtype=torch.float32, device=dev)
         self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU, sv.ys["conv4"], wc["conv5"][0], a5,
-                   es=c5.scale, et=c5.shift, stats=sv.a5_colsum, tag="fwd:conv5", **bnrelu("bn4"))
+                   es=c5.scale, et=c5.shift, stats=sv.a5_colsum, tag="fwd:conv5",
+                   extra_flags=L.FLAG_C_FP8 if self.fp8 else 0, **bnrelu("bn4"))
         sv.ys["a5"] = a5
 
         # global_feat (P:113-114): a5 W^T with BN statistics and max-pool partials in the
@@ -388,8 +409,13 @@ class Engine:
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
         st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
         # (es = bn_global's gamma: its sign tells the pool which extremum pcs_pool_finalize uses)
-        self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, wc["global_feat"][0], None,
-                   stats=st, pool=pool, es=P["bn_global.weight"], tag="fwd:global_feat")
+        if self.fp8:
+            Wq, wsc, _ = wc["global_feat_fp8"]
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wq, None, stats=st, pool=pool,
+                       es=P["bn_global.weight"], w_scale=wsc, extra_flags=L.FLAG_AW_FP8, tag="fwd:global_feat")
+        else:
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, wc["global_feat"][0], None,
+                       stats=st, pool=pool, es=P["bn_global.weight"], tag="fwd:global_feat")
         sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_g, rpc_g, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]
@@ -637,21 +663,35 @@ class Engine:
         # a5 > 0 (bn5's ReLU) and sums S1 = sum dz5; S2 comes from R = dz5^T a4 below.
         a5 = ys["a5"]
         Wg = P["global_feat.weight"]
-        Wg_r = self._rounded(Wg)   # the W the forward GEMM used (see pcs_round_weight)
-        Hg = self._empty(1024, 1024, device=dev)
+        # the W the forward GEMM used (see pcs_round_weight; fp8: the dequantized e4m3 rows)
+        Wg_r = wc["global_feat_fp8"][2] if self.fp8 else self._rounded(Wg)
         cvec = torch.empty(1024, dtype=torch.float32, device=dev)
-        L.call("pcs_bn_fold", L.ptr(Wg_r), 1024, 1024, Wg.shape[1], None, L.ptr(bg), L.ptr(gg), self.dt,
-               None, L.ptr(cvec), L.ptr(Hg), s)
+        if self.fp8:
+            # H in fp32, then e4m3 rows with one scale each (H is symmetric: row n = column n)
+            Hf = torch.empty(1024, 1024, dtype=torch.float32, device=dev)
+            L.call("pcs_bn_fold", L.ptr(Wg_r), 1024, 1024, Wg_r.shape[1], None, L.ptr(bg), L.ptr(gg), L.F32,
+                   None, L.ptr(cvec), L.ptr(Hf), s)
+            Hq, hsc, _ = self._quant_fp8(Hf)
+            Hg = (Hf, Hq, hsc)
+        else:
+            Hg = self._empty(1024, 1024, device=dev)
+            L.call("pcs_bn_fold", L.ptr(Wg_r), 1024, 1024, Wg.shape[1], None, L.ptr(bg), L.ptr(gg), self.dt,
+                   None, L.ptr(cvec), L.ptr(Hg), s)
         pc5 = sv.bn["bn5"]
         cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD)
         st5 = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
-        if self.dt == L.BF16 and not (self.flags & (L.FLAG_GENERIC | L.FLAG_NO_GLDS)):
+        if self.fp8:
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg[1], bufB, bias=cvec, Yp=a5,
+                       w_scale=Hg[2], extra_flags=L.FLAG_AW_FP8, stats=st5, tag="dgrad:global_feat")
+            L.call("pcs_pool_rows_add", L.ptr(bufB), self.dt, L.ptr(a5), L.FP8, B, N, 1024, L.ptr(sv.am),
+                   L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
+        elif self.dt == L.BF16 and not (self.flags & (L.FLAG_GENERIC | L.FLAG_NO_GLDS)):
             # LDS-DMA kernel without the max-pool rows (no ordinary global loads in its
             # epilogue), then their sparse term (pcs_pool_rows_add)
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
                        stats=st5, tag="dgrad:global_feat")
-            L.call("pcs_pool_rows_add", L.ptr(bufB), L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am), L.ptr(sp),
-                   L.ptr(Wg), Wg.shape[1], 1024, L.ptr(st5), cps5, s)
+            L.call("pcs_pool_rows_add", L.ptr(bufB), self.dt, L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am),
+                   L.ptr(sp), L.ptr(Wg), Wg.shape[1], 1024, L.ptr(st5), cps5, s)
         else:
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
                        pool_idx=sv.am, pool_coef=sp, pool_w=Wg, pool_ldw=Wg.shape[1], pool_c=1024,
@@ -668,7 +708,7 @@ class Engine:
             if nbytes < 0:
                 raise L.PcsError(L.load().pcs_last_error().decode())
             ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-            self._launch("wgrad:global_feat", "pcs_gram_raw", L.ptr(a5), M, 1024, L.ptr(ws), nbytes, L.ptr(gram), s)
+            self._launch("wgrad:global_feat", "pcs_gram_raw", L.ptr(a5), M, 1024, self.a5_dt, L.ptr(ws), nbytes, L.ptr(gram), s)
             cs2 = torch.empty(1024, 2, dtype=torch.float32, device=dev)
             L.call("pcs_reduce_partials", L.ptr(sv.a5_colsum), sv.a5_colsum.shape[0], 2048, 1.0, L.ptr(cs2),
                    2048, 2048, s)
@@ -682,7 +722,7 @@ class Engine:
                          self.dt, sps.value, L.ptr(ws), L.ptr(gram), L.ptr(colsum), s)
         self._launch("wgrad_asm:global_feat", "pcs_gram_wgrad", L.ptr(gram), L.ptr(colsum), L.ptr(Wg_r),
                      Wg.shape[1], L.ptr(bg), L.ptr(gg), L.ptr(sp), L.ptr(sv.am), L.ptr(a5),
-                     L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.dt, None, None,
+                     L.ptr(ones), L.ptr(zeros), B, 1024, 1024, self.a5_dt, None, None,
                      L.ptr(G("global_feat.weight")), 1024, s)
         keepalive.append((Hg, cvec, ones, zeros, gram, colsum, ws, Wg_r))
         bucket("global")

@@ -110,7 +110,7 @@ def test_folded_dgrad_sparse_mask_s1(variant, B, N, cps):
     if variant == "glds":
         # the LDS-DMA kernel leaves the max-pool rows to pcs_pool_rows_add
         L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
-        L.call("pcs_pool_rows_add", L.ptr(out), L.ptr(A), dt, B, N, K, L.ptr(am), L.ptr(sp), L.ptr(Wsp), K, Pc,
+        L.call("pcs_pool_rows_add", L.ptr(out), dt, L.ptr(A), dt, B, N, K, L.ptr(am), L.ptr(sp), L.ptr(Wsp), K, Pc,
                L.ptr(st), a.chunks_per_scene, L.stream_ptr())
     else:
         a.pool_idx, a.pool_coef, a.pool_w, a.pool_ldw, a.pool_c = am.data_ptr(), sp.data_ptr(), Wsp.data_ptr(), K, Pc

@@ -112,7 +112,7 @@ def test_gram_raw_lds_dma_matches_torch(M):
     outs = []
     for _ in range(3):
         G = torch.full((C, C), float("nan"), device=DEV)
-        L.call("pcs_gram_raw", L.ptr(A), M, C, L.ptr(ws), nbytes, L.ptr(G), L.stream_ptr())
+        L.call("pcs_gram_raw", L.ptr(A), M, C, L.BF16, L.ptr(ws), nbytes, L.ptr(G), L.stream_ptr())
         outs.append(G)
     torch.cuda.synchronize()
     ref = A.double().T @ A.double()

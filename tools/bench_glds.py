@@ -1,6 +1,8 @@
 """Micro-benchmark of the global_feat GEMMs at the cfg2 shape (M = 4 x 128^3 rows, 1024 x 1024,
 bf16, a5-like operand) with each epilogue feature on/off: the LDS-DMA kernel (gemm_glds.hip)
-against the register-staged 256x256 kernel (FLAG_NO_GLDS).  Prints ms and TF/s per variant."""
+against the register-staged 256x256 kernel (FLAG_NO_GLDS).  Prints ms and TF/s per variant.
+GLDS_GRAM=1: the Gram of a5 instead; GLDS_FP8=1: the fp8 (MX-scaled MFMA) forms of the
+LDS-DMA forward, input gradient and Gram."""
 import ctypes as ct
 import os
 import sys
@@ -62,6 +64,40 @@ def main():
         ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
         print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
 
+    if os.environ.get("GLDS_FP8"):
+        A8 = A.float().clamp(max=448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+        del A
+        W8 = torch.empty(Nc, K, dtype=torch.uint8, device=dev)
+        wsc = torch.empty(Nc, dtype=torch.uint8, device=dev)
+        Wf = W.float()
+        L.call("pcs_quant_fp8_rows", L.ptr(Wf), Nc, K, K, L.ptr(W8), L.ptr(wsc), None, L.stream_ptr())
+
+        def run8(name, epi, **kw):
+            a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=Nc, dtype=L.BF16, prologue=L.PRO_RAW,
+                           epilogue=epi, chunks_per_scene=0, flags=L.FLAG_AW_FP8)
+            lib.pcs_gemm_geometry(ct.byref(a))
+            nch = B * a.chunks_per_scene
+            keep = dict(stats=torch.empty(nch, Nc, 2, device=dev))
+            if epi == L.EPI_FWD:
+                keep["pool"] = torch.empty(nch, Nc, 4, device=dev)
+            a.A, a.W, a.w_scale = A8.data_ptr(), W8.data_ptr(), wsc.data_ptr()
+            for k, v in list(kw.items()) + list(keep.items()):
+                setattr(a, k, L.ptr(v))
+            ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
+            print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
+
+        for _ in range(2):
+            run8("[glds fp8] fwd + stats + pool", L.EPI_FWD, es=gsign)
+            run8("[glds fp8] dgrad: mask + store + bias + S1", L.EPI_DGRAD, C=C, Yp=A8, bias=c)
+        nb2 = lib.pcs_gram_raw_workspace(M, K)
+        ws2 = torch.empty(nb2 // 4, device=dev)
+        G2 = torch.empty(K, K, device=dev)
+        gfl = flops * 10 / 16
+        for _ in range(2):
+            ms = timeit(lambda: L.call("pcs_gram_raw", L.ptr(A8), M, K, L.FP8, L.ptr(ws2), nb2, L.ptr(G2),
+                                       L.stream_ptr()))
+            print(f"[gram fp8] LDS-DMA (pcs_gram_raw)               {ms:8.3f} ms  {gfl / ms / 1e9:8.1f} TF/s", flush=True)
+        return
     if os.environ.get("GLDS_GRAM"):   # Gram of a5: register-staged 256x256 vs LDS-DMA persistent
         sps = ct.c_int32(0)
         nb = lib.pcs_gram_workspace(B, N, K, L.BF16, ct.byref(sps))
@@ -76,7 +112,7 @@ def main():
             ms = timeit(lambda: L.call("pcs_gram", L.ptr(A), None, None, B, N, K, L.BF16, sps.value, L.ptr(ws),
                                        L.ptr(G), L.ptr(S), L.stream_ptr()))
             print(f"[gram] register-staged (pcs_gram)                {ms:8.3f} ms  {gfl / ms / 1e9:8.1f} TF/s", flush=True)
-            ms = timeit(lambda: L.call("pcs_gram_raw", L.ptr(A), M, K, L.ptr(ws2), nb2, L.ptr(G2), L.stream_ptr()))
+            ms = timeit(lambda: L.call("pcs_gram_raw", L.ptr(A), M, K, L.BF16, L.ptr(ws2), nb2, L.ptr(G2), L.stream_ptr()))
             print(f"[gram] LDS-DMA persistent (pcs_gram_raw)         {ms:8.3f} ms  {gfl / ms / 1e9:8.1f} TF/s", flush=True)
         torch.cuda.synchronize()
         print("max |G - G2| / max |G|:", float((G - G2).abs().max() / G.abs().max()))
