@@ -2,7 +2,10 @@
 on MI355X, points/s on a dense 128^3 grid, batch 4 scenes per GPU (BASELINE.json configs[1];
 SURVEY.md §8(d) cfg2).  One process per GPU; for N>1 launch with torch.distributed.run.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32] [--grid 128]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp8|fp32] [--grid 128]
+
+--dtype fp8 is BASELINE.json configs[4] (cfg5): the bf16 step with the 1024-wide layer's
+activation a5 and global_feat's GEMMs in e4m3 on MX-scaled MFMA.
 
 Prints ONE JSON line (rank 0).  value = points processed by all ranks / max-over-ranks
 wall time of K steps (bracketed by barrier + synchronize).  ``roofline`` describes the
@@ -30,7 +33,21 @@ from pcs_amd.model import PointNetSegmentation  # noqa: E402
 from pcs_amd.optim import FusedAdam  # noqa: E402
 from pcs_amd.train import FusedTrainStep  # noqa: E402
 
-PEAK = {"bf16": {"mfma": 2516.6, "hbm": 8000.0}, "fp32": {"mfma": 157.3, "hbm": 8000.0}}
+PEAK = {"bf16": {"mfma": 2516.6, "hbm": 8000.0}, "fp32": {"mfma": 157.3, "hbm": 8000.0},
+        "fp8": {"mfma": 5033.2, "hbm": 8000.0}}   # fp8: dense e4m3 (block-scaled MFMA), no sparsity
+
+
+def act_bytes(dtype):
+    """Bytes per stored activation element (fp8: the bf16 path outside the wide layer)."""
+    return 4 if dtype == "fp32" else 2
+
+
+def kernel_peak(tag, dtype):
+    """MFMA / HBM peaks the kernel behind ``tag`` is priced against: under fp8 the
+    global_feat kernels run e4m3 MFMA, everything else bf16."""
+    if dtype == "fp8":
+        return PEAK["fp8"] if tag.endswith(":global_feat") else PEAK["bf16"]
+    return PEAK[dtype]
 LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (64, 128),
               "conv5": (128, 1024), "global_feat": (1024, 1024), "seg_conv1": (64, 512),
               "seg_conv2": (512, 256), "seg_conv3": (256, 128)}
@@ -67,22 +84,27 @@ def pmc_traffic(tag, dtype, workload, points):
     return None
 
 
-def kernel_model(tag, M, ab):
-    """Algorithmic FLOPs and HBM bytes of one launch (SURVEY.md §8(d) accounting)."""
+def kernel_model(tag, M, dtype):
+    """Algorithmic FLOPs and HBM bytes of one launch (SURVEY.md §8(d) accounting).  fp8:
+    a5 (global_feat's input, conv5's stored output) is 1 byte, dz5 and the rest bf16."""
     kind, conv = tag.split(":", 1)
     if conv not in LAYER_DIMS or kind not in ("fwd", "dgrad", "wgrad", "dgrad+wgrad"):
         return None
+    ab = act_bytes(dtype)
+    a5b = 1 if dtype == "fp8" else ab
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
     if kind == "dgrad+wgrad":   # fused: dZ, Y in once, Y_{l-1} (+ addend) in, dZ_{l-1} out
         extra = cin if conv == "conv3" else 0
         return 2 * flops, M * (2 * cout + 2 * cin + extra) * ab
     if kind == "wgrad" and conv == "global_feat":   # Gram of a5: upper tiles, reads a5 once
-        return flops * GRAM_TILE_FRACTION, M * cin * ab
+        return flops * GRAM_TILE_FRACTION, M * cin * a5b
     if conv == "global_feat" and kind == "fwd":     # reads a5; statistics + pool only, no store
-        return flops, M * cin * ab
+        return flops, M * cin * a5b
     if conv == "global_feat" and kind == "dgrad":   # a5 (also the ReLU mask) in, dz5 out
-        return flops, M * (cin + cout) * ab
+        return flops, M * (cin * a5b + cout * ab)
+    if conv == "conv5" and kind == "fwd":           # a4 in, a5 out
+        return flops, M * (cin * ab + cout * a5b)
     if conv == "conv5" and kind in ("dgrad", "wgrad"):   # folded form: dz5 + y4/128-wide out
         return flops, M * (cout + cin) * ab
     if kind == "fwd":
@@ -98,23 +120,28 @@ def kernel_model(tag, M, ab):
     return flops, nbytes
 
 
-def step_roofline(M, C, ab, measured_ms):
+def step_roofline(M, C, dtype, measured_ms):
     """t_roof = sum over layers of max(F_l / P_mfma, Bytes_l / 8 TB/s) for
     the whole fwd+bwd step (decomposed seg_conv1: local 64->512 GEMM; conv1 has no dgrad;
-    every activation read or written once per pass)."""
+    every activation read or written once per pass).  fp8: global_feat at the e4m3 peak with
+    a 1-byte input, conv5's output 1 byte."""
     layers = [(4, 64, 2), (64, 64, 3), (64, 64, 3), (64, 128, 3), (128, 1024, 3), (1024, 1024, 3),
               (64, 512, 3), (512, 256, 3), (256, 128, 3), (128, C, 3)]
-    peak = PEAK["bf16" if ab == 2 else "fp32"]
+    ab = act_bytes(dtype)
     t = 0.0
     for cin, cout, passes in layers:
+        wide = (cin, cout) == (1024, 1024)
+        peak = PEAK["fp8"] if dtype == "fp8" and wide else PEAK["bf16" if ab == 2 else "fp32"]
         f = 2.0 * M * cin * cout * passes
-        b = 3.0 * M * (cin + cout) * ab
+        ib = 1 if dtype == "fp8" and wide else ab
+        ob = 1 if dtype == "fp8" and cout == 1024 and cin == 128 else ab
+        b = 3.0 * M * (cin * ib + cout * ob)
         t += max(f / (peak["mfma"] * 1e12), b / (peak["hbm"] * 1e9))
     return {"t_roof_ms": round(t * 1e3, 3), "frac": round(t * 1e3 / measured_ms, 4),
             "model": "sum_l max(F_l/P_mfma, B_l/8TB/s), SURVEY 8(d)"}
 
 
-def northstar_64(kernels, M, ab):
+def northstar_64(kernels, M, dtype):
     """HBM-only fraction of the 64->64 conv fwd+bwd (conv2: fwd, dgrad, wgrad)
     against t_HBM = 6 x 64 ch x M x bytes / 8 TB/s."""
     tags = ("fwd:conv2", "dgrad:conv2", "wgrad:conv2")
@@ -123,7 +150,7 @@ def northstar_64(kernels, M, ab):
     if not all(t in kernels for t in tags):
         return None
     ms = sum(kernels[t][0] / kernels[t][1] for t in tags)
-    t_hbm = 6 * 64 * M * ab / (PEAK["bf16"]["hbm"] * 1e9) * 1e3
+    t_hbm = 6 * 64 * M * act_bytes(dtype) / (PEAK["bf16"]["hbm"] * 1e9) * 1e3
     return {"layer": "conv2 (64->64) fwd+dgrad+wgrad", "ms": round(ms, 4), "t_hbm_ms": round(t_hbm, 4),
             "hbm_frac": round(t_hbm / ms, 4)}
 
@@ -163,7 +190,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--scenes", type=int, default=4)
     ap.add_argument("--classes", type=int, default=2)
@@ -258,7 +285,6 @@ def main():
         dist.all_reduce(t)
         real_points = int(t.item())
     total_points = real_points * args.steps
-    ab = 2 if args.dtype == "bf16" else 4
     roof = None
     kernels = {}
     if timing:
@@ -268,32 +294,33 @@ def main():
         dom = max(kernels, key=lambda k: kernels[k][0])
         tot, cnt = kernels[dom]
         avg_s = tot / cnt / 1e3
-        mdl = kernel_model(dom, M, ab)
+        mdl = kernel_model(dom, M, args.dtype)
         if mdl:
             flops, nbytes = mdl
             ai = flops / nbytes
             tr = pmc_traffic(dom, args.dtype, args.workload, M)
-            ridge = PEAK[args.dtype]["mfma"] * 1e12 / (PEAK[args.dtype]["hbm"] * 1e9)
+            pk = kernel_peak(dom, args.dtype)
+            ridge = pk["mfma"] * 1e12 / (pk["hbm"] * 1e9)
             if ai >= ridge:
                 ach = flops / avg_s / 1e12
                 roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
-                        "peak": PEAK[args.dtype]["mfma"], "unit": "TFLOP/s",
-                        "frac": round(ach / PEAK[args.dtype]["mfma"], 4),
+                        "peak": pk["mfma"], "unit": "TFLOP/s",
+                        "frac": round(ach / pk["mfma"], 4),
                         "traffic": tr and tr["bytes"], "traffic_source": tr and tr["source"],
                         "algorithmic_bytes": nbytes,
                         "algorithmic_flops": flops, "avg_ms": round(avg_s * 1e3, 4)}
             else:
                 ach = nbytes / avg_s / 1e9
                 roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
-                        "peak": PEAK[args.dtype]["hbm"], "unit": "GB/s",
-                        "frac": round(ach / PEAK[args.dtype]["hbm"], 4),
+                        "peak": pk["hbm"], "unit": "GB/s",
+                        "frac": round(ach / pk["hbm"], 4),
                         "traffic": tr and tr["bytes"], "traffic_source": tr and tr["source"],
                         "algorithmic_bytes": nbytes, "avg_ms": round(avg_s * 1e3, 4)}
         if rank == 0:
             step_ms = el / args.steps * 1e3
             print(f"# per-kernel (avg ms, share of {step_ms:.2f} ms step):", file=sys.stderr)
             for tag, (tot, cnt) in sorted(kernels.items(), key=lambda kv: -kv[1][0]):
-                mdl = kernel_model(tag, M, ab)
+                mdl = kernel_model(tag, M, args.dtype)
                 extra = ""
                 if mdl:
                     a = tot / cnt / 1e3
@@ -314,11 +341,14 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": "fp8 e4m3 (global_feat, a5) + bf16" if args.dtype == "fp8" else args.dtype,
             "data": ("synthetic (dense voxel-centre clouds, seeded)" if rb is None else
                      "synthetic (occupied-only voxel-centre clouds, ragged, seeded)"),
-            "config": ({"workload": f"PointNetSegmentation train step, {B} scenes x {G}^3 points "
-                                    f"per GPU, C={C}", "global_batch": B * world,
+            "config": ({"workload": ("cfg5: " if args.dtype == "fp8" else "") +
+                                    f"PointNetSegmentation train step, {B} scenes x {G}^3 points "
+                                    f"per GPU, C={C}" + (", a5 + global_feat in fp8 e4m3 (MX-scaled "
+                                                         "MFMA)" if args.dtype == "fp8" else ""),
+                        "global_batch": B * world,
                         "points_per_scene": N, "parallelism": f"dp{world}"} if rb is None else
                        {"workload": f"cfg3: PointNetSegmentation train step, {B} occupied-only "
                                     f"ragged scenes per GPU on a {G}^3 lattice ({args.occupancy:g} "
@@ -327,8 +357,8 @@ def main():
                         "real_points_per_step": real_points, "parallelism": f"dp{world}"}),
             "loss": round(loss_v, 6),
             "roofline": roof,
-            "step_roofline": step_roofline(M, C, ab, el / args.steps * 1e3),
-            "northstar_64x64": northstar_64(kernels, M, ab) if kernels else None,
+            "step_roofline": step_roofline(M, C, args.dtype, el / args.steps * 1e3),
+            "northstar_64x64": northstar_64(kernels, M, args.dtype) if kernels else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec))

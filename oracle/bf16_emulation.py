@@ -21,6 +21,13 @@ keeps in bf16 is rounded to bf16 (round-to-nearest-even) at the point the HIP pa
   folded global_feat / conv5 operands H and diag(alpha) W (the Gram-form weight gradients,
   the pool rows and the per-scene sums csum_b stay fp32).
 
+With ``store="fp8"`` the bf16 rounding above applies and, as the HIP fp8 path (compute dtype
+"fp8") stores them, a5 is rounded to e4m3 (OCP e4m3fn, nearest-even, saturating at 448) and
+global_feat's weight and the folded H are e4m3 rows with one power-of-two scale each
+(pcs_quant_fp8_rows: scale 2^ceil(log2(row max / 448))); the max-pool rows and the
+Gram-form weight gradient use the dequantized global_feat weight, as the HIP path does.
+``return_logits=True`` also returns the logits (float32 [M, C]).
+
 Memory is kept to the tensors the backward needs (about 9 KB per point plus a few [M, 1024]
 temporaries), so 4 scenes x 64^3 points run on a 64 GB host.
 """
@@ -41,6 +48,25 @@ def round_bf16(a):
     return r.view(F32)
 
 
+def round_e4m3(a):
+    """float32 -> nearest-even e4m3fn (4 significant bits, subnormal step 2^-9, |x| <= 448),
+    returned as float32."""
+    a = np.asarray(a, dtype=np.float64)
+    _, e = np.frexp(a)                                    # |a| in [2^(e-1), 2^e)
+    q = np.exp2(np.maximum(e - 4, -9).astype(np.float64))  # quantum of a's binade
+    r = np.round(a / q) * q                              # np.round: half to even
+    return np.clip(r, -448.0, 448.0).astype(F32)
+
+
+def quant_rows_e4m3(W):
+    """Row-scaled e4m3 copy of W (dequantized float32), as pcs_quant_fp8_rows."""
+    W = np.asarray(W, dtype=F32)
+    mx = np.abs(W).max(axis=1).astype(np.float64)
+    e = np.where(mx > 0, np.ceil(np.log2(np.where(mx > 0, mx, 1.0) / 448.0)), 0.0)
+    e = np.clip(e, -126, 127)
+    return (round_e4m3(W * np.exp2(-e)[:, None].astype(F32)).astype(np.float64) * np.exp2(e)[:, None]).astype(F32)
+
+
 def _stats(Y):
     """Batch mean and biased variance per column, fp64 accumulation (the HIP finalisation
     merges fp32 partials in fp64)."""
@@ -53,11 +79,12 @@ def _stats(Y):
     return mean, var / Y.shape[0]
 
 
-def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P):
+def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_logits=False):
     """One reference training step (without the optimizer).  Returns (loss, grads) with
     grads keyed by state-dict parameter name (float64 arrays); conv biases that BN cancels
     are returned as zeros (analytically ~0 in every path)."""
-    R = round_bf16 if store == "bf16" else (lambda a: np.ascontiguousarray(a, dtype=F32))
+    R = round_bf16 if store in ("bf16", "fp8") else (lambda a: np.ascontiguousarray(a, dtype=F32))
+    fp8 = store == "fp8"
     B, N, D = x.shape
     M = B * N
     X = x.reshape(M, D).astype(F32)
@@ -65,6 +92,8 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P):
                                     "seg_conv1", "seg_conv2", "seg_conv3", "seg_conv4")}
     Wr = {n: R(W[n]) for n in ("conv2", "conv3", "conv4", "conv5", "global_feat", "seg_conv2", "seg_conv3")}
     Wr["seg_conv1_l"] = R(W["seg_conv1"][:, :64])
+    if fp8:
+        Wr["global_feat"] = quant_rows_e4m3(W["global_feat"])
     Wg1 = np.ascontiguousarray(W["seg_conv1"][:, 64:])     # global half: fp32 (pcs_scene_gemv)
     gam = {bn: sd[f"{bn}.weight"].astype(np.float64) for bn in
            ("bn1", "bn2", "bn3", "bn4", "bn5", "bn_global", "bn_seg1", "bn_seg2", "bn_seg3")}
@@ -102,7 +131,7 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P):
     A4 = R(act(Y4, "bn4"))
     y5 = A4 @ Wr["conv5"].T                              # fp32 accumulators
     cache["bn5_st"] = bn_coef("bn5", *_stats(y5))
-    a5 = R(act(y5, "bn5"))
+    a5 = round_e4m3(act(y5, "bn5")) if fp8 else R(act(y5, "bn5"))
     del y5
     yg = a5 @ Wr["global_feat"].T
     mg, vg = _stats(yg)
@@ -194,12 +223,12 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P):
     gc = -al * rstd * S2 / M
     bc = -al * S1 / M - gc * mean
     Wgr = Wr["global_feat"].astype(np.float64)
-    H = R((Wgr.T * gc) @ Wgr)
+    H = quant_rows_e4m3((Wgr.T * gc) @ Wgr) if fp8 else R((Wgr.T * gc) @ Wgr)
     cvec = (Wgr.T @ bc).astype(F32)
     dA5 = a5 @ H + cvec
     rows = idx + (np.arange(B) * N)[:, None]
     sp = al * dzs                                                     # [B, 1024]
-    Wg32 = W["global_feat"].astype(np.float64)
+    Wg32 = Wgr if fp8 else W["global_feat"].astype(np.float64)
     for b in range(B):
         np.add.at(dA5, rows[b], (sp[b][:, None] * Wg32).astype(F32))
     dz5 = np.where(a5 > 0, dA5, F32(0))
@@ -251,4 +280,6 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P):
     dy = gam["bn1"] * rstd * (R(dz).astype(np.float64) - S1 / M - xh * (S2 / M))   # conv1 wgrad: fp32 dy
     grads["conv1.weight"] = (dy.T @ X.astype(np.float64))[:, :, None]
     grads["conv1.bias"] = np.zeros(64)
+    if return_logits:
+        return loss, grads, logits
     return loss, grads

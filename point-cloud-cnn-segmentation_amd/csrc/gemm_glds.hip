@@ -504,58 +504,57 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
       const uint32_t *mrow = mbits + ((qs / nks) & 1) * 2048 + wn * 2;
       const bool full = valid == BM;   // uniform: only a scene's last tile is partial
-      // masking: v = acc & (0 - bit) (v_bfe_i32 sign-extends the keep bit to a full mask).
+      float s1[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = 0.f;
       // Stores widened to 16 B (cdna_hip_programming.md T21 with v_permlane16_swap): a lane
       // holds 4 columns (8 B) of tile j; swapping tile j with tile j+1 between lane groups
       // 2h and 2h+1 leaves each lane 8 consecutive columns of tile j + (lg & 1), so every
-      // store instruction writes 16 rows x 64 contiguous bytes instead of 16 x 32.  One tile
-      // pair (q) at a time: 8 column sums and one mask word live, not 16 and two.
+      // store instruction writes 16 rows x 64 contiguous bytes instead of 16 x 32.
       const int scol = n0 + wn * 64 + 16 * (lg & 1) + 8 * (lg >> 1);
-      float S1 = 0.f;
+      // masking: v = acc & (0 - bit) (v_bfe_i32 sign-extends the keep bit to a full mask)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        float s1[2][4];
+      for (int i = 0; i < 8; ++i) {
+        const bool ok = full || ((rowok >> i) & 1u);
+        const uint2 mw = *reinterpret_cast<const uint2 *>(mrow + (wm * 128 + i * 16 + lr) * 8);
+        uint32_t pk[4][2];
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
+        for (int j = 0; j < 4; ++j) {
+          const int word = (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg));
+          float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s1[jj][r] = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const bool ok = full || ((rowok >> i) & 1u);
-          const uint32_t mw = mrow[(wm * 128 + i * 16 + lr) * 8 + q];
-          uint32_t pk[2][2];
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const int word = (int)(mw >> (jj * 16 + 4 * lg));
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
-              v[r] = __uint_as_float(__float_as_uint(acc[i][2 * q + jj][r]) & keep);
-              s1[jj][r] += ok ? v[r] : 0.f;
-            }
-            pk[jj][0] = pack2bf(v[0], v[1]);
-            pk[jj][1] = pack2bf(v[2], v[3]);
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
+            v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
+            s1[j][r] += ok ? v[r] : 0.f;
           }
+          pk[j][0] = pack2bf(v[0], v[1]);
+          pk[j][1] = pack2bf(v[2], v[3]);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
-            pk[0][h] = sw[0];
-            pk[1][h] = sw[1];
+            const auto sw = __builtin_amdgcn_permlane16_swap(pk[2 * q][h], pk[2 * q + 1][h], false, false);
+            pk[2 * q][h] = sw[0];
+            pk[2 * q + 1][h] = sw[1];
           }
           if (ok)
             // plain store: dz5 is re-read right away by conv5's backward (nt measured 1 ms slower)
             *reinterpret_cast<u32x4 *>(Cg + (rb + wm * 128 + i * 16 + lr) * Ncols + scol + 32 * q) =
-                mk_u32x4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
+                mk_u32x4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
         }
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float t = row_sum(s1[jj][r]);
-            if (lr == (2 * q + jj) * 4 + r) S1 = t;
-          }
       }
+      float S1 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = row_sum(s1[j][r]);
+          if (lr == j * 4 + r) S1 = t;
+        }
       if (do_stats) run[cme].x += S1;
       // The stores count in vmcnt but are not waited for here: the next counted wait
       // (vmcnt(10), phase 1) only relies on the LOADS completing in order among themselves

@@ -223,7 +223,9 @@ class Engine:
         return wc
 
     def _quant_fp8(self, W):
-        """(e4m3 rows, E8M0 row scales, fp32 dequantized copy) of a 2-D fp32 matrix."""
+        """(e4m3 rows, E8M0 row scales, fp32 dequantized copy) of an fp32 [rows, cols(, 1)]
+        matrix."""
+        W = W.reshape(W.shape[0], -1)
         rows, cols = W.shape
         dev = W.device
         Wq = torch.empty(rows, cols, dtype=torch.uint8, device=dev)

@@ -82,7 +82,10 @@ class PointNetSegmentation(nn.Module):
     """MI355X-native PointNetSegmentation (P:65-133).
 
     ``compute_dtype``: ``"fp32"`` (default; exact-f32 MFMA, parity with the reference's
-    fp32 CPU path) or ``"bf16"`` (bf16 MFMA, fp32 accumulation and BN statistics).
+    fp32 CPU path), ``"bf16"`` (bf16 MFMA, fp32 accumulation and BN statistics) or ``"fp8"``
+    (the bf16 path with the 1024-wide layer in e4m3: conv5 stores a5 as fp8 and global_feat's
+    forward, input gradient and Gram run on MX-scaled fp8 MFMA with per-row E8M0 weight
+    scales; fp32 accumulation and BN statistics throughout).
     """
 
     def __init__(self, num_classes, input_dim=4, *, compute_dtype: str = "fp32"):

@@ -32,3 +32,20 @@ def test_fp32_mode_is_the_reference_step():
             continue
         err = np.linalg.norm(g32[n].ravel() - v.ravel()) / max(np.linalg.norm(v), 1e-3 * gmax)
         assert err < 5e-3, (n, err)
+
+
+def test_e4m3_rounding_matches_torch():
+    """round_e4m3 / quant_rows_e4m3 (the fp8 storage emulation) against torch's
+    float8_e4m3fn cast, bit for bit, over normal and subnormal binades."""
+    import torch
+    from bf16_emulation import quant_rows_e4m3, round_e4m3
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(100000) * np.exp2(rng.integers(-14, 9, 100000))).astype(np.float32)
+    x = np.clip(x, -448, 448)
+    ref = torch.from_numpy(x).to(torch.float8_e4m3fn).float().numpy()
+    assert np.array_equal(round_e4m3(x), ref)
+    W = (rng.standard_normal((32, 100)) * 0.02).astype(np.float32)
+    mx = np.abs(W).max(1)
+    e = np.ceil(np.log2(mx / 448.0))
+    ref = torch.from_numpy(W * np.exp2(-e)[:, None].astype(np.float32)).to(torch.float8_e4m3fn).double().numpy()
+    assert np.array_equal(quant_rows_e4m3(W), (ref * np.exp2(e)[:, None]).astype(np.float32))
