@@ -187,10 +187,11 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
     for (int h = 0; h < 2; ++h) boff[h][g] = (uint32_t)b_row(h, qrow[g]) * (uint32_t)rowbytes + cbyte[g];
   }
-  auto issue = [&](int qseq, int region) {
+  // (qseq, tl, kt): K-tile sequence number and its (row tile, K-tile) -- the loop keeps the
+  // latter as counters, so the scalar path has no divisions
+  auto issue = [&](int qseq, int tl, int kt, int region) {
     if (qseq >= total) return;   // nothing left to prefetch: the loop's tail waits shrink
                                  // to match (see the phase waits below)
-    const int tl = qseq / nks, kt = qseq - tl * nks;
     char *dst = lds + (qseq & 1) * KBUF + region * REG;
     if (region < 2) {
       const int64_t rb = row0 + (int64_t)tl * BM;
@@ -320,8 +321,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   };
 
   // ---- prologue: K-tile 0 landed; A-lo, B-lo, B-hi of K-tile 1 in flight
-  issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
-  issue(1, 0); issue(1, 2); issue(1, 3);
+  const int tl1 = nks == 1 ? 1 : 0, kt1 = nks == 1 ? 0 : 1;   // K-tile 1
+  issue(0, 0, 0, 0); issue(0, 0, 0, 1); issue(0, 0, 0, 2); issue(0, 0, 0, 3);
+  issue(1, tl1, kt1, 0); issue(1, tl1, kt1, 2); issue(1, tl1, kt1, 3);
   wait_vm<6>();
   barrier_raw();
 
@@ -335,14 +337,20 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   // a region one phase after its last read safe across the stagger.
   if (wm == 1) barrier_raw();
 
-  for (int qs = 0; qs < total; ++qs) {
+  int kt = 0, tcur = 0, ta = 0, ka = 0;   // (row tile, K-tile) of qs and of qs + 1
+  for (int qs = 0; qs < total; ++qs, kt = ka, tcur = ta) {
     const int buf = qs & 1;
-    const int kt = qs % nks;
+    // (row tile, K-tile) of qs + 1 and qs + 2
+    const bool w1 = kt + 1 == nks;
+    ta = w1 ? tcur + 1 : tcur;
+    ka = w1 ? 0 : kt + 1;
+    const bool w2 = ka + 1 == nks;
+    const int tb = w2 ? ta + 1 : ta, kb = w2 ? 0 : ka + 1;
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
     read_a(buf, 0);
     read_b(buf, 2, 0);
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 0, kt - kq0, (qs / nks) & 1);
-    issue(qs + 1, 1);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 0, kt - kq0, tcur & 1);
+    issue(qs + 1, ta, ka, 1);
     // every counted wait assumes the five regions issued after the one it retires are in
     // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
     // regions actually issued (phase 1 retires B-hi(qs): newer are A-hi(qs) and, unless qs is
@@ -356,7 +364,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 2: (lo, hi); restage A-lo of K-tile qs+2
     read_b(buf, 3, 2);
-    issue(qs + 2, 0);
+    issue(qs + 2, tb, kb, 0);
     // retires A-hi(qs): newer are the four regions of qs+1 and A-lo(qs+2)
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<8>(); else wait_vm<0>();
     wait_lgkm0();
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
-    issue(qs + 2, 2);
+    issue(qs + 2, tb, kb, 2);
     wait_lgkm0();
     barrier_raw();
     __builtin_amdgcn_s_setprio(1);
@@ -377,8 +385,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 4: (hi, hi); restage B-hi of K-tile qs+2.  A-hi's mask bits are taken here, not
     // in phase 3: B-lo's fragments are dead by now, which keeps the extraction's registers
     // out of the accumulators' way (A-hi(qs) is restaged only in phase 1 of qs+1)
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 1, kt - kq0, (qs / nks) & 1);
-    issue(qs + 2, 3);
+    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 1, kt - kq0, tcur & 1);
+    issue(qs + 2, tb, kb, 3);
     // retires A-lo(qs+1), B-lo(qs+1): newer are B-hi(qs+1), A-hi(qs+1) and three of qs+2
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();
     barrier_raw();
@@ -389,8 +397,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 
     if (kt != nks - 1) continue;
 
-    // ===================== epilogue of row tile qs / nks =====================
-    const int64_t rb = row0 + (int64_t)(qs / nks) * BM;
+    // ===================== epilogue of row tile tcur =====================
+    const int64_t rb = row0 + (int64_t)tcur * BM;
     const int valid = (int)pcs_min64(BM, scene_end - rb);
     const int nvw = max(0, min(128, valid - wm * 128));   // valid rows of this wave's half
     // lane's columns c(j, r) = wn*64 + j*16 + 4*lg + r; rows m(i) = wm*128 + i*16 + lr
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       }
     } else {   // MODE_DGRAD
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
-      const uint32_t *mrow = mbits + ((qs / nks) & 1) * 2048 + wn * 2;
+      const uint32_t *mrow = mbits + (tcur & 1) * 2048 + wn * 2;
       const bool full = valid == BM;   // uniform: only a scene's last tile is partial
       float s1[4][4];
 #pragma unroll
