@@ -54,10 +54,11 @@ LAYER_DIMS = {"conv1": (4, 64), "conv2": (64, 64), "conv3": (64, 64), "conv4": (
 
 
 # bench tag -> HIP kernel symbol (as summarised from rocprofv3 in profiles/pmc_<round>.json)
+# (the template's bool is the fp8 form)
 TAG_KERNEL = {
-    "wgrad:global_feat": "gram_glds_kernel",                   # LDS-DMA Gram a5^T a5 (upper tiles)
-    "fwd:global_feat": "gemm_glds_kernel<0>",                  # LDS-DMA: BN stats + max-pool epilogue
-    "dgrad:global_feat": "gemm_glds_kernel<1>",                # LDS-DMA: folded a5 H, mask, sparse rows
+    "wgrad:global_feat": "gram_glds_kernel<{f}>",              # LDS-DMA Gram a5^T a5 (upper tiles)
+    "fwd:global_feat": "gemm_glds_kernel<0, {f}>",             # LDS-DMA: BN stats + max-pool epilogue
+    "dgrad:global_feat": "gemm_glds_kernel<1, {f}>",           # LDS-DMA: folded a5 H, ReLU mask
 }
 GRAM_TILE_FRACTION = 10.0 / 16.0   # upper 256-tiles of the symmetric 1024 x 1024 Gram
 
@@ -71,6 +72,7 @@ def pmc_traffic(tag, dtype, workload, points):
     sym = TAG_KERNEL.get(tag)
     if sym is None:
         return None
+    sym = sym.format(f="true" if dtype == "fp8" else "false")
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)

@@ -316,7 +316,7 @@ int pcs_head(const pcs_head_args *args, pcs_stream_t stream);
 int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weight,
                       int32_t C, int64_t *counts_ws, float *out, pcs_stream_t stream);
 
-/* Dropout(p) keep bits (P:96, P:124, P:126): Philox4x32-10(seed, offset + element),
+/* Dropout(p) keep bits (P:96, P:124, P:126): Philox4x32-7(seed, offset + element),
  * keep = u >= p, 8 bits per byte along the channel dimension; bits[M, C/8]. */
 int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
                      uint8_t *bits, pcs_stream_t stream);
@@ -350,7 +350,9 @@ int pcs_quant_fp8_rows(const float *W, int64_t rows, int64_t cols, int64_t ldw, 
  * applied after a PCS_EPI_DGRAD pcs_gemm that ran without pool_w (the LDS-DMA kernel):
  *   dz[m, n] += (Yp[m, n] > 0) * sum_{c : pool_idx[b, c] == m} pool_coef[b, c] pool_w[c, n]
  * for every distinct argmax row m (global row index) of scene b; the same term is added to
- * S1 (stats[.].x) of the scene's first chunk.  pool_idx / pool_coef: [B, pool_c].
+ * S1 (stats[.].x) of the scene's chunk partials (spread over its first min(16,
+ * chunks_per_scene) chunks; their sum is what the BN backward reads).  pool_idx / pool_coef:
+ * [B, pool_c].
  */
 int pcs_pool_rows_add(void *dz, int32_t dz_dtype, const void *Yp, int32_t yp_dtype, int64_t num_scenes,
                       int64_t scene_rows, int32_t Ncols, const int32_t *pool_idx, const float *pool_coef,

@@ -636,13 +636,18 @@ int pcs_gemm_glds_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s
 // pcs_pool_rows_add: the max-pool rows' term of global_feat's folded input gradient, after
 // the LDS-DMA kernel (which leaves it out, see the top of this file):
 //   dz[m, n] += (Yp[m, n] > 0) * sum_{c : idx[b, c] == m} coef[b, c] * Wp[c, n]
-// for every distinct argmax row m of scene b, and the same term summed into S1 of the scene's
-// first chunk.  One block per (scene, 256 columns), thread = column; the scene's (row,
-// channel) pairs are rank-sorted in LDS so equal rows are applied once, in a fixed order.
+// for every distinct argmax row m of scene b, and the same term summed into S1.  Block
+// (256 columns, scene, part): thread = column; the scene's (row, channel) pairs are rank-sorted
+// in LDS so equal rows are applied once, in a fixed order, and the sorted list is cut into
+// `parts` ranges at row boundaries (a row's pairs never straddle two blocks), so 1024 pairs
+// are not one 1024-long dependent load chain per thread.  Part j adds its S1 share into chunk
+// j's partial (j < chunks_per_scene): the partials are summed over chunks later, so no two
+// threads update one value and the result is deterministic.
 // ---------------------------------------------------------------------------------------
 namespace {
 
 constexpr int PR_MAXC = 1024;
+constexpr int PR_PARTS = 16;
 
 template <typename T, typename TY>
 __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, const TY *__restrict__ Yp, int64_t N,
@@ -651,7 +656,7 @@ __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, 
                                                             int64_t ldw, int P, float *__restrict__ stats, int cps) {
   __shared__ int rows[PR_MAXC], srow[PR_MAXC];
   __shared__ int sch[PR_MAXC];
-  const int b = blockIdx.y, tid = threadIdx.x;
+  const int b = blockIdx.y, part = blockIdx.z, parts = gridDim.z, tid = threadIdx.x;
   const int n = blockIdx.x * 256 + tid;
   for (int c = tid; c < P; c += 256) rows[c] = idx[(int64_t)b * P + c];
   __syncthreads();
@@ -666,12 +671,19 @@ __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, 
     sch[rank] = c;
   }
   __syncthreads();
-  if (n >= Ncols) return;
+  // this part's range [p0, p1): the nominal cut points moved forward to a row boundary
+  auto cut = [&](int j) {
+    int p = (int)((int64_t)j * P / parts);
+    while (p > 0 && p < P && srow[p] == srow[p - 1]) ++p;
+    return p;
+  };
+  const int p0 = cut(part), p1 = cut(part + 1);
+  if (n >= Ncols || p0 >= p1) return;
   float ds1 = 0.f, v = 0.f;
-  for (int p = 0; p < P; ++p) {
+  for (int p = p0; p < p1; ++p) {
     const int c = sch[p];
     v = fmaf(coef[(int64_t)b * P + c], Wp[(int64_t)c * ldw + n], v);
-    if (p + 1 == P || srow[p + 1] != srow[p]) {   // last pair of this row: apply
+    if (p + 1 == p1 || srow[p + 1] != srow[p]) {   // last pair of this row: apply
       const int64_t o = (int64_t)srow[p] * Ncols + n;
       if (load_elem(Yp, o) > 0.f) {
         const float d = load_elem(dz, o) + v;
@@ -682,7 +694,7 @@ __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, 
       v = 0.f;
     }
   }
-  if (stats) stats[((int64_t)b * cps * Ncols + n) * 2] += ds1;
+  if (stats) stats[(((int64_t)b * cps + part) * Ncols + n) * 2] += ds1;
 }
 
 }  // namespace
@@ -695,7 +707,8 @@ extern "C" int pcs_pool_rows_add(void *dz, int32_t dz_dtype, const void *Yp, int
       pool_c <= 0 || pool_c > PR_MAXC || pool_ldw < Ncols || (stats && chunks_per_scene <= 0))
     return pcs_set_einval("pcs_pool_rows_add", "bad arguments (0 < pool_c <= 1024, pool_ldw >= Ncols)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((Ncols + 255) / 256, (unsigned)num_scenes);
+  const int parts = stats ? (chunks_per_scene < PR_PARTS ? chunks_per_scene : PR_PARTS) : PR_PARTS;
+  const dim3 grid((Ncols + 255) / 256, (unsigned)num_scenes, (unsigned)parts);
 #define PCS_PRA(T, TY)                                                                                          \
   hipLaunchKernelGGL((pool_rows_add_kernel<T, TY>), grid, dim3(256), 0, s, static_cast<T *>(dz),                 \
                      static_cast<const TY *>(Yp), scene_rows, (int)Ncols, pool_idx, pool_coef, pool_w, pool_ldw, \

@@ -731,10 +731,11 @@ __global__ void ce_wsum_kernel(const unsigned long long *counts, const float *w,
   out[2] = s > 0 ? (float)(1.0 / s) : 0.f;
 }
 
-// Philox4x32-10
+// Philox4x32-7 (Salmon et al. 2011: 7 rounds already pass BigCrush; the 10-round default's
+// margin cost 0.5 ms per step in dropout_bits, which is ALU-bound)
 PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < 7; ++i) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0];
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr[2];
     const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;

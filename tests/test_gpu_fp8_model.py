@@ -15,9 +15,13 @@ Prediction-level bounds (measured r02, tools/fp8_accuracy.py, bound = measured +
   0.878 .. 0.956; bf16 0.955 .. 0.985) with |mIoU_fp8 - mIoU_fp32| <= 5e-3 (measured
   0.9e-3 .. 3.1e-3; bf16 0.2e-3 .. 1.8e-3): not 1e-3, and the emulation above shows that
   is what e4m3's 3 mantissa bits cost there, not a kernel error.
-* cfg2 size (4 x 128^3) with weights trained 300 steps in fp32 (eval-mode BN): agreement
-  >= 0.99 (measured 0.9977), |dmIoU| <= 1e-3 (measured 3.5e-4).  The path is deterministic
-  (fixed-order reductions, Philox dropout), so this is one fixed measurement, not a sample.
+* cfg2 size (4 x 128^3) with weights trained 3000 steps in fp32 on cfg1-sized scenes
+  (eval-mode BN): agreement >= 0.998 (measured 0.99906; bf16 0.99942), |dmIoU| <= 1e-3
+  (measured 5.4e-4; bf16 6e-5).  How far a prediction flip moves mIoU depends on how many
+  points sit near a decision boundary: after only 200-600 steps agreement is 0.987-0.998 and
+  |dmIoU| ranged 3.5e-4 .. 7.7e-3 for fp8 and 6e-5 .. 4.5e-3 for bf16 over training
+  lengths and dropout streams (tools/fp8_accuracy.py).  The path is deterministic
+  (fixed-order reductions, Philox dropout), so each figure is one fixed measurement.
 * training: 300 fp8 steps from the fp32 run's init track the fp32 loss curve (mean of the
   last 100 losses within 0.03; measured 600-step curves within 0.01).
 """
@@ -88,19 +92,18 @@ def test_fp8_golden_predictions_track_fp32(name):
     assert 0.5 <= err_hip / err_emu <= 2.0
 
 
-@pytest.fixture(scope="module")
-def trained():
-    """dtype -> (trained state, per-step losses): 300 steps on cfg1-sized scenes from one
-    init, in fp32 and in fp8."""
+def _train(dtypes, steps):
+    """dtype -> (trained state, per-step losses): ``steps`` FusedTrainStep + FusedAdam steps
+    on cfg1-sized synthetic scenes from one seeded init."""
     from pcs_amd.data import class_weights, synthetic_batch
     from pcs_amd.model import PointNetSegmentation
     from pcs_amd.optim import FusedAdam
     from pcs_amd.train import FusedTrainStep
-    C, B, N, steps = 2, 4, 4096, 300
+    C, B, N = 2, 4, 4096
     torch.manual_seed(0)
     init = {k: v.clone() for k, v in PointNetSegmentation(C).state_dict().items()}
     res = {}
-    for dt in ("fp32", "fp8"):
+    for dt in dtypes:
         m = _model(init, C, dt, True)
         opt = FusedAdam(m, lr=1e-3, weight_decay=1e-4)
         losses = []
@@ -114,6 +117,11 @@ def trained():
     return res
 
 
+@pytest.fixture(scope="module")
+def trained():
+    return _train(("fp32", "fp8"), 300)
+
+
 def test_fp8_training_tracks_fp32(trained):
     l32, l8 = trained["fp32"][1], trained["fp8"][1]
     assert np.isfinite(l8).all()
@@ -122,19 +130,22 @@ def test_fp8_training_tracks_fp32(trained):
     assert l8[-100:].mean() < l8[:10].mean() - 0.05        # it learns
 
 
-def test_fp8_cfg2_predictions_track_fp32(trained):
+def test_fp8_cfg2_predictions_track_fp32():
     from pcs_amd.data import synthetic_batch
-    sd = trained["fp32"][0]
+    sd = _train(("fp32",), 3000)["fp32"][0]
     pts, lab, _ = synthetic_batch(4242, [128 ** 3] * 4, 2, grid=128, dense=True)
     x, y = torch.from_numpy(pts).to(DEV), torch.from_numpy(lab).to(DEV)
     del pts, lab
     out = {}
-    for dt in ("fp32", "fp8"):
+    for dt in ("fp32", "bf16", "fp8"):
         m = _model(sd, 2, dt, False)
         with torch.no_grad():
             out[dt] = m(x).float()
         del m
+    m32 = _miou(out["fp32"], y, 2)
+    for dt in ("bf16", "fp8"):
+        print(f"cfg2: {dt} argmax agreement {_agree(out[dt], out['fp32'], y):.5f}, mIoU {_miou(out[dt], y, 2):.5f} "
+              f"(fp32 {m32:.5f})")
     agree = _agree(out["fp8"], out["fp32"], y)
-    m32, m8 = _miou(out["fp32"], y, 2), _miou(out["fp8"], y, 2)
-    print(f"cfg2: fp8 argmax agreement {agree:.5f}, mIoU fp8 {m8:.5f} fp32 {m32:.5f} (diff {m8 - m32:+.2e})")
-    assert agree >= 0.99 and abs(m8 - m32) <= 1e-3
+    m8 = _miou(out["fp8"], y, 2)
+    assert agree >= 0.998 and abs(m8 - m32) <= 1e-3

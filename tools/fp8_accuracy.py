@@ -75,13 +75,13 @@ def golden():
         compare(logits, y, C, name)
 
 
-def train_curves(steps):
+def train_curves(steps, dtypes=DTYPES):
     print(f"2. training {steps} steps from one init (cfg1-size scenes, C=2)")
     C, B, N = 2, 4, 4096
     torch.manual_seed(0)
     init = {k: v.clone() for k, v in PointNetSegmentation(C).state_dict().items()}
     trained = {}
-    for dt in DTYPES:
+    for dt in dtypes:
         m = model_from(init, C, dt, True)
         opt = FusedAdam(m, lr=1e-3, weight_decay=1e-4)
         losses = []
@@ -96,7 +96,7 @@ def train_curves(steps):
         trained[dt] = {k: v.detach().clone() for k, v in m.state_dict().items()}
     pts, lab, _ = synthetic_batch(99, [N] * B, C, grid=32)
     x, y = torch.from_numpy(pts).to(DEV), torch.from_numpy(lab).to(DEV)
-    for dt in DTYPES:
+    for dt in dtypes:
         for de in DTYPES:
             m = model_from(trained[dt], C, de, False)
             with torch.no_grad():
@@ -129,8 +129,9 @@ def trained_eval(sd):
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    golden()
-    sd = train_curves(steps)
+    if os.environ.get("FP8ACC_GOLDEN", "1") == "1":
+        golden()
+    sd = train_curves(steps, tuple(os.environ.get("FP8ACC_TRAIN", ",".join(DTYPES)).split(",")))
     trained_eval(sd)
 
 
