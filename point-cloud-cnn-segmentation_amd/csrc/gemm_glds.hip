@@ -42,6 +42,7 @@ constexpr int OFF_RUNN = OFF_BIAS + 256 * 4;       // [2] f32: rows merged per w
 constexpr int OFF_UNI = OFF_RUNN + 16;             // 16 KB, per mode:
 constexpr int OFF_POOL = OFF_UNI;                  //   FWD: [2][256] float4 max, argmax, min, argmin
 constexpr int OFF_SGN = OFF_UNI + 2 * 256 * 16;    //        [256] f32 +1 / -1 (pool keeps max / min)
+constexpr int OFF_CUR = OFF_SGN + 256 * 4;         //        [2][256] f32 running max of sgn * y
 constexpr int OFF_MASK = OFF_UNI;                  //   DGRAD: 2 x [256 rows][8 words] ReLU mask bits
 constexpr int LDS_BYTES = OFF_UNI + 2 * 256 * 8 * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   float *lbias = reinterpret_cast<float *>(lds + OFF_BIAS);
   float *runn = reinterpret_cast<float *>(lds + OFF_RUNN);
   float *lsgn = reinterpret_cast<float *>(lds + OFF_SGN);
+  float *lcur = reinterpret_cast<float *>(lds + OFF_CUR);
   uint32_t *mbits = reinterpret_cast<uint32_t *>(lds + OFF_MASK);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -167,9 +169,11 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     if constexpr (MODE == MODE_FWD) {
       lsgn[tid] = (a.es && a.es[n0 + tid] < 0.f) ? -1.f : 1.f;
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h) {
         runp[h * BN + tid] = make_float4(-__builtin_huge_valf(), __int_as_float(0x7fffffff),
                                          __builtin_huge_valf(), __int_as_float(0x7fffffff));
+        lcur[h * BN + tid] = -__builtin_huge_valf();
+      }
     }
   }
   if (tid < 2) runn[tid] = 0.f;
@@ -461,28 +465,45 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         }
         if (do_pool) {
           // only the extremum pool_finalize will use: max where es >= 0 (bn scale > 0), min
-          // where es < 0, as vx = max(sgn * y); the argmax row is searched only for columns
-          // whose running extremum this tile improves (rare after the first tiles)
-          const float4 q = runp[cme];
-          const float sgl = lsgn[cme - wm * BN];
-          const float cur = sgl > 0.f ? q.x : -q.z;
+          // where es < 0, as the max of sgn * y.  Fast path: each lane compares its own 8-row
+          // maxima with the half's running maxima (lcur, read 4 columns per ds_read_b128) and
+          // the wave moves on unless some lane beats one -- after the first tiles of a chunk
+          // that is rare, so the 16-lane reductions and the argmax search below (the slow
+          // path) run on few tiles.
+          const float *cur4 = lcur + wm * BN + wn * 64 + 4 * lg;
+          const float *sgn4 = lsgn + wn * 64 + 4 * lg;
+          uint32_t beat = 0;   // bit j: this lane beats a running max in tile column block j
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
+            const float4 c4 = *reinterpret_cast<const float4 *>(cur4 + j * 16);
+            const float4 g4 = *reinterpret_cast<const float4 *>(sgn4 + j * 16);
+            const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
+            bool bj = false;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float mx = -__builtin_huge_valf();
+#pragma unroll
+              for (int i = 0; i < 8; ++i)
+                if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, gg[r] * acc[i][j][r]);
+              bj |= mx > cc[r];
+            }
+            beat |= (uint32_t)bj << j;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (__builtin_amdgcn_ballot_w64((beat >> j) & 1u) == 0) continue;   // uniform
+            const float4 q = runp[cme];
+            const float sgl = lsgn[cme - wm * BN];
+            const float cur = sgl > 0.f ? q.x : -q.z;
             float vx[4], sg[4];
             float mine = -__builtin_huge_valf();
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              sg[r] = lsgn[wn * 64 + j * 16 + 4 * lg + r];
-              // max of sg * y over the lane's rows (= max y, or -min y where bn_global's scale < 0)
+              sg[r] = sgn4[j * 16 + r];
               float mx = -__builtin_huge_valf();
-              if (tile_full) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) mx = fmaxf(mx, sg[r] * acc[i][j][r]);
-              } else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                  if ((rowok >> i) & 1u) mx = fmaxf(mx, sg[r] * acc[i][j][r]);
-              }
+              for (int i = 0; i < 8; ++i)
+                if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, sg[r] * acc[i][j][r]);
               vx[r] = row_max(mx);
               if (lr == j * 4 + r) mine = vx[r];
             }
@@ -502,6 +523,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                 if (sgl > 0.f) { u.x = vx[r]; u.y = __int_as_float(ix); }
                 else { u.z = -vx[r]; u.w = __int_as_float(ix); }
                 runp[cme] = u;
+                lcur[cme] = vx[r];
               }
             }
           }

@@ -72,13 +72,13 @@ def main():
         Wf = W.float()
         L.call("pcs_quant_fp8_rows", L.ptr(Wf), Nc, K, K, L.ptr(W8), L.ptr(wsc), None, L.stream_ptr())
 
-        def run8(name, epi, **kw):
+        def run8(name, epi, stats=True, pool=True, **kw):
             a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=Nc, dtype=L.BF16, prologue=L.PRO_RAW,
                            epilogue=epi, chunks_per_scene=0, flags=L.FLAG_AW_FP8)
             lib.pcs_gemm_geometry(ct.byref(a))
             nch = B * a.chunks_per_scene
-            keep = dict(stats=torch.empty(nch, Nc, 2, device=dev))
-            if epi == L.EPI_FWD:
+            keep = dict(stats=torch.empty(nch, Nc, 2, device=dev)) if stats else {}
+            if epi == L.EPI_FWD and pool:
                 keep["pool"] = torch.empty(nch, Nc, 4, device=dev)
             a.A, a.W, a.w_scale = A8.data_ptr(), W8.data_ptr(), wsc.data_ptr()
             for k, v in list(kw.items()) + list(keep.items()):
@@ -86,6 +86,8 @@ def main():
             ms = timeit(lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()))
             print(f"{name:52s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s", flush=True)
 
+        run8("[glds fp8] fwd, no epilogue work", L.EPI_FWD, stats=False, pool=False, es=gsign)
+        run8("[glds fp8] fwd + stats", L.EPI_FWD, pool=False, es=gsign)
         for _ in range(2):
             run8("[glds fp8] fwd + stats + pool", L.EPI_FWD, es=gsign)
             run8("[glds fp8] dgrad: mask + store + bias + S1", L.EPI_DGRAD, C=C, Yp=A8, bias=c)
