@@ -166,6 +166,9 @@ int pcs_gemm_big_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_p
 constexpr int PCS_BIG_BM = 256;
 // LDS-DMA 256x256 kernel for the RAW-operand global_feat GEMMs (gemm_glds.hip)
 bool pcs_gemm_glds_applicable(const pcs_gemm_args &a);
+// gemm_wres.hip: W-resident LDS-DMA stream for conv5's BN+ReLU pass with an fp8 store (K = 128)
+bool pcs_gemm_wres_applicable(const pcs_gemm_args &a);
+int pcs_gemm_wres_launch(const pcs_gemm_args &g, int64_t rows_per_chunk, hipStream_t s);
 int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                          hipStream_t s);
 // wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)

@@ -591,7 +591,8 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (a.epilogue == PCS_EPI_BNRELU && (!a.es || !a.et || !a.C || a.pool))
     return pcs_set_einval("pcs_gemm", "EPI_BNRELU needs es, et and C (no pool)");
   // EPI_BNRELU statistics = per-chunk column sums of the stored output (bf16 256-wide kernel)
-  if (a.epilogue == PCS_EPI_BNRELU && a.stats && !(wide_class(a) && pcs_gemm_big_applicable(a)))
+  if (a.epilogue == PCS_EPI_BNRELU && a.stats &&
+      !(wide_class(a) && (pcs_gemm_wres_applicable(a) || pcs_gemm_big_applicable(a))))
     return pcs_set_einval("pcs_gemm", "EPI_BNRELU column sums need the bf16 256-wide kernel (Ncols % 256 == 0)");
   if (a.pool && a.epilogue != PCS_EPI_FWD) return pcs_set_einval("pcs_gemm", "pool needs EPI_FWD");
   if (a.pool_w && (a.epilogue != PCS_EPI_DGRAD || a.prologue != PCS_PRO_RAW || !a.pool_idx || !a.pool_coef ||
@@ -605,13 +606,14 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
     return pcs_set_einval("pcs_gemm", "fp8 operands (PCS_FLAG_AW_FP8) need the LDS-DMA kernel: bf16 C, RAW prologue, "
                                       "K % 256 == 0, Ncols % 256 == 0, w_scale, FWD (no C) or folded DGRAD");
   if ((a.flags & PCS_FLAG_C_FP8) && !(a.epilogue == PCS_EPI_BNRELU && a.prologue == PCS_PRO_BNRELU && !a.a_mask &&
-                                      wide_class(a) && pcs_gemm_big_applicable(a)))
+                                      wide_class(a) && (pcs_gemm_wres_applicable(a) || pcs_gemm_big_applicable(a))))
     return pcs_set_einval("pcs_gemm", "fp8 output (PCS_FLAG_C_FP8) needs PRO_BNRELU (no dropout) + EPI_BNRELU on the bf16 256-wide kernel");
   if (a.a_mask && a.prologue != PCS_PRO_BNRELU)
     return pcs_set_einval("pcs_gemm", "a_mask applies to the BNRELU prologue only");
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (wide_class(a) && pcs_gemm_wres_applicable(a)) return pcs_gemm_wres_launch(a, rpc, s);
   if (wide_class(a) && pcs_gemm_glds_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_glds_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
