@@ -148,6 +148,8 @@ class Saved:
     wc: dict = None                               # cast weights used by this pass
     gram4: tuple = None                           # (G, S) of a4 when the forward computed it
     a5_colsum: torch.Tensor = None                # bf16: per-chunk column sums of a5 (conv5 epilogue)
+    mask_bufs: tuple = None                       # dropout keep bits drawn on the side stream
+    mask_ready: object = None                     # torch.cuda.Event recorded after them
 
 
 class Engine:
@@ -168,6 +170,7 @@ class Engine:
         self.offsets, self.total_params = flat_offsets(num_classes, input_dim)   # flat order
         self.buckets = bucket_ranges(num_classes, input_dim)
         self._geo = {}
+        self._side = {}   # device -> side stream
         self.flags = 0       # L.FLAG_GENERIC forces the generic GEMM (cross-checks)
         self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
         L.load()
@@ -187,6 +190,13 @@ class Engine:
     # ------------------------------------------------------------------ helpers
     def _stream(self):
         return L.stream_ptr()
+
+    def _side_stream(self, dev):
+        """A per-device HIP stream for work with no data dependence on the trunk (dropout bits)."""
+        st = self._side.get(dev)
+        if st is None:
+            st = self._side.setdefault(dev, torch.cuda.Stream(device=dev))
+        return st
 
     def geometry(self, B, N, K, ncols, pro=L.PRO_BNRELU, epi=L.EPI_FWD):
         """(chunks_per_scene, rows_per_chunk) of the kernel pcs_gemm picks for these args."""
@@ -333,6 +343,23 @@ class Engine:
         sv = Saved(B=B, N=N, train=train) if saved is None else saved
         sv.B, sv.N, sv.train, sv.x = B, N, train, x
         sv.gram4 = None   # (a reused Saved must not carry the previous pass's Gram)
+        if train and masks is None:
+            # Philox keep bits (ALU-bound, no data dependence) drawn on a side stream while the
+            # trunk's kernels run; the stream waits for everything enqueued before (the buffers
+            # may reuse memory the previous kernels still read) and seg_conv2 waits for it
+            m1 = torch.empty(M, 64, dtype=torch.uint8, device=dev)
+            m2 = torch.empty(M, 32, dtype=torch.uint8, device=dev)
+            side = self._side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                ss = L.stream_ptr()
+                L.call("pcs_dropout_bits", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), ss)
+                L.call("pcs_dropout_bits", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), ss)
+                sv.mask_ready = torch.cuda.Event()
+                sv.mask_ready.record(side)
+            m1.record_stream(side)
+            m2.record_stream(side)
+            sv.mask_bufs = (m1, m2)
         sv.wc = wc = self.cast_weights(P)
         T = self.tdt
 
@@ -448,10 +475,8 @@ class Engine:
                                      f"{tuple(m1.shape)} {m1.dtype} and {tuple(m2.shape)} {m2.dtype}")
                 m1, m2 = m1.contiguous(), m2.contiguous()
             else:
-                m1 = torch.empty(M, 64, dtype=torch.uint8, device=dev)
-                m2 = torch.empty(M, 32, dtype=torch.uint8, device=dev)
-                L.call("pcs_dropout_bits", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), s)
-                L.call("pcs_dropout_bits", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), s)
+                m1, m2 = sv.mask_bufs
+                torch.cuda.current_stream(dev).wait_event(sv.mask_ready)   # drawn on the side stream
             sv.masks = (m1, m2)
             keep = 1.0 / (1.0 - DROPOUT_P)
         else:
