@@ -262,8 +262,12 @@ def main():
     for i in range(args.warmup):
         loss = run_step()
     torch.cuda.synchronize()
+    # inside the timed region only the dominant-kernel candidates (the global_feat GEMMs and
+    # Gram) are bracketed by HIP events, so the measurement barely perturbs the step; the full
+    # per-kernel breakdown comes from two extra steps after it
     timing = {} if not args.no_kernel_timing else None
     step.timing = timing
+    step.timing_tags = set(TAG_KERNEL)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -275,6 +279,13 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     step.timing = None
+    breakdown = {}
+    if timing is not None:
+        step.timing, step.timing_tags = breakdown, None
+        for i in range(2):
+            run_step()
+        torch.cuda.synchronize()
+        step.timing = None
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -288,11 +299,14 @@ def main():
         real_points = int(t.item())
     total_points = real_points * args.steps
     roof = None
-    kernels = {}
+    kernels, full = {}, {}
     if timing:
         for tag, evs in timing.items():
             ms = [a.elapsed_time(b) for a, b in evs]
             kernels[tag] = (sum(ms), len(ms))
+        for tag, evs in breakdown.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            full[tag] = (sum(ms), len(ms))
         dom = max(kernels, key=lambda k: kernels[k][0])
         tot, cnt = kernels[dom]
         avg_s = tot / cnt / 1e3
@@ -320,8 +334,9 @@ def main():
                         "algorithmic_bytes": nbytes, "avg_ms": round(avg_s * 1e3, 4)}
         if rank == 0:
             step_ms = el / args.steps * 1e3
-            print(f"# per-kernel (avg ms, share of {step_ms:.2f} ms step):", file=sys.stderr)
-            for tag, (tot, cnt) in sorted(kernels.items(), key=lambda kv: -kv[1][0]):
+            print(f"# per-kernel (avg ms over 2 steps after the timed region, share of the {step_ms:.2f} ms "
+                  f"step):", file=sys.stderr)
+            for tag, (tot, cnt) in sorted(full.items(), key=lambda kv: -kv[1][0]):
                 mdl = kernel_model(tag, M, args.dtype)
                 extra = ""
                 if mdl:
@@ -360,7 +375,7 @@ def main():
             "loss": round(loss_v, 6),
             "roofline": roof,
             "step_roofline": step_roofline(M, C, args.dtype, el / args.steps * 1e3),
-            "northstar_64x64": northstar_64(kernels, M, args.dtype) if kernels else None,
+            "northstar_64x64": northstar_64(full, M, args.dtype) if kernels else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec))

@@ -173,11 +173,12 @@ class Engine:
         self._side = {}   # device -> side stream
         self.flags = 0       # L.FLAG_GENERIC forces the generic GEMM (cross-checks)
         self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
+        self.timing_tags = None   # set of tags to bracket (None = every tagged launch)
         L.load()
 
     def _launch(self, tag, name, *args):
         """C-ABI call, bracketed by HIP events on the launch stream when timing is on."""
-        if self.timing is None or tag is None:
+        if self.timing is None or tag is None or (self.timing_tags is not None and tag not in self.timing_tags):
             return L.call(name, *args)
         st = torch.cuda.Event(enable_timing=True)
         en = torch.cuda.Event(enable_timing=True)

@@ -83,6 +83,7 @@ class FusedTrainStep:
         self.counts = torch.empty(max(16, C), dtype=torch.int64, device=dev)
         self.inv_wsum = torch.empty(1, dtype=torch.float32, device=dev)
         self.timing = None   # optional dict tag -> list of (start, end) events
+        self.timing_tags = None   # optional set: only these tags are bracketed (None = all)
 
     def _distributed(self):
         if not (dist.is_available() and dist.is_initialized()):
@@ -93,6 +94,7 @@ class FusedTrainStep:
         model = self.model
         eng = model._engine()
         eng.timing = self.timing
+        eng.timing_tags = self.timing_tags
         model.train()
         P = model._param_dict()
         bufs = model._buffer_dict()
