@@ -417,6 +417,22 @@ int pcs_bn_stats_from_gram(const float *G, const float *S, int64_t count, const 
                            pcs_stream_t stream);
 
 /*
+ * As pcs_bn_stats_from_gram from per-scene column sums Sb [num_scenes, Cin] (each scene
+ * scene_rows rows): exact per-scene means (pcs_bn_fwd_finalize's scene sums), per-scene M2
+ * partials whose merge is the total M2.  bn_global's statistics on the bf16 / fp8 path
+ * (P:113): the Gram of the stored a5 (global_feat's weight gradient needs it anyway) and the
+ * per-chunk column sums of conv5's BN+ReLU epilogue replace the LDS-DMA forward's statistics
+ * epilogue.  Requires C == Cin (G is read k-major, as its own transpose), both multiples of
+ * 64, 1 <= num_scenes <= 64; the workspace (fp64 per-tile partials of w G w^T) is
+ * pcs_bn_stats_from_gram_scenes_workspace(C, Cin) bytes.  Two launches: an fp64 64x64-tiled
+ * G W^T contracted with W in its epilogue, then a per-channel fixed-order finalize.
+ */
+int64_t pcs_bn_stats_from_gram_scenes_workspace(int32_t C, int32_t Cin);
+int pcs_bn_stats_from_gram_scenes(const float *G, const float *Sb, int64_t scene_rows, const void *W, int32_t dtype,
+                                  int64_t ldw, int32_t C, int32_t Cin, int64_t num_scenes, void *workspace,
+                                  int64_t workspace_bytes, float *stats, pcs_stream_t stream);
+
+/*
  * S2 of a BN-fed layer's backward from R = dz^T a (pcs_wgrad with dy_mode RAW) instead of the
  * stored output: y = a W^T (bias-free, W [C, Cin] in dtype, row stride ldw), so
  *   S2[c] = sum_m dz[m,c] (y[m,c] - mean[c]) rstd[c] = rstd[c] (sum_k W[c,k] R[c,k] - mean[c] S1[c]).

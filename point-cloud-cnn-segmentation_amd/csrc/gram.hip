@@ -218,6 +218,96 @@ __global__ __launch_bounds__(256) void bn_stats_gram_kernel(const float *__restr
   }
 }
 
+// bn_global's statistics from G = a^T a (C x C, full) and per-scene column sums Sb [B, Cin]:
+// mean_b = Sb[b] w / N exactly, M2 = w (G - S S^T / M) w^T (S = sum_b Sb), and per-scene
+// M2_b chosen so that merging the B partials (Chan) gives M2:
+//   M2_b = (M2 - N sum_b (mean_b - mean)^2) / B   (clamped at 0)
+// Pass 1 (gram_quad_kernel): part[jt][c] = sum_{j in 64-tile jt} w_c[j] (G w_c^T)[j] as an
+// fp64 64x64-tiled product (G read k-major: it is symmetric); pass 2 adds the tiles in a
+// fixed order, subtracts (S w)^2 / M and forms the per-scene pairs.
+template <typename T>
+__global__ __launch_bounds__(256) void gram_quad_kernel(const float *__restrict__ G, const T *__restrict__ W,
+                                                        int64_t ldw, int Cin, double *__restrict__ part) {
+  __shared__ double gs[16][64];   // gs[k][j] = G[k0 + k][j0 + j] (= G[j][k])
+  __shared__ double wt[16][65];   // wt[k][c] = W[c0 + c][k0 + k]
+  __shared__ double red[16][64];
+  const int C = gridDim.x * 64, c0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  double acc[4][4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
+  for (int k0 = 0; k0 < Cin; k0 += 16) {
+#pragma unroll
+    for (int e = tid; e < 1024; e += 256) {
+      gs[e >> 6][e & 63] = (double)G[(int64_t)(k0 + (e >> 6)) * Cin + j0 + (e & 63)];
+      wt[e & 15][e >> 4] = (double)load_elem(W, (int64_t)(c0 + (e >> 4)) * ldw + k0 + (e & 15));
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) { a[p] = gs[kk][ty * 4 + p]; b[p] = wt[kk][tx * 4 + p]; }
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[p][q] = fma(a[p], b[q], acc[p][q]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t wr = (int64_t)(c0 + tx * 4 + q) * ldw + j0 + ty * 4;
+    double s = 0.0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) s = fma((double)load_elem(W, wr + p), acc[p][q], s);
+    red[ty][tx * 4 + q] = s;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    double s = 0.0;
+    for (int r = 0; r < 16; ++r) s += red[r][tid];
+    part[(int64_t)blockIdx.y * C + c0 + tid] = s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_scenes_kernel(const double *__restrict__ part, int njt,
+                                                              const float *__restrict__ Sb, double nb,
+                                                              const T *__restrict__ W, int64_t ldw, int C, int Cin,
+                                                              int B, float *__restrict__ stats) {
+  __shared__ double sh[256];
+  __shared__ double d[64];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  for (int b = 0; b < B; ++b) {
+    double x = 0.0;
+    for (int k = tid; k < Cin; k += 256)
+      x = fma((double)load_elem(W, (int64_t)c * ldw + k), (double)Sb[(int64_t)b * Cin + k], x);
+    sh[tid] = x;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if (tid < st) sh[tid] += sh[tid + st];
+      __syncthreads();
+    }
+    if (tid == 0) d[b] = sh[0];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double n = nb * B;
+    double q = 0.0, s = 0.0, between = 0.0;
+    for (int jt = 0; jt < njt; ++jt) q += part[(int64_t)jt * C + c];
+    for (int b = 0; b < B; ++b) s += d[b];
+    const double mean = s / n;
+    for (int b = 0; b < B; ++b) between += nb * (d[b] / nb - mean) * (d[b] / nb - mean);
+    double m2b = (q - s * s / n - between) / B;
+    m2b = m2b > 0.0 ? m2b : 0.0;
+    for (int b = 0; b < B; ++b)
+      *reinterpret_cast<float2 *>(stats + ((int64_t)b * C + c) * 2) = make_float2((float)(d[b] / nb), (float)m2b);
+  }
+}
+
 // S2 of a BN-fed layer from R = dz^T a: rstd (sum_k W[c,k] R[c,k] - mean S1), rewritten into
 // the per-chunk partials (chunk 0 = total, others 0).  One block per channel, fp64 sums.
 template <typename T>
@@ -312,6 +402,43 @@ extern "C" int pcs_bn_s2_from_r(float *stats, int64_t num_chunks, int32_t C, con
                        reinterpret_cast<const float *>(W), ldw, (int)Cin, mean, rstd);
   else
     return pcs_set_einval("pcs_bn_s2_from_r", "bad dtype");
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t pcs_bn_stats_from_gram_scenes_workspace(int32_t C, int32_t Cin) {
+  if (C <= 0 || Cin <= 0 || C % 64 || Cin % 64) return pcs_set_einval("pcs_bn_stats_from_gram_scenes_workspace", "C, Cin must be positive multiples of 64");
+  return (int64_t)(Cin / 64) * C * (int64_t)sizeof(double);
+}
+
+template <typename T>
+static void launch_stats_scenes(const float *G, const float *Sb, int64_t nb, const T *W, int64_t ldw, int C, int Cin,
+                                int B, double *part, float *stats, hipStream_t st) {
+  hipLaunchKernelGGL(gram_quad_kernel<T>, dim3(C / 64, Cin / 64), dim3(256), 0, st, G, W, ldw, Cin, part);
+  hipLaunchKernelGGL(bn_stats_scenes_kernel<T>, dim3(C), dim3(256), 0, st, part, Cin / 64, Sb, (double)nb, W, ldw,
+                     C, Cin, B, stats);
+}
+
+extern "C" int pcs_bn_stats_from_gram_scenes(const float *G, const float *Sb, int64_t scene_rows, const void *W,
+                                             int32_t dtype, int64_t ldw, int32_t C, int32_t Cin, int64_t num_scenes,
+                                             void *workspace, int64_t workspace_bytes, float *stats,
+                                             pcs_stream_t stream) {
+  if (!G || !Sb || !W || !stats || !workspace || scene_rows <= 0 || C <= 0 || Cin <= 0 || C % 64 || Cin % 64 ||
+      ldw < Cin || C != Cin || num_scenes <= 0 || num_scenes > 64)
+    return pcs_set_einval("pcs_bn_stats_from_gram_scenes",
+                          "bad arguments (C == Cin, multiples of 64; 1 <= num_scenes <= 64)");
+  if (workspace_bytes < (int64_t)(Cin / 64) * C * (int64_t)sizeof(double))
+    return pcs_set_einval("pcs_bn_stats_from_gram_scenes", "workspace too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double *part = static_cast<double *>(workspace);
+  if (dtype == PCS_BF16)
+    launch_stats_scenes<bf16_t>(G, Sb, scene_rows, reinterpret_cast<const bf16_t *>(W), ldw, C, Cin,
+                                (int)num_scenes, part, stats, st);
+  else if (dtype == PCS_F32)
+    launch_stats_scenes<float>(G, Sb, scene_rows, reinterpret_cast<const float *>(W), ldw, C, Cin, (int)num_scenes,
+                               part, stats, st);
+  else
+    return pcs_set_einval("pcs_bn_stats_from_gram_scenes", "bad dtype");
   PCS_CHECK_LAUNCH();
   return 0;
 }

@@ -149,6 +149,8 @@ class Saved:
     gram4: tuple = None                           # (G, S) of a4 when the forward computed it
     a5_colsum: torch.Tensor = None                # bf16: per-chunk column sums of a5 (conv5 epilogue)
     mask_bufs: tuple = None                       # dropout keep bits drawn on the side stream
+    gram5: tuple = None                           # bf16/fp8: (G, per-scene S, workspace) of a5, from the forward
+    wg_eff: torch.Tensor = None                   # global_feat's weight as the forward GEMM saw it (fp32)
     mask_ready: object = None                     # torch.cuda.Event recorded after them
 
 
@@ -433,20 +435,50 @@ class Engine:
                    extra_flags=L.FLAG_C_FP8 if self.fp8 else 0, **bnrelu("bn4"))
         sv.ys["a5"] = a5
 
-        # global_feat (P:113-114): a5 W^T with BN statistics and max-pool partials in the
-        # epilogue; the 1024-wide output itself is never stored
+        # global_feat (P:113-114): a5 W^T with max-pool partials (and, on the fp32 / generic
+        # paths, BN statistics) in the epilogue; the 1024-wide output itself is never stored.
+        # bf16 / fp8: bn_global's statistics come from the Gram of a5 -- computed here rather
+        # than in the backward, whose Gram-form weight gradient reuses it -- and conv5's
+        # per-chunk column sums (pcs_bn_stats_from_gram_scenes), so the LDS-DMA forward runs
+        # the max-pool epilogue only.
         cps_g, rpc_g = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD)
         pool = torch.empty(B * cps_g, 1024, 4, dtype=torch.float32, device=dev)
-        st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
+        sv.gram5 = None
+        if train and self._raw_gram():
+            Wg = P["global_feat.weight"]
+            sv.wg_eff = wc["global_feat_fp8"][2] if self.fp8 else self._rounded(Wg.reshape(1024, -1))
+            G5 = torch.empty(1024, 1024, dtype=torch.float32, device=dev)
+            nbytes = L.load().pcs_gram_raw_workspace(M, 1024)
+            if nbytes < 0:
+                raise L.PcsError(L.load().pcs_last_error().decode())
+            gws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            self._launch("wgrad:global_feat", "pcs_gram_raw", L.ptr(a5), M, 1024, self.a5_dt, L.ptr(gws), nbytes,
+                         L.ptr(G5), s)
+            # per-scene column sums of a5 from conv5's per-chunk partials (chunks are scene-aligned)
+            Sb2 = torch.empty(B, 1024, 2, dtype=torch.float32, device=dev)
+            for b in range(B):
+                L.call("pcs_reduce_partials", L.ptr(sv.a5_colsum[b * cps5c:]), cps5c, 2048, 1.0, L.ptr(Sb2[b]),
+                       2048, 2048, s)
+            Sb = Sb2[..., 0].contiguous()
+            st = torch.empty(B, 1024, 2, dtype=torch.float32, device=dev)
+            qbytes = L.load().pcs_bn_stats_from_gram_scenes_workspace(1024, 1024)
+            qws = torch.empty(qbytes // 8, dtype=torch.float64, device=dev)
+            self._launch("stats:global_feat", "pcs_bn_stats_from_gram_scenes", L.ptr(G5), L.ptr(Sb), N, L.ptr(sv.wg_eff), L.F32, 1024, 1024,
+                         1024, B, L.ptr(qws), qbytes, L.ptr(st), s)
+            sv.gram5 = (G5, Sb, gws)
+            st_g, cps_st, rpc_st = None, 1, N
+        else:
+            st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
+            st_g, cps_st, rpc_st = st, cps_g, rpc_g
         # (es = bn_global's gamma: its sign tells the pool which extremum pcs_pool_finalize uses)
         if self.fp8:
             Wq, wsc, _ = wc["global_feat_fp8"]
-            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wq, None, stats=st, pool=pool,
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wq, None, stats=st_g, pool=pool,
                        es=P["bn_global.weight"], w_scale=wsc, extra_flags=L.FLAG_AW_FP8, tag="fwd:global_feat")
         else:
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, wc["global_feat"][0], None,
-                       stats=st, pool=pool, es=P["bn_global.weight"], tag="fwd:global_feat")
-        sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_g, rpc_g, P, bufs,
+                       stats=st_g, pool=pool, es=P["bn_global.weight"], tag="fwd:global_feat")
+        sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_st, rpc_st, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]
         sv.g = torch.empty(B, 1024, dtype=torch.float32, device=dev)
@@ -692,7 +724,10 @@ class Engine:
         a5 = ys["a5"]
         Wg = P["global_feat.weight"]
         # the W the forward GEMM used (see pcs_round_weight; fp8: the dequantized e4m3 rows)
-        Wg_r = wc["global_feat_fp8"][2] if self.fp8 else self._rounded(Wg)
+        if sv.gram5 is not None:
+            Wg_r = sv.wg_eff
+        else:
+            Wg_r = wc["global_feat_fp8"][2] if self.fp8 else self._rounded(Wg)
         cvec = torch.empty(1024, dtype=torch.float32, device=dev)
         if self.fp8:
             # H in fp32, then e4m3 rows with one scale each (H is symmetric: row n = column n)
@@ -730,7 +765,12 @@ class Engine:
         ones = torch.ones(1024, dtype=torch.float32, device=dev)
         zeros = torch.zeros(1024, dtype=torch.float32, device=dev)
         gram = torch.empty(1024, 1024, dtype=torch.float32, device=dev)
-        if self._raw_gram() and sv.a5_colsum is not None:
+        if sv.gram5 is not None:
+            # computed in the forward (bn_global's statistics); S = sum of the per-scene sums
+            gram, Sb, ws = sv.gram5
+            colsum = torch.empty(1024, dtype=torch.float32, device=dev)
+            L.call("pcs_reduce_partials", L.ptr(Sb), B, 1024, 1.0, L.ptr(colsum), 1024, 1024, s)
+        elif self._raw_gram() and sv.a5_colsum is not None:
             # a5 is the activation itself: LDS-DMA Gram; S from conv5's per-chunk column sums
             nbytes = L.load().pcs_gram_raw_workspace(M, 1024)
             if nbytes < 0:

@@ -183,6 +183,45 @@ def test_bn_stats_from_gram(dtype):
     assert err_m < 1e-5 and err_v < 1e-4, (err_m, err_v)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_bn_stats_from_gram_scenes(dtype):
+    """bn_global statistics of y = a W^T (bf16 / fp8 path) from the Gram of a and per-scene
+    column sums: the partials finalise to the batch mean / biased variance and to exact
+    per-scene sums of y, with scenes of deliberately different means."""
+    import pcs_amd._lib as L
+    dt, tdt = (L.BF16, torch.bfloat16) if dtype == "bf16" else (L.F32, torch.float32)
+    g = torch.Generator().manual_seed(6)
+    B, N, C = 3, 1000, 256
+    shift_b = torch.tensor([0.0, 0.5, -0.2]).repeat_interleave(N)[:, None]
+    a = torch.relu(torch.randn(B * N, C, generator=g) + 0.3 + shift_b).to(tdt).to(DEV)
+    W = (torch.randn(C, C, generator=g) * 0.06).to(tdt).to(DEV)
+    ad = a.double()
+    G = (ad.T @ ad).float()
+    Sb = ad.reshape(B, N, C).sum(1).float().contiguous()
+    nbytes = L.load().pcs_bn_stats_from_gram_scenes_workspace(C, C)
+    assert nbytes == (C // 64) * C * 8
+    ws = torch.empty(nbytes // 8, dtype=torch.float64, device=DEV)
+    st = torch.empty(B, C, 2, device=DEV)
+    L.call("pcs_bn_stats_from_gram_scenes", L.ptr(G), L.ptr(Sb), N, L.ptr(W), dt, C, C, C, B, L.ptr(ws), nbytes,
+           L.ptr(st), L.stream_ptr())
+    mean, rstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
+    ssum = torch.empty(B, C, device=DEV)
+    ones, zeros = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    L.call("pcs_bn_fwd_finalize", L.ptr(st), B, N, C, 1, N, L.ptr(ones), L.ptr(zeros), None, None, None,
+           0.1, 1e-5, 0, L.ptr(mean), L.ptr(rstd), L.ptr(scale), L.ptr(shift), L.ptr(ssum), L.stream_ptr())
+    torch.cuda.synchronize()
+    y = ad @ W.double().T
+    sd = y.std(0).min()
+    err_m = float((mean.double() - y.mean(0)).abs().max() / sd)
+    var = 1.0 / rstd.double() ** 2 - 1e-5
+    err_v = float(((var - y.var(0, unbiased=False)) / y.var(0, unbiased=False)).abs().max())
+    err_s = float((ssum.double() - y.reshape(B, N, C).sum(1)).abs().max() / (N * sd))
+    assert err_m < 1e-5 and err_v < 1e-4 and err_s < 1e-5, (err_m, err_v, err_s)
+    with pytest.raises(L.PcsError):
+        L.call("pcs_bn_stats_from_gram_scenes", L.ptr(G), L.ptr(Sb), N, L.ptr(W), dt, C, C, C, B, L.ptr(ws),
+               nbytes - 8, L.ptr(st), L.stream_ptr())
+
+
 def test_bn_s2_from_r():
     """S2 = rstd (sum_k W R - mean S1), rewritten into the (S1, S2) partials (chunk 0 total)."""
     import pcs_amd._lib as L
