@@ -40,7 +40,11 @@ enum {
                            W rows carry E8M0 scales in w_scale, A is unscaled; the LDS-DMA
                            kernel runs v_mfma_scale_f32_16x16x128_f8f6f4 (K % 256 == 0; RAW
                            prologue; FWD statistics / pool or DGRAD)                         */
-  PCS_FLAG_C_FP8 = 8    /* EPI_BNRELU of the bf16 256-wide kernel stores C as fp8 e4m3      */
+  PCS_FLAG_C_FP8 = 8,   /* EPI_BNRELU of the bf16 256-wide kernel stores C as fp8 e4m3      */
+  PCS_FLAG_POOL_SIGNED_W = 16 /* FWD max-pool on the LDS-DMA kernel: the caller has multiplied
+                           W's rows (pcs_sign_rows) and bias by sign(es), so the pool keeps the
+                           plain column max of acc (no multiply); es still names the sign.
+                           Needs pool and es, no statistics (they would be of the signed y)  */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
@@ -334,6 +338,14 @@ int64_t pcs_gram_workspace(int64_t num_scenes, int64_t scene_rows, int32_t C, in
 int pcs_gram(const void *Y, const float *s, const float *t, int64_t num_scenes, int64_t scene_rows,
              int32_t C, int32_t dtype, int32_t splits_per_scene, float *workspace, float *G,
              float *colsum, pcs_stream_t stream);
+
+/*
+ * out[r, :] = W[r, :] with its sign flipped where sign_of[r] < 0 (exact: the sign bit), rows x
+ * cols contiguous, dtype F32, BF16 or FP8 (e4m3 bytes; an E8M0 row scale is unchanged).  The
+ * forward global_feat weight for PCS_FLAG_POOL_SIGNED_W (sign_of = bn_global's gamma, P:113).
+ */
+int pcs_sign_rows(const void *W, int32_t dtype, int64_t rows, int64_t cols, const float *sign_of, void *out,
+                  pcs_stream_t stream);
 
 /*
  * fp8 e4m3 (OCP) rows with one E8M0 scale per row, for the fp8 wide layer (MX-scaled MFMA

@@ -45,6 +45,7 @@ FLAG_GENERIC = 1
 FLAG_NO_GLDS = 2
 FLAG_AW_FP8 = 4
 FLAG_C_FP8 = 8
+FLAG_POOL_SIGNED_W = 16
 
 
 class WgradArgs(ct.Structure):
@@ -129,6 +130,7 @@ SIGNATURES = [
     ("pcs_bn_s2_from_r", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
     ("pcs_bn_stats_from_gram", ct.c_int, [_vp, _vp, _i64, _vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp]),
     ("pcs_bn_stats_from_gram_scenes_workspace", _i64, [_i32, _i32]),
+    ("pcs_sign_rows", ct.c_int, [_vp, _i32, _i64, _i64, _vp, _vp, _vp]),
     ("pcs_bn_stats_from_gram_scenes", ct.c_int, [_vp, _vp, _i64, _vp, _i32, _i64, _i32, _i32, _i64, _vp, _i64, _vp,
                                                  _vp]),
     ("pcs_confusion", ct.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),

@@ -2,7 +2,9 @@
 // 8-phase software pipeline, for the two 1024-deep GEMMs of global_feat, whose operand is
 // the materialised a5 = relu(bn5(y5)) (no prologue transform, so the operand goes
 // HBM -> LDS without passing through registers):
-//   forward   y_g = a5 Wg^T            epilogue: BN statistics + max-pool partials (P:113-114)
+//   forward   y_g = a5 Wg^T            epilogue: max-pool partials (P:113-114), optionally BN
+//             statistics (the bf16 / fp8 training path takes them from the Gram of a5 instead
+//             and passes W's rows pre-multiplied by sign(gamma_g), PCS_FLAG_POOL_SIGNED_W)
 //   backward  dA5 = a5 H + c  with H = Wg^T diag(gamma_g) Wg, c = Wg^T beta_g (pcs_bn_fold),
 //             the ReLU mask of bn5 read from the operand itself, S1 = sum dz per column
 //             (autograd of P:110-114, P:254); the max-pool rows' sparse term is added after
@@ -102,6 +104,18 @@ PCS_DEV float row_min(float v) {
   v = fminf(v, dppf<0xB1>(v)); v = fminf(v, dppf<0x4E>(v)); v = fminf(v, dppf<0x141>(v));
   return fminf(v, dppf<0x140>(v));
 }
+// v_max3_f32 / v_max_f32 as single instructions: on MFMA results hipcc otherwise inserts a
+// canonicalising v_max before each fmaxf (MI355X_MICROARCH 'Per-instruction cycle constants')
+PCS_DEV float max3f(float a, float b, float c) {
+  float r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+PCS_DEV float max2f(float a, float b) {
+  float r;
+  asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 PCS_DEV int row_mini(int v) {
   v = min(v, dppi<0xB1>(v)); v = min(v, dppi<0x4E>(v)); v = min(v, dppi<0x141>(v));
   return min(v, dppi<0x140>(v));
@@ -162,6 +176,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first glds)
   const bool do_stats = a.stats != nullptr;
   const bool do_pool = MODE == MODE_FWD && a.pool != nullptr;
+  const bool signed_w = (a.flags & PCS_FLAG_POOL_SIGNED_W) != 0;   // acc is already sgn * y
   if (tid < BN) {
     lbias[tid] = a.bias ? a.bias[n0 + tid] : 0.f;
 #pragma unroll
@@ -473,21 +488,41 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
           const float *cur4 = lcur + wm * BN + wn * 64 + 4 * lg;
           const float *sgn4 = lsgn + wn * 64 + 4 * lg;
           uint32_t beat = 0;   // bit j: this lane beats a running max in tile column block j
+          if (signed_w && tile_full) {
+            // PCS_FLAG_POOL_SIGNED_W: acc = sgn * y, 4 max3/max per column and a compare
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float4 c4 = *reinterpret_cast<const float4 *>(cur4 + j * 16);
-            const float4 g4 = *reinterpret_cast<const float4 *>(sgn4 + j * 16);
-            const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
-            bool bj = false;
+            for (int j = 0; j < 4; ++j) {
+              const float4 c4 = *reinterpret_cast<const float4 *>(cur4 + j * 16);
+              const float cc[4] = {c4.x, c4.y, c4.z, c4.w};
+              bool bj = false;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float mx = -__builtin_huge_valf();
-#pragma unroll
-              for (int i = 0; i < 8; ++i)
-                if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, gg[r] * acc[i][j][r]);
-              bj |= mx > cc[r];
+              for (int r = 0; r < 4; ++r) {
+                const float t0 = max3f(acc[0][j][r], acc[1][j][r], acc[2][j][r]);
+                const float t1 = max3f(acc[3][j][r], acc[4][j][r], acc[5][j][r]);
+                const float t2 = max3f(acc[6][j][r], acc[7][j][r], t0);
+                bj |= max2f(t1, t2) > cc[r];
+              }
+              beat |= (uint32_t)bj << j;
             }
-            beat |= (uint32_t)bj << j;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float4 c4 = *reinterpret_cast<const float4 *>(cur4 + j * 16);
+              const float4 g4 = *reinterpret_cast<const float4 *>(sgn4 + j * 16);
+              const float cc[4] = {c4.x, c4.y, c4.z, c4.w};
+              const float gg[4] = {signed_w ? 1.f : g4.x, signed_w ? 1.f : g4.y, signed_w ? 1.f : g4.z,
+                                   signed_w ? 1.f : g4.w};
+              bool bj = false;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float mx = -__builtin_huge_valf();
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                  if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, gg[r] * acc[i][j][r]);
+                bj |= mx > cc[r];
+              }
+              beat |= (uint32_t)bj << j;
+            }
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -499,7 +534,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
             float mine = -__builtin_huge_valf();
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              sg[r] = sgn4[j * 16 + r];
+              sg[r] = signed_w ? 1.f : sgn4[j * 16 + r];
               float mx = -__builtin_huge_valf();
 #pragma unroll
               for (int i = 0; i < 8; ++i)
@@ -588,7 +623,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       if (do_stats) run[cme].x += S1;
       // The stores count in vmcnt but are not waited for here: the next counted wait
       // (vmcnt(10), phase 1) only relies on the LOADS completing in order among themselves
-      // (pending stores can only make it wait longer), so they drain behind phase 1's reads.
+      // (pending stores make it wait longer).  Counting the 16 stores in the next four waits
+      // instead (so the loads need not wait for them) measured 0.15-0.25 ms SLOWER per call.
     }
 
     bias_init(acc);
@@ -632,7 +668,9 @@ bool pcs_gemm_glds_applicable(const pcs_gemm_args &a) {
   if (a.prologue != PCS_PRO_RAW || a.K % (fp8 ? 256 : 2 * BK) != 0 || a.Ncols % BN != 0) return false;
   // forward: statistics / max-pool only (nothing stored); the pool keeps one extremum per
   // column, chosen by sign(es), so a pool needs es
-  if (a.epilogue == PCS_EPI_FWD) return a.C == nullptr && a.scene_bias == nullptr && (!a.pool || a.es);
+  if (a.epilogue == PCS_EPI_FWD)
+    return a.C == nullptr && a.scene_bias == nullptr && (!a.pool || a.es) &&
+           (!(a.flags & PCS_FLAG_POOL_SIGNED_W) || (a.pool && !a.stats));
   if (a.epilogue == PCS_EPI_DGRAD)   // mask read from the operand itself, no S2, no addend
     return a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask &&
            !a.pool_w;
@@ -785,6 +823,42 @@ extern "C" int pcs_quant_fp8_rows(const float *W, int64_t rows, int64_t cols, in
   if (!W || !Wq || !scale || rows <= 0 || cols <= 0 || ldw < cols) return pcs_set_einval("pcs_quant_fp8_rows", "bad arguments");
   hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((unsigned)rows), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), W,
                      cols, ldw, Wq, scale, deq);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// pcs_sign_rows: W's rows with the sign bit flipped where sign_of[r] < 0 (PCS_FLAG_POOL_SIGNED_W)
+// ---------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void sign_rows_kernel(const T *__restrict__ W, int64_t cols,
+                                                        const float *__restrict__ sign_of, T *__restrict__ out) {
+  const int64_t r = blockIdx.y;
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= cols) return;
+  constexpr uint32_t SB = 1u << (8 * sizeof(T) - 1);
+  out[r * cols + k] = sign_of[r] < 0.f ? (T)(W[r * cols + k] ^ SB) : W[r * cols + k];
+}
+}  // namespace
+
+extern "C" int pcs_sign_rows(const void *W, int32_t dtype, int64_t rows, int64_t cols, const float *sign_of, void *out,
+                             pcs_stream_t stream) {
+  if (!W || !sign_of || !out || rows <= 0 || rows > 65535 || cols <= 0)
+    return pcs_set_einval("pcs_sign_rows", "bad arguments (0 < rows <= 65535)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)rows);
+  if (dtype == PCS_F32)
+    hipLaunchKernelGGL(sign_rows_kernel<uint32_t>, grid, dim3(256), 0, s, static_cast<const uint32_t *>(W), cols,
+                       sign_of, static_cast<uint32_t *>(out));
+  else if (dtype == PCS_BF16)
+    hipLaunchKernelGGL(sign_rows_kernel<uint16_t>, grid, dim3(256), 0, s, static_cast<const uint16_t *>(W), cols,
+                       sign_of, static_cast<uint16_t *>(out));
+  else if (dtype == PCS_FP8)
+    hipLaunchKernelGGL(sign_rows_kernel<uint8_t>, grid, dim3(256), 0, s, static_cast<const uint8_t *>(W), cols,
+                       sign_of, static_cast<uint8_t *>(out));
+  else
+    return pcs_set_einval("pcs_sign_rows", "bad dtype");
   PCS_CHECK_LAUNCH();
   return 0;
 }

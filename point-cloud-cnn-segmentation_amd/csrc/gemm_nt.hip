@@ -608,6 +608,10 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if ((a.flags & PCS_FLAG_C_FP8) && !(a.epilogue == PCS_EPI_BNRELU && a.prologue == PCS_PRO_BNRELU && !a.a_mask &&
                                       wide_class(a) && (pcs_gemm_wres_applicable(a) || pcs_gemm_big_applicable(a))))
     return pcs_set_einval("pcs_gemm", "fp8 output (PCS_FLAG_C_FP8) needs PRO_BNRELU (no dropout) + EPI_BNRELU on the bf16 256-wide kernel");
+  if ((a.flags & PCS_FLAG_POOL_SIGNED_W) && !(a.epilogue == PCS_EPI_FWD && a.pool && a.es && !a.stats &&
+                                             wide_class(a) && pcs_gemm_glds_applicable(a)))
+    return pcs_set_einval("pcs_gemm", "PCS_FLAG_POOL_SIGNED_W needs EPI_FWD with pool and es, no statistics, on the "
+                                      "LDS-DMA kernel");
   if (a.a_mask && a.prologue != PCS_PRO_BNRELU)
     return pcs_set_einval("pcs_gemm", "a_mask applies to the BNRELU prologue only");
   const int64_t rpc = pcs_gemm_geometry(&a);

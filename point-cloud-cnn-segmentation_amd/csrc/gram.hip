@@ -222,9 +222,13 @@ __global__ __launch_bounds__(256) void bn_stats_gram_kernel(const float *__restr
 // mean_b = Sb[b] w / N exactly, M2 = w (G - S S^T / M) w^T (S = sum_b Sb), and per-scene
 // M2_b chosen so that merging the B partials (Chan) gives M2:
 //   M2_b = (M2 - N sum_b (mean_b - mean)^2) / B   (clamped at 0)
-// Pass 1 (gram_quad_kernel): part[jt][c] = sum_{j in 64-tile jt} w_c[j] (G w_c^T)[j] as an
-// fp64 64x64-tiled product (G read k-major: it is symmetric); pass 2 adds the tiles in a
-// fixed order, subtracts (S w)^2 / M and forms the per-scene pairs.
+// Pass 1 (gram_quad_kernel): part[kz][jt][c] = sum_{j in 64-tile jt} w_c[j] (G_{:, kz} w_c^T)[j]
+// as an fp64 64x64-tiled product over one of QK_SPLIT k-ranges (G read k-major: it is
+// symmetric; the split gives 1024 workgroups at C = 1024 instead of 256 one-wave-per-SIMD
+// ones); pass 2 adds the partials in a fixed order, subtracts (S w)^2 / M and forms the
+// per-scene pairs.
+constexpr int QK_SPLIT = 4;
+
 template <typename T>
 __global__ __launch_bounds__(256) void gram_quad_kernel(const float *__restrict__ G, const T *__restrict__ W,
                                                         int64_t ldw, int Cin, double *__restrict__ part) {
@@ -238,7 +242,9 @@ __global__ __launch_bounds__(256) void gram_quad_kernel(const float *__restrict_
   for (int p = 0; p < 4; ++p)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
-  for (int k0 = 0; k0 < Cin; k0 += 16) {
+  const int kz0 = (int)((int64_t)Cin / 16 * blockIdx.z / QK_SPLIT) * 16;
+  const int kz1 = (int)((int64_t)Cin / 16 * (blockIdx.z + 1) / QK_SPLIT) * 16;
+  for (int k0 = kz0; k0 < kz1; k0 += 16) {
 #pragma unroll
     for (int e = tid; e < 1024; e += 256) {
       gs[e >> 6][e & 63] = (double)G[(int64_t)(k0 + (e >> 6)) * Cin + j0 + (e & 63)];
@@ -269,7 +275,7 @@ __global__ __launch_bounds__(256) void gram_quad_kernel(const float *__restrict_
   if (tid < 64) {
     double s = 0.0;
     for (int r = 0; r < 16; ++r) s += red[r][tid];
-    part[(int64_t)blockIdx.y * C + c0 + tid] = s;
+    part[((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * C + c0 + tid] = s;
   }
 }
 
@@ -294,10 +300,17 @@ __global__ __launch_bounds__(256) void bn_stats_scenes_kernel(const double *__re
     if (tid == 0) d[b] = sh[0];
     __syncthreads();
   }
+  double qp = 0.0;   // the partials: strided per thread, then a fixed-order tree
+  for (int jt = tid; jt < njt; jt += 256) qp += part[(int64_t)jt * C + c];
+  sh[tid] = qp;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) sh[tid] += sh[tid + st];
+    __syncthreads();
+  }
   if (tid == 0) {
     const double n = nb * B;
-    double q = 0.0, s = 0.0, between = 0.0;
-    for (int jt = 0; jt < njt; ++jt) q += part[(int64_t)jt * C + c];
+    double q = sh[0], s = 0.0, between = 0.0;
     for (int b = 0; b < B; ++b) s += d[b];
     const double mean = s / n;
     for (int b = 0; b < B; ++b) between += nb * (d[b] / nb - mean) * (d[b] / nb - mean);
@@ -408,14 +421,15 @@ extern "C" int pcs_bn_s2_from_r(float *stats, int64_t num_chunks, int32_t C, con
 
 extern "C" int64_t pcs_bn_stats_from_gram_scenes_workspace(int32_t C, int32_t Cin) {
   if (C <= 0 || Cin <= 0 || C % 64 || Cin % 64) return pcs_set_einval("pcs_bn_stats_from_gram_scenes_workspace", "C, Cin must be positive multiples of 64");
-  return (int64_t)(Cin / 64) * C * (int64_t)sizeof(double);
+  return (int64_t)QK_SPLIT * (Cin / 64) * C * (int64_t)sizeof(double);
 }
 
 template <typename T>
 static void launch_stats_scenes(const float *G, const float *Sb, int64_t nb, const T *W, int64_t ldw, int C, int Cin,
                                 int B, double *part, float *stats, hipStream_t st) {
-  hipLaunchKernelGGL(gram_quad_kernel<T>, dim3(C / 64, Cin / 64), dim3(256), 0, st, G, W, ldw, Cin, part);
-  hipLaunchKernelGGL(bn_stats_scenes_kernel<T>, dim3(C), dim3(256), 0, st, part, Cin / 64, Sb, (double)nb, W, ldw,
+  hipLaunchKernelGGL(gram_quad_kernel<T>, dim3(C / 64, Cin / 64, QK_SPLIT), dim3(256), 0, st, G, W, ldw, Cin, part);
+  hipLaunchKernelGGL(bn_stats_scenes_kernel<T>, dim3(C), dim3(256), 0, st, part, QK_SPLIT * (Cin / 64), Sb,
+                     (double)nb, W, ldw,
                      C, Cin, B, stats);
 }
 
@@ -427,7 +441,7 @@ extern "C" int pcs_bn_stats_from_gram_scenes(const float *G, const float *Sb, in
       ldw < Cin || C != Cin || num_scenes <= 0 || num_scenes > 64)
     return pcs_set_einval("pcs_bn_stats_from_gram_scenes",
                           "bad arguments (C == Cin, multiples of 64; 1 <= num_scenes <= 64)");
-  if (workspace_bytes < (int64_t)(Cin / 64) * C * (int64_t)sizeof(double))
+  if (workspace_bytes < (int64_t)QK_SPLIT * (Cin / 64) * C * (int64_t)sizeof(double))
     return pcs_set_einval("pcs_bn_stats_from_gram_scenes", "workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double *part = static_cast<double *>(workspace);

@@ -470,14 +470,23 @@ class Engine:
         else:
             st = torch.empty(B * cps_g, 1024, 2, dtype=torch.float32, device=dev) if train else None
             st_g, cps_st, rpc_st = st, cps_g, rpc_g
-        # (es = bn_global's gamma: its sign tells the pool which extremum pcs_pool_finalize uses)
+        # (es = bn_global's gamma: its sign tells the pool which extremum pcs_pool_finalize uses;
+        # without statistics on the LDS-DMA kernel, W's rows come pre-multiplied by that sign,
+        # PCS_FLAG_POOL_SIGNED_W, and the pool keeps a plain column max)
+        gamma_g = P["bn_global.weight"]
+        Wf = wc["global_feat_fp8"][0] if self.fp8 else wc["global_feat"][0]
+        sflag = 0
+        if st_g is None and self._raw_gram() and not (self.flags & L.FLAG_NO_GLDS):
+            Wsg = torch.empty_like(Wf)
+            L.call("pcs_sign_rows", L.ptr(Wf), L.FP8 if self.fp8 else self.dt, 1024, 1024, L.ptr(gamma_g),
+                   L.ptr(Wsg), s)
+            Wf, sflag = Wsg, L.FLAG_POOL_SIGNED_W
         if self.fp8:
-            Wq, wsc, _ = wc["global_feat_fp8"]
-            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wq, None, stats=st_g, pool=pool,
-                       es=P["bn_global.weight"], w_scale=wsc, extra_flags=L.FLAG_AW_FP8, tag="fwd:global_feat")
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wf, None, stats=st_g, pool=pool, es=gamma_g,
+                       w_scale=wc["global_feat_fp8"][1], extra_flags=L.FLAG_AW_FP8 | sflag, tag="fwd:global_feat")
         else:
-            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, wc["global_feat"][0], None,
-                       stats=st_g, pool=pool, es=P["bn_global.weight"], tag="fwd:global_feat")
+            self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wf, None, stats=st_g, pool=pool, es=gamma_g,
+                       extra_flags=sflag, tag="fwd:global_feat")
         sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_st, rpc_st, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]

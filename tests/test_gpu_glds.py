@@ -84,6 +84,60 @@ def test_forward_stats_and_pool(variant, B, N, cps):
     assert float((at - ext).abs().max()) < ptol * scl
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("B,N,cps", [(2, 256 * 7 + 77, 2), (3, 256 * 3, 1)])
+def test_forward_pool_signed_w(fp8, B, N, cps):
+    """PCS_FLAG_POOL_SIGNED_W: with W's rows multiplied by sign(gamma) (pcs_sign_rows, exact)
+    the LDS-DMA forward's max-pool partials match the unsigned kernel's (which multiplies by
+    the sign in its epilogue); a signed W with statistics is refused."""
+    import pcs_amd._lib as L
+    K = Nc = 512
+    g = torch.Generator().manual_seed(31 + N)
+    A = torch.relu(torch.randn(B * N, K, generator=g))
+    W = torch.randn(Nc, K, generator=g) * 0.05
+    gamma = torch.randn(Nc, generator=g).to(DEV)
+    flags, extra = 0, {}
+    if fp8:
+        A = A.clamp(max=448.0).to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
+        Wq = torch.empty(Nc, K, dtype=torch.uint8, device=DEV)
+        wsc = torch.empty(Nc, dtype=torch.uint8, device=DEV)
+        L.call("pcs_quant_fp8_rows", L.ptr(W.to(DEV)), Nc, K, K, L.ptr(Wq), L.ptr(wsc), None, L.stream_ptr())
+        W, wdt, flags, extra = Wq, L.FP8, L.FLAG_AW_FP8, {"w_scale": wsc}
+    else:
+        A, W, wdt = A.to(torch.bfloat16).to(DEV), W.to(torch.bfloat16).to(DEV), L.BF16
+    Ws = torch.empty_like(W)
+    L.call("pcs_sign_rows", L.ptr(W), wdt, Nc, K, L.ptr(gamma), L.ptr(Ws), L.stream_ptr())
+    flip = 0x80 if fp8 else -0x8000                      # the sign bit of a byte / an int16
+    Wi = W.view(torch.uint8) if fp8 else W.view(torch.int16)
+    Wsi = Ws.view(torch.uint8) if fp8 else Ws.view(torch.int16)
+    ref = torch.where((gamma < 0)[:, None], Wi ^ flip, Wi)
+    assert torch.equal(Wsi, ref)
+    pools = []
+    for w, fl in ((W, flags), (Ws, flags | L.FLAG_POOL_SIGNED_W)):
+        a, _ = _args(L, B, N, K, Nc, L.BF16, L.PRO_RAW, L.EPI_FWD, fl, cps)
+        pool = torch.full((B * a.chunks_per_scene, Nc, 4), float("nan"), device=DEV)
+        a.A, a.W, a.C, a.pool, a.es = A.data_ptr(), w.data_ptr(), None, pool.data_ptr(), gamma.data_ptr()
+        for k, v in extra.items():
+            setattr(a, k, v.data_ptr())
+        L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+        pools.append(pool)
+    torch.cuda.synchronize()
+    # bitwise (the untouched slots hold NaN-pattern argument sentinels)
+    # the extremum pcs_pool_finalize reads (max where gamma > 0, min where gamma < 0) and its
+    # row: the MFMA's fp32 sums of negated products are not always bitwise the negated sums
+    # (measured: one value in 4096 off by 2 ulp), so values agree to 1e-6 relative, rows exactly
+    val = torch.where(gamma[None, :] > 0, pools[0][..., 0], pools[0][..., 2])
+    vals = torch.where(gamma[None, :] > 0, pools[1][..., 0], pools[1][..., 2])
+    row = torch.where(gamma[None, :] > 0, pools[0][..., 1], pools[0][..., 3]).view(torch.int32)
+    rows = torch.where(gamma[None, :] > 0, pools[1][..., 1], pools[1][..., 3]).view(torch.int32)
+    assert torch.isfinite(val).all() and torch.equal(row, rows)
+    assert float(((val - vals).abs() / val.abs()).max()) <= 1e-6
+    st = torch.empty(B * a.chunks_per_scene, Nc, 2, device=DEV)
+    a.stats = st.data_ptr()
+    with pytest.raises(L.PcsError):
+        L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+
+
 @pytest.mark.parametrize("variant", ["glds", "noglds", "fp32"])
 @pytest.mark.parametrize("B,N,cps", [(2, 256 * 5 + 33, 2), (1, 300, 0)])
 def test_folded_dgrad_sparse_mask_s1(variant, B, N, cps):
@@ -199,7 +253,7 @@ def test_bn_stats_from_gram_scenes(dtype):
     G = (ad.T @ ad).float()
     Sb = ad.reshape(B, N, C).sum(1).float().contiguous()
     nbytes = L.load().pcs_bn_stats_from_gram_scenes_workspace(C, C)
-    assert nbytes == (C // 64) * C * 8
+    assert nbytes >= (C // 64) * C * 8
     ws = torch.empty(nbytes // 8, dtype=torch.float64, device=DEV)
     st = torch.empty(B, C, 2, device=DEV)
     L.call("pcs_bn_stats_from_gram_scenes", L.ptr(G), L.ptr(Sb), N, L.ptr(W), dt, C, C, C, B, L.ptr(ws), nbytes,

@@ -72,9 +72,9 @@ def main():
         Wf = W.float()
         L.call("pcs_quant_fp8_rows", L.ptr(Wf), Nc, K, K, L.ptr(W8), L.ptr(wsc), None, L.stream_ptr())
 
-        def run8(name, epi, stats=True, pool=True, **kw):
+        def run8(name, epi, stats=True, pool=True, flags=0, **kw):
             a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=Nc, dtype=L.BF16, prologue=L.PRO_RAW,
-                           epilogue=epi, chunks_per_scene=0, flags=L.FLAG_AW_FP8)
+                           epilogue=epi, chunks_per_scene=0, flags=L.FLAG_AW_FP8 | flags)
             lib.pcs_gemm_geometry(ct.byref(a))
             nch = B * a.chunks_per_scene
             keep = dict(stats=torch.empty(nch, Nc, 2, device=dev)) if stats else {}
@@ -88,7 +88,18 @@ def main():
 
         run8("[glds fp8] fwd, no epilogue work", L.EPI_FWD, stats=False, pool=False, es=gsign)
         run8("[glds fp8] fwd + stats", L.EPI_FWD, pool=False, es=gsign)
+        W8u = W8
+        W8s = torch.empty_like(W8)
+        signed = hasattr(L, "FLAG_POOL_SIGNED_W")
+        if signed:
+            L.call("pcs_sign_rows", L.ptr(W8), L.FP8, Nc, K, L.ptr(gsign), L.ptr(W8s), L.stream_ptr())
         for _ in range(2):
+            run8("[glds fp8] fwd + pool", L.EPI_FWD, stats=False, es=gsign)
+            if signed:
+                W8 = W8s
+                run8("[glds fp8] fwd + pool, signed W (training path)", L.EPI_FWD, stats=False, es=gsign,
+                     flags=L.FLAG_POOL_SIGNED_W)
+                W8 = W8u
             run8("[glds fp8] fwd + stats + pool", L.EPI_FWD, es=gsign)
             run8("[glds fp8] dgrad: mask + store + bias + S1", L.EPI_DGRAD, C=C, Yp=A8, bias=c)
         nb2 = lib.pcs_gram_raw_workspace(M, K)
@@ -123,6 +134,14 @@ def main():
         run(f"[{tag}] fwd, no epilogue work", L.EPI_FWD, fl, es=gsign)
         run(f"[{tag}] fwd + stats", L.EPI_FWD, fl, stats=True, es=gsign)
         run(f"[{tag}] fwd + stats + pool", L.EPI_FWD, fl, stats=True, pool=True, es=gsign)
+        run(f"[{tag}] fwd + pool", L.EPI_FWD, fl, pool=True, es=gsign)
+    if hasattr(L, "FLAG_POOL_SIGNED_W"):   # the training path: W rows pre-multiplied by sign(es)
+        Wu = W
+        W = torch.empty_like(Wu)
+        L.call("pcs_sign_rows", L.ptr(Wu), L.BF16, Nc, K, L.ptr(gsign), L.ptr(W), L.stream_ptr())
+        run("[glds] fwd + pool, signed W (bf16 training path)", L.EPI_FWD, L.FLAG_POOL_SIGNED_W, pool=True,
+            es=gsign)
+        W = Wu
     run("[glds] dgrad: mask + store", L.EPI_DGRAD, 0, C=C, Yp=A)
     run("[glds] dgrad: mask + store + bias + S1", L.EPI_DGRAD, 0, C=C, Yp=A, bias=c, stats=True)
     run("[gen ] dgrad (generic kernel, FLAG_NO_GLDS)", L.EPI_DGRAD, L.FLAG_NO_GLDS, C=C, Yp=A, bias=c, stats=True,
