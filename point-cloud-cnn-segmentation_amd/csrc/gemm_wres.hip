@@ -12,7 +12,10 @@
 // * y4 streams through a 5-stage LDS ring of 64-row tiles by LDS-DMA
 //   (global_load_lds_dwordx4): tile t+4 is requested as soon as tile t-1's stage is free, so
 //   four tiles of loads are in flight while tile t computes;
-// * a tile's output is stored one tile late (packed in registers meanwhile), and the wait for
+// * a tile's output is stored one tile late -- fp8: staged in the half's own rows of the tile's
+//   A stage (dead between its MFMAs and its restaging) and stored as whole 256-B row segments
+//   (4.4 -> 4.0 ms against 16 rows x 32 B per store instruction); bf16: packed in registers,
+//   16 rows x 64 B per store (its 16 KB per half do not fit those rows) -- and the wait for
 //   a tile's DMA is counted: vmcnt(n) with n = the vector-memory operations issued after it
 //   (gfx9 retires loads and stores on this counter in issue order, as hipcc itself assumes),
 //   so neither the newer loads nor the recent stores are drained;
@@ -208,6 +211,22 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
   uint32_t pend[NI][2][PW];        // the previous tile's output, stored one tile late
   int64_t pend_rb = 0;
   int pend_valid = 0;
+  // fp8: the packed outputs of tile t go to the half's own rows of A stage t (dead once its
+  // MFMAs have read it, until it is restaged one iteration later) in the A layout's swizzle,
+  // and are stored from there as whole 256-B row segments (16 lanes per row, two 16-B
+  // chunks per lane) instead of 16 rows x 32 B per store instruction
+  const int hq = tid & 255;   // the thread's index in its half
+  auto store_rows = [&](int t) {
+    const char *st = lds + OFF_A + (t % NSTAGE) * A_BYTES;
+    if (pend_valid == BMW) issued += 2;   // a partial tile may skip stores: count none
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = hq + 256 * h, r = wm * (BMW / 2) + (q >> 4), sl = q & 15;
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(st + r * ROWB + swz(r, sl) * 16);
+      if (r < pend_valid)
+        *reinterpret_cast<u32x4 *>(reinterpret_cast<fp8_t *>(a.C) + (pend_rb + r) * Ncols + n0 + sl * 16) = v;
+    }
+  };
   auto store_pending = [&]() {
     // a partial tile's stores may skip whole waves: count none of them (over-waits, safely)
     if (pend_valid == BMW) issued += NI * 2;
@@ -236,6 +255,9 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_raw();
+    if constexpr (C8) {
+      if (t > 0) store_rows(t - 1);   // tile t-1's rows, staged in its A stage by section 2
+    }
     const char *At = lds + OFF_A + (t % NSTAGE) * A_BYTES;
     f32x4 acc[NI][4];
 #pragma unroll
@@ -267,7 +289,9 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
     // transform tile t+1, epilogue of tile t
     barrier_raw();
     issue(t + NSTAGE - 1);
-    if (t > 0) store_pending();
+    if constexpr (!C8) {
+      if (t > 0) store_pending();
+    }
     if (t + 1 < ntl) transform(t + 1);
     // ---- epilogue: lane holds a5[m = 32 wm + 16 i + lr][c = 64 wn + 16 j + 4 lg + r]
     const int64_t rb = scene_row0 + (int64_t)(t_begin + t) * BMW;
@@ -305,6 +329,13 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
           csum2[j][1] += d[1];
         }
       }
+      if constexpr (C8) {
+        // -> this half's rows of stage t: row m, 16-B slot 4 wn + j (swizzled), dword lg
+        char *st = lds + OFF_A + (t % NSTAGE) * A_BYTES + m * ROWB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<uint32_t *>(st + swz(m, 4 * wn + j) * 16 + 4 * lg) = pk[j][0];
+        continue;
+      }
       // v_permlane16_swap: lane groups 2h / 2h+1 trade tiles 2q / 2q+1, leaving each lane 8
       // consecutive columns of tile 2q + (lg & 1)
 #pragma unroll
@@ -328,8 +359,19 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
     pend_rb = rb;
     pend_valid = valid;
   }
-  if (wm == 0) barrier_raw();   // re-align the halves
-  if (ntl > 0) store_pending();
+  if constexpr (C8) {
+    // the last tile's rows: the half's epilogue writes retire, then one barrier (half 0's
+    // matches half 1's last loop barrier), then half 0 re-aligns with half 1's
+    if (ntl > 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();
+      store_rows(ntl - 1);
+    }
+    if (wm == 0) barrier_raw();
+  } else {
+    if (wm == 0) barrier_raw();   // re-align the halves
+    if (ntl > 0) store_pending();
+  }
   wait_vm<0>();
 
   // ---- chunk end: column sums over the 16 lanes of each row group, then the two wave rows
@@ -350,7 +392,7 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
 
 }  // namespace
 
-// Measured at cfg2 (tools/bench_conv5.py): fp8 store 4.3-4.4 ms here vs 4.9 ms on the
+// Measured at cfg2 (tools/bench_conv5.py): fp8 store 4.0 ms here vs 4.9 ms on the
 // register-staged kernel; bf16 store 5.4 vs 5.0 ms, so bf16 stays there (the pass is bound by
 // the epilogue's vector work and the store issue, not by the MFMAs or the loads).
 bool pcs_gemm_wres_applicable(const pcs_gemm_args &a) {

@@ -71,10 +71,11 @@ def test_quant_fp8_rows_bit_exact():
     assert torch.equal(deq.cpu().double(), _dec(ref) * torch.exp2(e.double())[:, None])
 
 
-def test_bnrelu_epilogue_fp8_store_and_colsums():
+@pytest.mark.parametrize("B,N", [(2, 700), (3, 64 * 37 + 5), (1, 64 * 64)])
+def test_bnrelu_epilogue_fp8_store_and_colsums(B, N):
     import pcs_amd._lib as L
-    B, N, K, Nc = 2, 700, 128, 1024
-    g = torch.Generator().manual_seed(3)
+    K, Nc = 128, 1024
+    g = torch.Generator().manual_seed(3 + N)
     Y = torch.randn(B * N, K, generator=g).to(torch.bfloat16).to(DEV)
     ps = (torch.rand(K, generator=g) + 0.5).to(DEV)
     pt = (torch.randn(K, generator=g) * 0.2).to(DEV)
