@@ -172,6 +172,23 @@ int64_t pcs_dgrad_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_
 int pcs_dgrad_wgrad(const pcs_wgrad_args *args, const void *Wt, void *dX, pcs_stream_t stream);
 
 /*
+ * The same two gradients in folded form, without reading bn_seg1's stored output Y'
+ * (dy_mode PCS_PRO_RAW: dZ is bn_seg1's output gradient dz; x_mode PCS_PRO_BNRELU as above).
+ * With dy = alpha dz + beta + gamma Y' and Y' = x W^T + scene_bias[b] (the stored seg_conv1
+ * output, W = its local half as the forward GEMM saw it, fp32 [512, ldw]):
+ *   dX[m]  = dz[m] WaT^T + x[m] H + cvec[b],  cvec[b] = W^T (beta + gamma * scene_bias[b])
+ *   dW     = diag(alpha) dz^T x + beta (x) S + diag(gamma) (W G + sum_b scene_bias[b] (x) S_b)
+ * with WaT = (diag(alpha) W)^T [64, 512] and H = W^T diag(gamma) W [64, 64] in bf16 (pcs_bn_fold),
+ * G = x^T x, S_b = per-scene column sums of x (collected by the same pass).  dW (fp32, columns
+ * 0..63 of rows with stride ldw, as W) is written, not accumulated.  Workspace:
+ * pcs_dgrad_wgrad_folded_workspace() bytes (partials, their sums and cvec).  One pass reads
+ * dz [M, 512] and X [M, 64] and writes dX: 1.2 KB per point instead of 2.3 KB.
+ */
+int64_t pcs_dgrad_wgrad_folded_workspace(pcs_wgrad_args *args); /* bytes; fills splits_per_scene */
+int pcs_dgrad_wgrad_folded(const pcs_wgrad_args *args, const void *WaT, const void *H, const float *W,
+                           const float *scene_bias, void *dX, pcs_stream_t stream);
+
+/*
  * Fused input + weight gradient of a layer whose input gradient ends in the previous
  * layer's ReLU / dropout / BN-statistics epilogue (bf16; (Cout, Cin) = (K, Ncols) in
  * {64x64, 128x64}: conv2, conv3, conv4).  Takes the pcs_gemm arguments

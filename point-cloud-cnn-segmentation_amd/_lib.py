@@ -131,6 +131,8 @@ SIGNATURES = [
     ("pcs_bn_stats_from_gram", ct.c_int, [_vp, _vp, _i64, _vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp]),
     ("pcs_bn_stats_from_gram_scenes_workspace", _i64, [_i32, _i32]),
     ("pcs_sign_rows", ct.c_int, [_vp, _i32, _i64, _i64, _vp, _vp, _vp]),
+    ("pcs_dgrad_wgrad_folded_workspace", _i64, [ct.POINTER(WgradArgs)]),
+    ("pcs_dgrad_wgrad_folded", ct.c_int, [ct.POINTER(WgradArgs), _vp, _vp, _vp, _vp, _vp, _vp]),
     ("pcs_bn_stats_from_gram_scenes", ct.c_int, [_vp, _vp, _i64, _vp, _i32, _i64, _i32, _i32, _i64, _vp, _i64, _vp,
                                                  _vp]),
     ("pcs_confusion", ct.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),

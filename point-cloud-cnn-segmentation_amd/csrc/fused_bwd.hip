@@ -33,6 +33,13 @@ constexpr int OFF_OUT = OFF_X + MS * X_ROWB;       // dA2 tile [MS][CIN] bf16
 constexpr int OFF_COEF = OFF_OUT + MS * CIN * 2;  // alpha | beta | gamma [COUT], s | t [CIN]
 constexpr int LDS_BYTES = OFF_COEF + (3 * COUT + 2 * CIN) * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+// folded form: s | t | cvec [CIN] f32, then H [CIN][CIN] bf16 (XOR-swizzled 16-B slots)
+constexpr int OFF_H = OFF_COEF + 3 * CIN * 4;
+constexpr int H_ROWB = CIN * 2;
+constexpr int LDS_BYTES_F = OFF_H + CIN * H_ROWB;
+static_assert(LDS_BYTES_F <= 160 * 1024, "LDS budget (folded)");
+// folded form's per-slice partial slab: R = dz^T x [COUT][CIN] | G = x^T x [CIN][CIN] | S = sum x [CIN]
+constexpr int SLAB_F = COUT * CIN + CIN * CIN + CIN;
 constexpr int DY_CPR = COUT / 8, DY_RP = THREADS / DY_CPR, DY_NCH = MS / DY_RP;   // 64, 8, 8
 constexpr int X_CPR = CIN / 8, X_RP = THREADS / X_CPR;                            // 8, 64
 static_assert(X_RP == MS, "one x chunk per thread");
@@ -62,9 +69,18 @@ PCS_DEV bf16x8 tr_read(const char *base, int r0, int r1, int rowb, int col) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// FOLDED (dy_mode RAW): dy is dZ itself and Wt = (diag(alpha) W_l)^T, so the same contractions
+// give P = dZ (diag(alpha) W_l) and R = dZ^T x; the input gradient adds x H + cvec[scene] (H =
+// W_l^T diag(gamma) W_l, cvec = W_l^T (beta + gamma * scene_bias[b]), pcs_bn_fold algebra:
+// gamma * Y' W_l = x H + scene-bias terms, as Y' = x W_l^T + scene_bias[b]), and the slab also
+// collects G = x^T x and S = sum x for the Gram-form weight gradient (pcs_dgrad_wgrad_folded)
+// -- bn_seg1's stored Y' [M, 512] is not read at all.
+template <bool FOLDED>
 __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args a, const bf16_t *__restrict__ Wt,
-                                                                 bf16_t *__restrict__ dX, int64_t rows_per_split) {
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+                                                                 bf16_t *__restrict__ dX, int64_t rows_per_split,
+                                                                 const bf16_t *__restrict__ Hg,
+                                                                 const float *__restrict__ cvec) {
+  __shared__ __attribute__((aligned(16))) char lds[FOLDED ? LDS_BYTES_F : LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int sps = a.splits_per_scene;
@@ -87,10 +103,20 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
 
   // per-channel prologue coefficients -> LDS (read back at each store: fewer live registers)
   float *cf = reinterpret_cast<float *>(lds + OFF_COEF);
-  for (int i = tid; i < COUT; i += THREADS) {
-    cf[i] = a.alpha[i]; cf[COUT + i] = a.beta[i]; cf[2 * COUT + i] = a.gamma[i];
+  constexpr int CS = FOLDED ? 0 : 3 * COUT;   // x's bn2 scale | shift
+  if constexpr (FOLDED) {
+    if (tid < CIN) { cf[tid] = a.s[tid]; cf[CIN + tid] = a.t[tid]; cf[2 * CIN + tid] = cvec[scene * CIN + tid]; }
+    for (int i = tid; i < CIN * CIN / 8; i += THREADS) {   // H rows [c][j]
+      const int c = i / (CIN / 8), slot = i % (CIN / 8);
+      *reinterpret_cast<u32x4 *>(lds + OFF_H + c * H_ROWB + ((slot ^ (c & 7)) << 4)) =
+          *reinterpret_cast<const u32x4 *>(Hg + (int64_t)c * CIN + slot * 8);
+    }
+  } else {
+    for (int i = tid; i < COUT; i += THREADS) {
+      cf[i] = a.alpha[i]; cf[COUT + i] = a.beta[i]; cf[2 * COUT + i] = a.gamma[i];
+    }
+    if (tid < CIN) { cf[3 * COUT + tid] = a.s[tid]; cf[3 * COUT + CIN + tid] = a.t[tid]; }
   }
-  if (tid < CIN) { cf[3 * COUT + tid] = a.s[tid]; cf[3 * COUT + CIN + tid] = a.t[tid]; }
   __syncthreads();
 
   // staging ownership: dy column chunk dc (8 channels), rows dr0 + 8 i; x chunk xc, row xr
@@ -104,33 +130,49 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
       const int64_t r = pcs_min64(m0 + dr0 + DY_RP * i, hi - 1);
       const int64_t off = (sbase + r) * COUT + dc * 8;
       rz[i] = *reinterpret_cast<const u32x4 *>(dZ + off);
-      ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
+      if constexpr (!FOLDED) ry[i] = *reinterpret_cast<const u32x4 *>(Yg + off);
     }
     const int64_t r = pcs_min64(m0 + xr, hi - 1);
     rx = *reinterpret_cast<const u32x4 *>(Xg + (sbase + r) * CIN + xc * 8);
   };
+  float xsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // FOLDED: this thread's column sums of x
   auto store_step = [&](int64_t m0) {
-    float ca[8], cb[8], cg[8];
-    lds_vec8(cf + dc * 8, ca); lds_vec8(cf + COUT + dc * 8, cb); lds_vec8(cf + 2 * COUT + dc * 8, cg);
+    if constexpr (FOLDED) {   // dy = dZ: a copy
 #pragma unroll
-    for (int i = 0; i < DY_NCH; ++i) {
-      const int rl = dr0 + DY_RP * i;
-      float v[8], y[8];
-      unpack_chunk(rz[i], v);
-      unpack_chunk(ry[i], y);
+      for (int i = 0; i < DY_NCH; ++i) {
+        const int rl = dr0 + DY_RP * i;
+        const u32x4 out = m0 + rl >= hi ? mk_u32x4(0, 0, 0, 0) : rz[i];
+        *reinterpret_cast<u32x4 *>(lds + OFF_DY + prow(rl) * DY_ROWB + dc * 16) = out;
+      }
+    } else {
+      float ca[8], cb[8], cg[8];
+      lds_vec8(cf + dc * 8, ca); lds_vec8(cf + COUT + dc * 8, cb); lds_vec8(cf + 2 * COUT + dc * 8, cg);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
-      u32x4 out = pack_chunk(v);
-      if (m0 + rl >= hi) out = mk_u32x4(0, 0, 0, 0);
-      *reinterpret_cast<u32x4 *>(lds + OFF_DY + prow(rl) * DY_ROWB + dc * 16) = out;
+      for (int i = 0; i < DY_NCH; ++i) {
+        const int rl = dr0 + DY_RP * i;
+        float v[8], y[8];
+        unpack_chunk(rz[i], v);
+        unpack_chunk(ry[i], y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+        u32x4 out = pack_chunk(v);
+        if (m0 + rl >= hi) out = mk_u32x4(0, 0, 0, 0);
+        *reinterpret_cast<u32x4 *>(lds + OFF_DY + prow(rl) * DY_ROWB + dc * 16) = out;
+      }
     }
     float v[8], xs[8], xt[8];
-    lds_vec8(cf + 3 * COUT + xc * 8, xs); lds_vec8(cf + 3 * COUT + CIN + xc * 8, xt);
+    lds_vec8(cf + CS + xc * 8, xs); lds_vec8(cf + CS + CIN + xc * 8, xt);
     unpack_chunk(rx, v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
     u32x4 out = pack_chunk(v);
     if (m0 + xr >= hi) out = mk_u32x4(0, 0, 0, 0);
+    if constexpr (FOLDED) {   // the sums of the stored (bf16) x, as the contractions see it
+      float d[8];
+      unpack_chunk(out, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xsum[e] += d[e];
+    }
     *reinterpret_cast<u32x4 *>(lds + OFF_X + prow(xr) * X_ROWB + xc * 16) = out;
   };
 
@@ -139,6 +181,8 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // FOLDED: G = x^T x, tiles (w / 2, 2 (w % 2) + u) of the 4 x 4 16-tiles
+  f32x4 accg[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
   const int nsteps = (int)((hi - lo + MS - 1) / MS);
   if (nsteps > 0) {
@@ -154,8 +198,12 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
   const char *tDY = lds + OFF_DY, *tX = lds + OFF_X;
   for (int st = 0; st < nsteps; ++st) {
     const int64_t m0 = lo + (int64_t)st * MS;
-    // dgrad: out^T[c][m] = sum_k Wt[c][k] dy[m][k]
+    // dgrad: out^T[c][m] = sum_k Wt[c][k] dy[m][k]  (FOLDED: starts at cvec[c], + x H below)
     f32x4 accd[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if constexpr (FOLDED) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) accd[j] = *reinterpret_cast<const f32x4 *>(cf + 2 * CIN + (cb0 + j) * 16 + 4 * g);
+    }
     const int mrow = prow(mb * 16 + l16);
 #pragma unroll 4
     for (int kk = 0; kk < COUT / 32; ++kk) {
@@ -165,6 +213,19 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
       for (int j = 0; j < 2; ++j) {
         const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(lds + wt_off((cb0 + j) * 16 + l16, slot));
         accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf, accd[j], 0, 0, 0);
+      }
+    }
+    if constexpr (FOLDED) {   // + x H (K = 64: two k-steps over the staged x tile)
+#pragma unroll
+      for (int kk = 0; kk < CIN / 32; ++kk) {
+        const int slot = 4 * kk + g;
+        const bf16x8 xf = *reinterpret_cast<const bf16x8 *>(tX + mrow * X_ROWB + slot * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = (cb0 + j) * 16 + l16;
+          const bf16x8 hf = *reinterpret_cast<const bf16x8 *>(lds + OFF_H + c * H_ROWB + ((slot ^ (c & 7)) << 4));
+          accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf, xf, accd[j], 0, 0, 0);
+        }
       }
     }
     // wgrad: dW[o][c] += sum_m dy[m][o] x[m][c]; lane group g holds m = 8g..8g+7 of 32
@@ -182,6 +243,14 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           accw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], yf[i], accw[i][j], 0, 0, 0);
+      if constexpr (FOLDED) {   // fragments re-read at this wave's columns (no runtime register index)
+        const bf16x8 xi = tr_read(tX, r0, r1, X_ROWB, (wid >> 1) * 16 + 4 * p);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bf16x8 xj = tr_read(tX, r0, r1, X_ROWB, (2 * (wid & 1) + u) * 16 + 4 * p);
+          accg[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xj, xi, accg[u], 0, 0, 0);
+        }
+      }
     }
     // dA2 tile -> LDS: lane holds out[m = 16 mb + l16][c = 16 cb + 4 g + r]
 #pragma unroll
@@ -206,7 +275,25 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
   }
 
   // this slice's dW partial: lane holds dW[o = 64 w + 16 i + l16][c = 16 j + 4 g ..]
-  float *out = a.partial + (int64_t)L * COUT * CIN;
+  float *out = a.partial + (int64_t)L * (FOLDED ? SLAB_F : COUT * CIN);
+  if constexpr (FOLDED) {
+    // G tile (w / 2, 2 (w % 2) + u): lane holds G[16 (w / 2) + l16][16 (2 (w % 2) + u) + 4 g + r]
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *reinterpret_cast<float4 *>(out + COUT * CIN + ((wid >> 1) * 16 + l16) * CIN + (2 * (wid & 1) + u) * 16 + 4 * g) =
+          make_float4(accg[u][0], accg[u][1], accg[u][2], accg[u][3]);
+    // S: the 64 row-threads of each 8-column chunk, summed in a fixed order through LDS
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(lds + OFF_DY);   // [64 rows][64 cols]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[xr * CIN + xc * 8 + e] = xsum[e];
+    __syncthreads();
+    if (tid < CIN) {
+      float t = 0.f;
+      for (int r = 0; r < X_RP; ++r) t += red[r * CIN + tid];
+      out[COUT * CIN + CIN * CIN + tid] = t;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int o = wid * 64 + i * 16 + l16;
@@ -250,10 +337,116 @@ extern "C" int pcs_dgrad_wgrad(const pcs_wgrad_args *ap, const void *Wt, void *d
   const int64_t rps = ((a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene + MS - 1) / MS * MS;
   const int nb = (int)(a.num_scenes * a.splits_per_scene);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(dgrad_wgrad_s1_kernel, dim3(nb), dim3(THREADS), 0, s, a, static_cast<const bf16_t *>(Wt),
-                     static_cast<bf16_t *>(dX), rps);
+  hipLaunchKernelGGL(dgrad_wgrad_s1_kernel<false>, dim3(nb), dim3(THREADS), 0, s, a, static_cast<const bf16_t *>(Wt),
+                     static_cast<bf16_t *>(dX), rps, nullptr, nullptr);
   PCS_CHECK_LAUNCH();
   return pcs_reduce_partials(a.partial, nb, (int64_t)COUT * CIN, 1.0f, a.dW, a.ldw ? a.ldw : CIN, CIN, stream);
+}
+
+// ---------------------------------------------------------------------------------------
+// Folded form (pcs_dgrad_wgrad_folded): the slab sums, then the Gram-form weight gradient
+//   dW_l = diag(alpha) R + beta (x) S + diag(gamma) (W_l G + sum_b scene_bias[b] (x) S_b)
+// (dy = alpha dz + beta + gamma Y', Y' = x W_l^T + scene_bias[b]), and the per-scene
+// constant row of the input gradient cvec[b] = W_l^T (beta + gamma * scene_bias[b]).
+// ---------------------------------------------------------------------------------------
+namespace {
+
+constexpr int RG_LEN = COUT * CIN + CIN * CIN;   // R | G, summed over every slab
+
+// red[0 .. RG_LEN) = sum over slabs (fixed order); Sb[b][j] = sum over scene b's slabs
+__global__ __launch_bounds__(256) void folded_reduce_kernel(const float *__restrict__ part, int nslab, int sps,
+                                                            int B, float *__restrict__ red, float *__restrict__ Sb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < RG_LEN) {
+    float t = 0.f;
+    for (int sl = 0; sl < nslab; ++sl) t += part[(int64_t)sl * SLAB_F + i];
+    red[i] = t;
+  } else if (i < RG_LEN + B * CIN) {
+    const int b = (i - RG_LEN) / CIN, j = (i - RG_LEN) % CIN;
+    float t = 0.f;
+    for (int sl = b * sps; sl < (b + 1) * sps; ++sl) t += part[(int64_t)sl * SLAB_F + RG_LEN + j];
+    Sb[b * CIN + j] = t;
+  }
+}
+
+// block = output row k of dW_l (COUT blocks), thread = input channel j (CIN threads)
+__global__ __launch_bounds__(CIN) void folded_assemble_kernel(const float *__restrict__ red, const float *__restrict__ Sb,
+                                                              int B, const float *__restrict__ W, int64_t ldw,
+                                                              const float *__restrict__ alpha,
+                                                              const float *__restrict__ beta,
+                                                              const float *__restrict__ gamma,
+                                                              const float *__restrict__ sbias, float *__restrict__ dW,
+                                                              int64_t ldo) {
+  __shared__ float wk[CIN];
+  const int k = blockIdx.x, j = threadIdx.x;
+  wk[j] = W[(int64_t)k * ldw + j];
+  __syncthreads();
+  const float *G = red + COUT * CIN;
+  float wg = 0.f;
+  for (int i = 0; i < CIN; ++i) wg = fmaf(wk[i], G[i * CIN + j], wg);
+  float S = 0.f, sbs = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float sbj = Sb[b * CIN + j];
+    S += sbj;
+    sbs = fmaf(sbias[(int64_t)b * COUT + k], sbj, sbs);
+  }
+  dW[(int64_t)k * ldo + j] = fmaf(alpha[k], red[k * CIN + j], fmaf(beta[k], S, gamma[k] * (wg + sbs)));
+}
+
+// cvec[b][j] = sum_k (beta[k] + gamma[k] * sbias[b][k]) W[k][j]: block b, thread j
+__global__ __launch_bounds__(CIN) void folded_cvec_kernel(const float *__restrict__ W, int64_t ldw,
+                                                          const float *__restrict__ beta, const float *__restrict__ gamma,
+                                                          const float *__restrict__ sbias, float *__restrict__ cvec) {
+  const int b = blockIdx.x, j = threadIdx.x;
+  float t = 0.f;
+  for (int k = 0; k < COUT; ++k)
+    t = fmaf(fmaf(gamma[k], sbias[(int64_t)b * COUT + k], beta[k]), W[(int64_t)k * ldw + j], t);
+  cvec[b * CIN + j] = t;
+}
+
+bool folded_shapes_ok(const pcs_wgrad_args &a) {
+  return a.dtype == PCS_BF16 && a.Cout == COUT && a.Cin == CIN && a.dy_mode == PCS_PRO_RAW &&
+         a.x_mode == PCS_PRO_BNRELU && !a.x_mask && !(a.flags & PCS_FLAG_GENERIC);
+}
+
+}  // namespace
+
+extern "C" int64_t pcs_dgrad_wgrad_folded_workspace(pcs_wgrad_args *a) {
+  if (!a || a->num_scenes <= 0 || a->scene_rows <= 0)
+    return pcs_set_einval("pcs_dgrad_wgrad_folded_workspace", "bad geometry");
+  if (!folded_shapes_ok(*a))
+    return pcs_set_einval("pcs_dgrad_wgrad_folded_workspace",
+                          "bf16, Cout=512, Cin=64, dy_mode PRO_RAW, x_mode PRO_BNRELU, no x_mask only");
+  a->splits_per_scene = (int32_t)splits_of(*a);
+  const int64_t nb = a->num_scenes * a->splits_per_scene;
+  return (nb * SLAB_F + RG_LEN + a->num_scenes * CIN + a->num_scenes * CIN) * 4;
+}
+
+extern "C" int pcs_dgrad_wgrad_folded(const pcs_wgrad_args *ap, const void *WaT, const void *H, const float *W,
+                                      const float *scene_bias, void *dX, pcs_stream_t stream) {
+  if (!ap || !WaT || !H || !W || !scene_bias || !dX) return pcs_set_einval("pcs_dgrad_wgrad_folded", "null argument");
+  pcs_wgrad_args a = *ap;
+  if (pcs_dgrad_wgrad_folded_workspace(&a) < 0) return PCS_EINVAL;
+  if (!a.dZ || !a.alpha || !a.beta || !a.gamma || !a.X || !a.s || !a.t || !a.partial || !a.dW || a.ldw < CIN)
+    return pcs_set_einval("pcs_dgrad_wgrad_folded", "missing operand (dZ, alpha, beta, gamma, X, s, t, partial, dW, "
+                                                    "ldw >= 64)");
+  if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31) return pcs_set_einval("pcs_dgrad_wgrad_folded", "M must be < 2^31");
+  const int64_t rps = ((a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene + MS - 1) / MS * MS;
+  const int B = (int)a.num_scenes;
+  const int nb = B * a.splits_per_scene;
+  float *red = a.partial + (int64_t)nb * SLAB_F;
+  float *Sb = red + RG_LEN;
+  float *cvec = Sb + B * CIN;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(folded_cvec_kernel, dim3(B), dim3(CIN), 0, s, W, a.ldw, a.beta, a.gamma, scene_bias, cvec);
+  hipLaunchKernelGGL(dgrad_wgrad_s1_kernel<true>, dim3(nb), dim3(THREADS), 0, s, a, static_cast<const bf16_t *>(WaT),
+                     static_cast<bf16_t *>(dX), rps, static_cast<const bf16_t *>(H), cvec);
+  hipLaunchKernelGGL(folded_reduce_kernel, dim3((RG_LEN + B * CIN + 255) / 256), dim3(256), 0, s, a.partial, nb,
+                     a.splits_per_scene, B, red, Sb);
+  hipLaunchKernelGGL(folded_assemble_kernel, dim3(COUT), dim3(CIN), 0, s, red, Sb, B, W, a.ldw, a.alpha, a.beta,
+                     a.gamma, scene_bias, a.dW, a.ldw);
+  PCS_CHECK_LAUNCH();
+  return 0;
 }
 
 // =======================================================================================
@@ -425,7 +618,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
     f32x4 accd[F::TPW_D];
 #pragma unroll
     for (int u = 0; u < F::TPW_D; ++u) accd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
+#pragma unroll 4
     for (int kk = 0; kk < COUT / 32; ++kk) {
       const int slot = 4 * kk + g;
       const bf16x8 yf = *reinterpret_cast<const bf16x8 *>(tDY + prow(ml) * F::DY_ROWB + slot * 16);

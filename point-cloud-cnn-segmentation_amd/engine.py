@@ -151,6 +151,7 @@ class Saved:
     mask_bufs: tuple = None                       # dropout keep bits drawn on the side stream
     gram5: tuple = None                           # bf16/fp8: (G, per-scene S, workspace) of a5, from the forward
     wg_eff: torch.Tensor = None                   # global_feat's weight as the forward GEMM saw it (fp32)
+    sbias_s1: torch.Tensor = None                 # [B, 512] per-scene (centred) bias of the stored seg_conv1 output
     mask_ready: object = None                     # torch.cuda.Event recorded after them
 
 
@@ -503,6 +504,7 @@ class Engine:
         Ws1 = P["seg_conv1.weight"]
         L.call("pcs_scene_gemv", L.ptr(sv.g), B, 1024, L.ptr(Ws1), Ws1.shape[1], 64,
                L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), L.ptr(soff), s)
+        sv.sbias_s1 = sbias   # the stored Y'_seg1 = a2 W_l^T + sbias[b] (the folded backward)
         layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", soff, scene_bias=sbias)
 
         # dropout keep bits (P:124, P:126)
@@ -702,22 +704,32 @@ class Engine:
         # seg_conv1 local half: dA2 contribution (raw) and dW[:, :64]
         dA2 = torch.empty(M, 64, dtype=self.tdt, device=dev)
         if self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC):
-            # one pass over dy's inputs for both gradients (csrc/fused_bwd.hip)
+            # folded form, one pass over dz_s1 and y2 (csrc/fused_bwd.hip): with dy = a1 dz +
+            # b1 + g1 Y' and Y' = a2 W_l^T + sbias[b] (the stored pre-BN output),
+            #   dA2 = dz (diag(a1) W_l) + a2 H + cvec[b],  H = W_l^T diag(g1) W_l,
+            #   dW_l = diag(a1) dz^T a2 + b1 (x) S + diag(g1) (W_l G2 + sum_b sbias[b] (x) S_b)
+            # (G2 = a2^T a2, S_b = per-scene column sums of a2), so bn_seg1's Y' is not read
             p2 = sv.bn["bn2"]
+            Ws1_r = self._rounded(Ws1)     # the W_l the forward GEMM used
+            WaT = torch.empty(64, 512, dtype=self.tdt, device=dev)
+            Hs1 = torch.empty(64, 64, dtype=self.tdt, device=dev)
+            cf1 = torch.empty(64, dtype=torch.float32, device=dev)
+            L.call("pcs_bn_fold", L.ptr(Ws1_r), 512, 64, Ws1.shape[1], L.ptr(a1), L.ptr(b1), L.ptr(g1), self.dt,
+                   L.ptr(WaT), L.ptr(cf1), L.ptr(Hs1), s)
             fa = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=512, Cin=64, dtype=self.dt,
-                             splits_per_scene=0, dy_mode=L.PRO_BWD, x_mode=L.PRO_BNRELU,
+                             splits_per_scene=0, dy_mode=L.PRO_RAW, x_mode=L.PRO_BNRELU,
                              x_keep_scale=1.0, dW=L.ptr(G("seg_conv1.weight")), ldw=Ws1.shape[1],
-                             flags=self.flags, dZ=L.ptr(dz_s1), Y=L.ptr(ys["seg_conv1"]), alpha=L.ptr(a1),
+                             flags=self.flags, dZ=L.ptr(dz_s1), alpha=L.ptr(a1),
                              beta=L.ptr(b1), gamma=L.ptr(g1), X=L.ptr(ys["conv2"]), s=L.ptr(p2.scale),
                              t=L.ptr(p2.shift))
-            nbytes = L.load().pcs_dgrad_wgrad_workspace(ct.byref(fa))
+            nbytes = L.load().pcs_dgrad_wgrad_folded_workspace(ct.byref(fa))
             if nbytes < 0:
                 raise L.PcsError(L.load().pcs_last_error().decode())
             ws1 = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
             fa.partial = ws1.data_ptr()
-            self._launch("dgrad+wgrad:seg_conv1", "pcs_dgrad_wgrad", ct.byref(fa), L.ptr(wc["seg_conv1"][1]),
-                         L.ptr(dA2), s)
-            keepalive.append(ws1)
+            self._launch("dgrad+wgrad:seg_conv1", "pcs_dgrad_wgrad_folded", ct.byref(fa), L.ptr(WaT), L.ptr(Hs1),
+                         L.ptr(Ws1_r), L.ptr(sv.sbias_s1), L.ptr(dA2), s)
+            keepalive.append((ws1, Ws1_r, WaT, Hs1, cf1))
         else:
             self._gemm(B, N, 512, 64, L.PRO_BWD, L.EPI_RAW, dz_s1, wc["seg_conv1"][1], dA2,
                        A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")

@@ -56,6 +56,55 @@ def test_dgrad_wgrad_matches_torch(B, N):
     assert torch.all(dW[:, 64:] == 7.0)
 
 
+@pytest.mark.parametrize("B,N", [(3, 1000), (4, 4096), (1, 70), (2, 64 * 300 + 17)])
+def test_dgrad_wgrad_folded_matches_torch(B, N):
+    """pcs_dgrad_wgrad_folded: the same two gradients from dz and x alone (bn_seg1's stored
+    Y' = x W^T + sbias[b] is never read), against torch fp64 of the unfolded definition:
+    dy = alpha dz + beta + gamma Y', dX = dy W, dW = dy^T x.  dX carries the bf16 rounding of
+    the folded operands (diag(alpha) W)^T and H = W^T diag(gamma) W and of dX itself (1e-2
+    norm-relative, as the unfolded kernel's bf16 dy); dW is assembled in fp32 from exact
+    bf16 products (2e-4)."""
+    import pcs_amd._lib as L
+    g = torch.Generator(device="cpu").manual_seed(B * 7907 + N)
+    M = B * N
+    dZ = (torch.randn(M, 512, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    X = torch.randn(M, 64, generator=g).to(DEV, torch.bfloat16)
+    alpha, beta, gamma = (torch.randn(512, generator=g).to(DEV) * s for s in (1.0, 0.01, 0.05))
+    sx, tx = torch.rand(64, generator=g).to(DEV) + 0.5, torch.randn(64, generator=g).to(DEV) * 0.2
+    Wf = torch.zeros(512, 1088, device=DEV)
+    Wf[:, :64] = (torch.randn(512, 64, generator=g) * 0.05).to(torch.bfloat16).float().to(DEV)
+    sbias = torch.randn(B, 512, generator=g).to(DEV) * 0.5
+    WaT = torch.empty(64, 512, dtype=torch.bfloat16, device=DEV)
+    H = torch.empty(64, 64, dtype=torch.bfloat16, device=DEV)
+    c = torch.empty(64, device=DEV)
+    L.call("pcs_bn_fold", L.ptr(Wf), 512, 64, 1088, L.ptr(alpha), L.ptr(beta), L.ptr(gamma), L.BF16, L.ptr(WaT),
+           L.ptr(c), L.ptr(H), L.stream_ptr())
+    dW = torch.full((512, 1088), 7.0, device=DEV)
+    dX = torch.empty(M, 64, device=DEV, dtype=torch.bfloat16)
+    a = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=512, Cin=64, dtype=L.BF16, splits_per_scene=0,
+                    dy_mode=L.PRO_RAW, x_mode=L.PRO_BNRELU, x_keep_scale=1.0, dW=dW.data_ptr(), ldw=1088,
+                    dZ=dZ.data_ptr(), alpha=alpha.data_ptr(), beta=beta.data_ptr(), gamma=gamma.data_ptr(),
+                    X=X.data_ptr(), s=sx.data_ptr(), t=tx.data_ptr())
+    nbytes = L.load().pcs_dgrad_wgrad_folded_workspace(ct.byref(a))
+    assert nbytes > 0
+    ws = torch.empty(nbytes // 4, device=DEV)
+    a.partial = ws.data_ptr()
+    L.call("pcs_dgrad_wgrad_folded", ct.byref(a), L.ptr(WaT), L.ptr(H), L.ptr(Wf), L.ptr(sbias), L.ptr(dX),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    x = torch.relu(X.float() * sx + tx).to(torch.bfloat16).double()
+    Wl = Wf[:, :64].double()
+    Yp = x @ Wl.t() + sbias.double().repeat_interleave(N, dim=0)
+    dy = alpha.double() * dZ.double() + beta.double() + gamma.double() * Yp
+    ref_dx, ref_dw = dy @ Wl, dy.t() @ x
+    print(f"dX rel {_rel(dX.double(), ref_dx):.2e}  dW rel {_rel(dW[:, :64].double(), ref_dw):.2e}")
+    assert _rel(dX.double(), ref_dx) < 1e-2
+    assert _rel(dW[:, :64].double(), ref_dw) < 2e-4
+    assert torch.all(dW[:, 64:] == 7.0)
+    a.dy_mode = L.PRO_BWD
+    assert L.load().pcs_dgrad_wgrad_folded_workspace(ct.byref(a)) < 0
+
+
 def test_dgrad_wgrad_rejects_other_shapes():
     import pcs_amd._lib as L
     a = L.WgradArgs(num_scenes=1, scene_rows=128, Cout=256, Cin=64, dtype=L.BF16, dy_mode=L.PRO_BWD,
