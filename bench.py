@@ -96,6 +96,8 @@ def kernel_model(tag, M, dtype):
     a5b = 1 if dtype == "fp8" else ab
     cin, cout = LAYER_DIMS[conv]
     flops = 2.0 * M * cin * cout
+    if kind == "dgrad+wgrad" and conv == "seg_conv1":   # folded: dz and y2 in, dA2 out (Y' not read)
+        return 2 * flops, M * (cout + 2 * cin) * ab
     if kind == "dgrad+wgrad":   # fused: dZ, Y in once, Y_{l-1} (+ addend) in, dZ_{l-1} out
         extra = cin if conv == "conv3" else 0
         return 2 * flops, M * (2 * cout + 2 * cin + extra) * ab
@@ -107,7 +109,9 @@ def kernel_model(tag, M, dtype):
         return flops, M * (cin * a5b + cout * ab)
     if conv == "conv5" and kind == "fwd":           # a4 in, a5 out
         return flops, M * (cin * ab + cout * a5b)
-    if conv == "conv5" and kind in ("dgrad", "wgrad"):   # folded form: dz5 + y4/128-wide out
+    if conv == "conv5" and kind == "dgrad":   # folded, one pass: dz5, y4 in, dz4 out (+ a4 H4 FLOPs)
+        return flops + 2.0 * M * cin * cin, M * (cout + 2 * cin) * ab
+    if conv == "conv5" and kind == "wgrad":   # R = dz5^T a4: dz5, y4 in
         return flops, M * (cout + cin) * ab
     if kind == "fwd":
         nbytes = M * (cin + cout) * ab

@@ -52,8 +52,13 @@ enum {
   PCS_PRO_RAW = 0,      /* a = A                                                        */
   PCS_PRO_BNRELU = 1,   /* a = max(A*s[k] + t[k], 0) [* keep(m,k) * keep_scale]  P:106-127 */
   PCS_PRO_BWD = 2,      /* a = alpha[k]*dZ[m,k] + beta[k] + gamma[k]*Y[m,k]   BN backward */
-  PCS_PRO_BWD_POOL = 3  /* a = beta[k] + gamma[k]*Y[m,k] + (m==am[b,k] ? sp[b,k] : 0)
+  PCS_PRO_BWD_POOL = 3, /* a = beta[k] + gamma[k]*Y[m,k] + (m==am[b,k] ? sp[b,k] : 0)
                            BN backward of bn_global fed by the max-pool (P:113-114)      */
+  PCS_PRO_CAT = 4       /* a = [A | relu(A2*s + t)] concatenated along k: columns k < K1 raw
+                           from A [M, K1], columns K1.. from A2 [M, K-K1] through BN+ReLU
+                           (s = pa, t = pb over A2's channels); W [Ncols, K1] for the first
+                           part, W2 [Ncols, K-K1] for the second (generic kernel only).
+                           conv5's folded input gradient dz5 Ws + a4 H4 in one pass        */
 };
 
 /* epilogue of the points-major GEMM */
@@ -117,6 +122,8 @@ typedef struct {
   int64_t pool_ldw;
   int32_t pool_c;
   const uint8_t *w_scale; /* [Ncols] E8M0 scale of each W row (PCS_FLAG_AW_FP8) */
+  const void *W2;       /* [Ncols, K - K1] dtype: the second W block (PCS_PRO_CAT) */
+  int32_t K1;           /* PCS_PRO_CAT: width of A (a multiple of the 32/16-element k-step) */
 } pcs_gemm_args;
 
 /* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error.  The

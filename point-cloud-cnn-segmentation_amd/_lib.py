@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "csrc", "libpcs.so")
 
 F32, BF16, FP8 = 0, 1, 2
-PRO_RAW, PRO_BNRELU, PRO_BWD, PRO_BWD_POOL = 0, 1, 2, 3
+PRO_RAW, PRO_BNRELU, PRO_BWD, PRO_BWD_POOL, PRO_CAT = 0, 1, 2, 3, 4
 EPI_FWD, EPI_DGRAD, EPI_RAW, EPI_BNRELU = 0, 1, 2, 3
 HEAD_FWD, HEAD_CE, HEAD_BWD = 0, 1, 2
 
@@ -38,6 +38,7 @@ class GemmArgs(ct.Structure):
         ("Yp", _vp), ("es", _vp), ("et", _vp), ("emean", _vp), ("erstd", _vp),
         ("stats", _vp), ("pool", _vp), ("flags", _i32),
         ("pool_w", _vp), ("pool_ldw", _i64), ("pool_c", _i32), ("w_scale", _vp),
+        ("W2", _vp), ("K1", _i32),
     ]
 
 

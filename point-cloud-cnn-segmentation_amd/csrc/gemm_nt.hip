@@ -60,7 +60,8 @@ PCS_DEV int xcd_remap(int bid, int nb) {
 constexpr int KMAX = 1024;   // prologue coefficient arrays staged in LDS (K <= KMAX)
 
 template <int PRO> struct Coef {   // per-channel prologue arrays kept in LDS
-  static constexpr int N = PRO == PCS_PRO_BNRELU ? 2 : PRO == PCS_PRO_BWD ? 3 : PRO == PCS_PRO_BWD_POOL ? 4 : 0;
+  static constexpr int N = (PRO == PCS_PRO_BNRELU || PRO == PCS_PRO_CAT) ? 2 : PRO == PCS_PRO_BWD ? 3
+                           : PRO == PCS_PRO_BWD_POOL ? 4 : 0;
 };
 
 template <int EPC>
@@ -79,6 +80,24 @@ PCS_DEV void nt_load(const pcs_gemm_args &a, const T *__restrict__ Ag, const T *
                      int srow, u32x4 (&ra)[BM / 64], u32x4 (&ra2)[BM / 64], u32x4 (&rb)[BN / 64],
                      uint32_t (&mk)[BM / 64]) {
   constexpr int EPC = Elem<T>::EPC;
+  if constexpr (PRO == PCS_PRO_CAT) {   // k-steps never straddle K1 (a multiple of the k-step)
+    const int K1 = a.K1, K2 = K - K1;
+    const bool first = k0 < K1;
+#pragma unroll
+    for (int i = 0; i < BM / 64; ++i) {
+      const int r = min(srow + 64 * i, valid - 1);
+      ra[i] = first ? *reinterpret_cast<const u32x4 *>(Ag + (row_base + r) * K1 + k0)
+                    : *reinterpret_cast<const u32x4 *>(A2g + (row_base + r) * K2 + (k0 - K1));
+    }
+    const T *W2g = reinterpret_cast<const T *>(a.W2);
+#pragma unroll
+    for (int i = 0; i < BN / 64; ++i) {
+      const int64_t n = n0 + srow + 64 * i;
+      rb[i] = first ? *reinterpret_cast<const u32x4 *>(Wg + n * K1 + k0)
+                    : *reinterpret_cast<const u32x4 *>(W2g + n * K2 + (k0 - K1));
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < BM / 64; ++i) {
     const int r = min(srow + 64 * i, valid - 1);   // clamped: rows >= valid are zeroed later
@@ -104,8 +123,11 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, const float *cf, int64_t
   constexpr int EPC = Elem<T>::EPC;
   char *tB = tA + BM * ROWB;
   float c0[EPC], c1[EPC], c2[EPC];
+  const bool cat2 = PRO == PCS_PRO_CAT && k0 >= a.K1;   // the BN+ReLU part of a CAT operand
   if constexpr (PRO == PCS_PRO_BNRELU) {
     lds_vec<EPC>(cf + k0, c0); lds_vec<EPC>(cf + KMAX + k0, c1);
+  } else if constexpr (PRO == PCS_PRO_CAT) {
+    if (cat2) { lds_vec<EPC>(cf + (k0 - a.K1), c0); lds_vec<EPC>(cf + KMAX + (k0 - a.K1), c1); }
   } else if constexpr (PRO == PCS_PRO_BWD || PRO == PCS_PRO_BWD_POOL) {
     lds_vec<EPC>(cf + k0, c0); lds_vec<EPC>(cf + KMAX + k0, c1); lds_vec<EPC>(cf + 2 * KMAX + k0, c2);
   }
@@ -121,6 +143,11 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, const float *cf, int64_t
         if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
         v[e] = x;
       }
+    } else if constexpr (PRO == PCS_PRO_CAT) {
+      if (cat2) {
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v[e] = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+      }
     } else if constexpr (PRO == PCS_PRO_BWD) {
       float y[EPC];
       unpack_chunk(ra2[i], y);
@@ -132,7 +159,7 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, const float *cf, int64_t
 #pragma unroll
       for (int e = 0; e < EPC; ++e) v[e] = fmaf(c2[e], v[e], c1[e]) + (am[e] == grow ? c0[e] : 0.f);
     }
-    u32x4 out = PRO == PCS_PRO_RAW ? ra[i] : pack_chunk(v);
+    u32x4 out = (PRO == PCS_PRO_RAW || (PRO == PCS_PRO_CAT && !cat2)) ? ra[i] : pack_chunk(v);
     if (r >= valid) out = mk_u32x4(0, 0, 0, 0);
     *reinterpret_cast<u32x4 *>(tA + r * ROWB + swz(r, slot) * 16) = out;
   }
@@ -193,8 +220,8 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
   T *__restrict__ Cg = reinterpret_cast<T *>(a.C);
 
   // per-channel coefficients -> LDS (a workgroup's rows never leave its scene)
-  for (int k = tid; k < K; k += THREADS) {
-    if constexpr (PRO == PCS_PRO_BNRELU) {
+  for (int k = tid; k < (PRO == PCS_PRO_CAT ? K - a.K1 : K); k += THREADS) {
+    if constexpr (PRO == PCS_PRO_BNRELU || PRO == PCS_PRO_CAT) {
       cf[k] = a.pa[k]; cf[KMAX + k] = a.pb[k];
     } else if constexpr (PRO == PCS_PRO_BWD) {
       cf[k] = a.pa[k]; cf[KMAX + k] = a.pb[k]; cf[2 * KMAX + k] = a.pc[k];
@@ -518,6 +545,8 @@ int dispatch_pro_epi(const pcs_gemm_args &a, int tps, int tpc, hipStream_t s) {
           return launch_t<T, BM, BN, PCS_PRO_BWD_POOL, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
         case PCS_PRO_BNRELU:   // a_{l-1} H (folded BN backward of a wide layer, see pcs_bn_fold)
           return launch_t<T, BM, BN, PCS_PRO_BNRELU, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
+        case PCS_PRO_CAT:      // dz5 (diag alpha W5) + a4 H4 + c (conv5, folded, one pass)
+          return launch_t<T, BM, BN, PCS_PRO_CAT, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
         case PCS_PRO_RAW:      // a5 H + c + max-pool rows (global_feat, folded)
           return a.pool_w ? launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_DGRAD, false, true>(a, tps, tpc, s)
                           : launch_t<T, BM, BN, PCS_PRO_RAW, PCS_EPI_DGRAD, false>(a, tps, tpc, s);
@@ -555,6 +584,7 @@ static constexpr int GEMM_BM = 128;
 // of that class ends up on the generic kernel (an operand combination the wide kernels do not
 // implement), that kernel walks the same chunks in 128-row tiles.
 static bool wide_class(const pcs_gemm_args &a) {
+  if (a.prologue == PCS_PRO_CAT) return false;   // generic kernel only
   // seg_conv3's input gradient (K 128 -> 256 columns, DGRAD epilogue): the 128-row kernel
   // measured faster at cfg2 (3.13 vs 3.38 ms, tools/bench_bwd_shapes.py)
   if (a.K == 128 && a.Ncols == 256 && a.epilogue == PCS_EPI_DGRAD) return false;
@@ -601,7 +631,14 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
                                       "0 < pool_c <= 1024, pool_ldw >= Ncols");
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31)
     return pcs_set_einval("pcs_gemm", "M must be < 2^31 rows");
-  if (a.K > KMAX) return pcs_set_einval("pcs_gemm", "K must be <= 1024");
+  if (a.prologue == PCS_PRO_CAT) {
+    if (!a.A2 || !a.W2 || !a.pa || !a.pb || a.K1 <= 0 || a.K1 >= a.K || a.K1 % kstep || a.K - a.K1 > KMAX ||
+        a.epilogue != PCS_EPI_DGRAD || a.a_mask)
+      return pcs_set_einval("pcs_gemm", "PRO_CAT needs A2, W2, pa, pb, 0 < K1 < K (a k-step multiple), "
+                                        "K - K1 <= 1024, EPI_DGRAD, no a_mask");
+  } else if (a.K > KMAX) {
+    return pcs_set_einval("pcs_gemm", "K must be <= 1024");
+  }
   if ((a.flags & PCS_FLAG_AW_FP8) && !(wide_class(a) && pcs_gemm_glds_applicable(a)))
     return pcs_set_einval("pcs_gemm", "fp8 operands (PCS_FLAG_AW_FP8) need the LDS-DMA kernel: bf16 C, RAW prologue, "
                                       "K % 256 == 0, Ncols % 256 == 0, w_scale, FWD (no C) or folded DGRAD");

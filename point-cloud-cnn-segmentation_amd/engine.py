@@ -276,7 +276,7 @@ class Engine:
                        A=L.ptr(A), W=L.ptr(W), C=L.ptr(C),
                        a_keep_scale=kw.pop("a_keep_scale", 1.0),
                        c_keep_scale=kw.pop("c_keep_scale", 1.0),
-                       pool_ldw=kw.pop("pool_ldw", 0), pool_c=kw.pop("pool_c", 0))
+                       pool_ldw=kw.pop("pool_ldw", 0), pool_c=kw.pop("pool_c", 0), K1=kw.pop("K1", 0))
         for k, v in kw.items():
             setattr(a, k, L.ptr(v))
         self._launch(tag, "pcs_gemm", ct.byref(a), self._stream())
@@ -835,19 +835,18 @@ class Engine:
         h4 = self._empty(128, 128, device=dev)
         L.call("pcs_bn_fold", L.ptr(W5_r), 1024, 128, 128, L.ptr(al5), L.ptr(be5), L.ptr(ga5), self.dt,
                L.ptr(ws_t), L.ptr(c5), L.ptr(h4), s)
-        pbuf = self._empty(M, 128, device=dev)
-        self._gemm(B, N, 1024, 128, L.PRO_RAW, L.EPI_FWD, dz5, ws_t, pbuf, bias=c5, tag="dgrad:conv5")
-        cps4, _ = self.geometry(B, N, 128, 128, L.PRO_BNRELU, L.EPI_DGRAD)
+        # one pass: [dz5 | a4] [Ws ; H4] + c5 (PCS_PRO_CAT), then bn4's ReLU mask and S1 / S2
+        cps4, _ = self.geometry(B, N, 1024 + 128, 128, L.PRO_CAT, L.EPI_DGRAD)
         st = torch.empty(B * cps4, 128, 2, dtype=torch.float32, device=dev)
-        self._gemm(B, N, 128, 128, L.PRO_BNRELU, L.EPI_DGRAD, ys["conv4"], h4, bufA, pa=pc4.scale,
-                   pb=pc4.shift, Yp=ys["conv4"], es=pc4.scale, et=pc4.shift, emean=pc4.mean,
-                   erstd=pc4.rstd, addend=pbuf, stats=st, tag="dgrad2:conv5")
+        self._gemm(B, N, 1024 + 128, 128, L.PRO_CAT, L.EPI_DGRAD, dz5, ws_t, bufA, K1=1024, A2=ys["conv4"],
+                   W2=h4, pa=pc4.scale, pb=pc4.shift, bias=c5, Yp=ys["conv4"], es=pc4.scale, et=pc4.shift,
+                   emean=pc4.mean, erstd=pc4.rstd, stats=st, tag="dgrad:conv5")
         g4, s4, ws4 = sv.gram4 if sv.gram4 is not None else \
             self._gram(ys["conv4"], pc4.scale, pc4.shift, B, N, 128, tag="gram:conv4")
         self._launch("wgrad_asm:conv5", "pcs_gram_wgrad", L.ptr(g4), L.ptr(s4), L.ptr(W5_r), 128, L.ptr(be5),
                      L.ptr(ga5), None, None, None, None, None, B, 1024, 128, self.dt, L.ptr(r5), L.ptr(al5),
                      L.ptr(G("conv5.weight")), 128, s)
-        keepalive.append((ws_t, c5, h4, pbuf, r5, g4, s4, ws4, W5_r))
+        keepalive.append((ws_t, c5, h4, r5, g4, s4, ws4, W5_r))
         bn_bwd("bn4", "conv4", st, cps4)
         dz4 = bufA
         st, cps = dgrad_wgrad("conv4", "bn4", 64, 128, dz4, ys["conv4"], "conv3", "bn3", bufB)
