@@ -563,6 +563,37 @@ int pcs_voxel_padded_index(const int64_t *voxel_of_point, int64_t T, const int64
 int pcs_gather_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t n, int32_t C,
                     float *dst, pcs_stream_t stream);
 
+/*
+ * Dense 3-D convolution on channels-last voxel grids (the north star's 3x3x3 Conv3d
+ * U-Net with LDS-staged stencils and transposed convolutions; build-defined, the reference has no
+ * voxel grid: parity is against torch conv3d / conv_transpose3d in fp64, not the reference).
+ * X [B, Di, Hi, Wi, Cin] bf16, W [Cout, k, k, k, Cin] bf16 (torch Conv3d weight permuted
+ * (0, 2, 3, 4, 1); ConvTranspose3d weight permuted (1, 2, 3, 4, 0)), bias [Cout] f32 or NULL,
+ * Y [B, Do, Ho, Wo, Cout] in ydtype (PCS_F32 | PCS_BF16), fp32 accumulation:
+ *   transposed = 0:  Y[o] = b + sum_t W_t X[o s - p + t]                  Do = (Di + 2p - k) / s + 1
+ *   transposed = 1:  Y[o] = b + sum_t W_t X[(o + p - t) / s] (exact only)  Do = (Di - 1) s - 2p + k
+ * k in 1..3, s in {1, 2}, 0 <= p < k.  pcs_conv3d: Cin % 32 == 0, Cout % 64 == 0.  The input
+ * gradient of either form is the other form applied to dY with pcs_conv3d_weight_t(W) and the
+ * grids swapped.  pcs_conv3d_wgrad: dW [Cout, k, k, k, Cin] f32 = sum_o dY[o] (x) X[in(o, t)]
+ * over the forward's index map, db [Cout] f32 = sum_o dY[o] (may be NULL); Cin, Cout % 64 == 0;
+ * fp32 partials summed in a fixed order (deterministic).
+ */
+typedef struct {
+  int64_t B;
+  int32_t Di, Hi, Wi;   /* input grid */
+  int32_t Do, Ho, Wo;   /* output grid */
+  int32_t Cin, Cout;
+  int32_t k, s, p;      /* cubic kernel, stride, padding */
+  int32_t transposed;
+} pcs_conv3d_geom;
+int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W, const float *bias, void *Y,
+               int32_t ydtype, pcs_stream_t stream);
+int64_t pcs_conv3d_wgrad_workspace(const pcs_conv3d_geom *g);   /* bytes */
+int pcs_conv3d_wgrad(const pcs_conv3d_geom *g, const void *X, const void *dY, void *workspace,
+                     int64_t workspace_bytes, float *dW, float *db, pcs_stream_t stream);
+/* W [Cout][taps][Cin] -> Wt [Cin][taps][Cout] (bf16) */
+int pcs_conv3d_weight_t(const void *W, int32_t Cout, int32_t taps, int32_t Cin, void *Wt, pcs_stream_t stream);
+
 /* Build-time identification and error string. */
 int pcs_abi_version(void);
 const char *pcs_last_error(void);

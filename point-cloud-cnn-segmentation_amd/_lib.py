@@ -62,6 +62,13 @@ class WgradArgs(ct.Structure):
     ]
 
 
+class Conv3dGeom(ct.Structure):
+    _fields_ = [
+        ("B", _i64), ("Di", _i32), ("Hi", _i32), ("Wi", _i32), ("Do", _i32), ("Ho", _i32), ("Wo", _i32),
+        ("Cin", _i32), ("Cout", _i32), ("k", _i32), ("s", _i32), ("p", _i32), ("transposed", _i32),
+    ]
+
+
 class PoolBwdArgs(ct.Structure):
     _fields_ = [
         ("num_scenes", _i64), ("scene_rows", _i64),
@@ -118,6 +125,10 @@ SIGNATURES = [
     ("pcs_bnrelu_bwd", ct.c_int, [_vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32,
                                   _i32, _i64, _vp, _vp]),
     ("pcs_abi_version", ct.c_int, []),
+    ("pcs_conv3d", ct.c_int, [ct.POINTER(Conv3dGeom), _vp, _vp, _vp, _vp, _i32, _vp]),
+    ("pcs_conv3d_wgrad_workspace", _i64, [ct.POINTER(Conv3dGeom)]),
+    ("pcs_conv3d_wgrad", ct.c_int, [ct.POINTER(Conv3dGeom), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    ("pcs_conv3d_weight_t", ct.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
     ("pcs_gram_workspace", _i64, [_i64, _i64, _i32, _i32, ct.POINTER(_i32)]),
     ("pcs_gram", ct.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     ("pcs_pool_rows_add", ct.c_int, [_vp, _i32, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i32,

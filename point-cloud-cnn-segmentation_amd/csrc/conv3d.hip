@@ -1,0 +1,450 @@
+// Dense 3-D convolution on channels-last voxel grids: the north star's "3x3x3 Conv3d U-Net with
+// LDS-staged stencils, transposed conv" building blocks.  Build-defined: the
+// reference (P) has no voxel grid, so parity is against torch.nn.functional.conv3d /
+// conv_transpose3d in fp64 (tests/test_gpu_conv3d.py), not against the reference.
+//
+// Layouts: X [B, D, H, W, C] bf16 (channels innermost), W [Cout, k, k, k, Cin] bf16 (one row of
+// taps x input channels per output channel), Y [B, D', H', W', Cout] f32 or bf16.
+//   conv       Y[o] = b + sum_t W_t X[o s - p + t]
+//   transposed Y[o] = b + sum_t W_t X[(o + p - t) / s]   (only where o + p - t is a multiple of s)
+// The input gradient of one is the other with W_t transposed (pcs_conv3d_weight_t), so one
+// kernel serves the forward and the input gradient of both; the weight gradient uses the
+// forward's index map.
+//
+// conv3d_kernel: implicit GEMM, rows = output voxels, columns = output channels, k = (tap,
+// 32-channel slice).  A k-step gathers the 64 rows' input voxels of one tap into LDS (zero rows
+// off the grid or off the stride lattice): the 27-tap stencil is 27 shifted gathers of the same
+// channels-last rows, so after the first tap the re-reads come from L2.  The next k-step is
+// loaded into registers while the MFMAs of this one run; one barrier per k-step.
+// conv3d_wgrad_kernel: dW_t = dY^T X_t over output voxels in 32-voxel k-steps, both operands
+// staged transposed ([channel][voxel]) so the MFMA's k runs over voxels; split over voxel
+// slices with fp32 partials summed in a fixed order (deterministic).
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 256;
+constexpr int BM = 64, BN = 64, KS = 32;   // output tile (voxels x channels), k-step (bf16 elements)
+constexpr int ROWB = KS * 2;               // 64 B per LDS operand row
+
+// 16-B slot swizzle of a 64-B LDS row: conflict-free ds_read_b128 fragment reads (rows 4 apart
+// land on different slots of a 256-B bank row)
+PCS_DEV int cswz(int row, int slot) { return slot ^ ((-(row >> 2)) & 3); }
+
+// input voxel feeding output voxel (b, z, y, x) through tap (dz, dy, dx); -1 = none (zero)
+PCS_DEV int64_t in_voxel(const pcs_conv3d_geom &g, int b, int z, int y, int x, int dz, int dy, int dx) {
+  int iz, iy, ix;
+  if (!g.transposed) {
+    iz = z * g.s - g.p + dz;
+    iy = y * g.s - g.p + dy;
+    ix = x * g.s - g.p + dx;
+  } else {
+    const int tz = z + g.p - dz, ty = y + g.p - dy, tx = x + g.p - dx;
+    if (tz < 0 || ty < 0 || tx < 0) return -1;
+    if (g.s == 2 && ((tz | ty | tx) & 1)) return -1;
+    const int sh = g.s == 2 ? 1 : 0;
+    iz = tz >> sh;
+    iy = ty >> sh;
+    ix = tx >> sh;
+  }
+  if (iz < 0 || iy < 0 || ix < 0 || iz >= g.Di || iy >= g.Hi || ix >= g.Wi) return -1;
+  return (((int64_t)b * g.Di + iz) * g.Hi + iy) * g.Wi + ix;
+}
+
+PCS_DEV void decode(const pcs_conv3d_geom &g, int64_t u, int &b, int &z, int &y, int &x) {
+  x = (int)(u % g.Wo);
+  u /= g.Wo;
+  y = (int)(u % g.Ho);
+  u /= g.Ho;
+  z = (int)(u % g.Do);
+  b = (int)(u / g.Do);
+}
+
+// Transposed form with stride 2: an output voxel o only meets the taps t with o + p - t even, so
+// the outputs fall into 8 parity classes c (o = 2 o' + c per dimension), each with its own tap
+// subset (t = (c + p) mod 2, + 2, ... < k: one tap per dimension for k = 2).  Tiles are cut per
+// class, so no MFMA runs on a tap that is off the lattice for every row.
+struct PClass {
+  int cz, cy, cx;   // parity of the class
+  int nz, ny, nx;   // class sub-grid (output voxels 2 o' + c inside the grid)
+  int tz0, ty0, tx0, ntz, nty, ntx;   // first tap and tap count per dimension
+};
+
+PCS_DEV PClass pclass(const pcs_conv3d_geom &g, int c) {
+  PClass q;
+  q.cz = (c >> 2) & 1; q.cy = (c >> 1) & 1; q.cx = c & 1;
+  q.nz = (g.Do - q.cz + 1) >> 1; q.ny = (g.Ho - q.cy + 1) >> 1; q.nx = (g.Wo - q.cx + 1) >> 1;
+  q.tz0 = (q.cz + g.p) & 1; q.ty0 = (q.cy + g.p) & 1; q.tx0 = (q.cx + g.p) & 1;
+  q.ntz = q.tz0 < g.k ? (g.k - q.tz0 + 1) >> 1 : 0;
+  q.nty = q.ty0 < g.k ? (g.k - q.ty0 + 1) >> 1 : 0;
+  q.ntx = q.tx0 < g.k ? (g.k - q.tx0 + 1) >> 1 : 0;
+  return q;
+}
+
+// class row u (b, z', y', x' over the class sub-grid) -> output voxel (b, z, y, x)
+PCS_DEV void decode_class(const PClass &q, int64_t u, int &b, int &z, int &y, int &x) {
+  x = 2 * (int)(u % q.nx) + q.cx;
+  u /= q.nx;
+  y = 2 * (int)(u % q.ny) + q.cy;
+  u /= q.ny;
+  z = 2 * (int)(u % q.nz) + q.cz;
+  b = (int)(u / q.nz);
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
+                                                         const bf16_t *__restrict__ W, const float *__restrict__ bias,
+                                                         void *__restrict__ Y, int64_t M) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2 * BM * ROWB];   // per buffer: A | B, 4 KB each
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  // class mode (transposed, stride 2): blockIdx.x = tile * 8 + class, rows index the class sub-grid
+  const bool cm = g.transposed && g.s == 2;
+  PClass pc{};
+  int64_t Mrows = M;
+  int64_t m0 = (int64_t)blockIdx.x * BM;
+  if (cm) {
+    pc = pclass(g, blockIdx.x & 7);
+    Mrows = g.B * pc.nz * pc.ny * pc.nx;
+    m0 = (int64_t)(blockIdx.x >> 3) * BM;
+    if (m0 >= Mrows) return;   // uniform: this class has fewer tiles than the largest
+  }
+  const int n0 = blockIdx.y * BN;
+  const int srow = tid >> 2, q = tid & 3;   // staging: one 16-B chunk of one row of A and of B
+  const int64_t u = m0 + srow;
+  const bool rvalid = u < Mrows;
+  int b = 0, z = 0, y = 0, x = 0;
+  if (rvalid) {
+    if (cm) decode_class(pc, u, b, z, y, x);
+    else decode(g, u, b, z, y, x);
+  }
+  const int k = g.k, taps = k * k * k, cps = g.Cin / KS;
+  const int ctaps = cm ? pc.ntz * pc.nty * pc.ntx : taps;   // taps this tile runs
+  const int nks = ctaps * cps;
+  const bf16_t *wrow = W + (int64_t)(n0 + srow) * taps * g.Cin + q * 8;
+
+  u32x4 ra, rb;
+  auto load = [&](int ks) {
+    const int j = ks / cps, c0 = (ks - j * cps) * KS;
+    int dz, dy, dx;
+    if (cm) {
+      dz = pc.tz0 + 2 * (j / (pc.nty * pc.ntx));
+      dy = pc.ty0 + 2 * ((j / pc.ntx) % pc.nty);
+      dx = pc.tx0 + 2 * (j % pc.ntx);
+    } else {
+      dz = j / (k * k); dy = (j / k) % k; dx = j % k;
+    }
+    const int t = (dz * k + dy) * k + dx;
+    const int64_t iv = rvalid ? in_voxel(g, b, z, y, x, dz, dy, dx) : -1;
+    ra = iv >= 0 ? *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + c0 + q * 8) : mk_u32x4(0, 0, 0, 0);
+    rb = *reinterpret_cast<const u32x4 *>(wrow + (int64_t)t * g.Cin + c0);
+  };
+  auto stage = [&](int buf) {
+    char *tA = lds[buf], *tB = lds[buf] + BM * ROWB;
+    *reinterpret_cast<u32x4 *>(tA + srow * ROWB + cswz(srow, q) * 16) = ra;
+    *reinterpret_cast<u32x4 *>(tB + srow * ROWB + cswz(srow, q) * 16) = rb;
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nks > 0) {
+    load(0);
+    stage(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nks) load(ks + 1);
+    const char *tA = lds[buf], *tB = lds[buf] + BM * ROWB;
+    bf16x8 af[2], bw[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wr * 32 + i * 16 + lr;
+      af[i] = *reinterpret_cast<const bf16x8 *>(tA + r * ROWB + cswz(r, lg) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wc * 32 + j * 16 + lr;
+      bw[j] = *reinterpret_cast<const bf16x8 *>(tB + r * ROWB + cswz(r, lg) * 16);
+    }
+    // W rows as the MFMA A operand: each lane ends with 4 consecutive output channels of one voxel
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+    if (ks + 1 < nks) stage(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int64_t uo = m0 + wr * 32 + i * 16 + lr;
+    if (uo >= Mrows) continue;
+    if (cm) {   // class row -> output voxel
+      int ob, oz, oy, ox;
+      decode_class(pc, uo, ob, oz, oy, ox);
+      uo = (((int64_t)ob * g.Do + oz) * g.Ho + oy) * g.Wo + ox;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = n0 + wc * 32 + j * 16 + 4 * lg;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        const float4 bb = *reinterpret_cast<const float4 *>(bias + co);
+        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      }
+      if constexpr (OUT_BF16) {
+        *reinterpret_cast<uint2 *>(reinterpret_cast<bf16_t *>(Y) + uo * g.Cout + co) =
+            make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      } else {
+        *reinterpret_cast<float4 *>(reinterpret_cast<float *>(Y) + uo * g.Cout + co) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+// ---- weight gradient: dW[co][t][ci] = sum_o dY[o][co] X[in(o, t)][ci], one (co, ci) 64x64 tile
+// of one tap per workgroup and voxel slice; operands staged as [channel][32 voxels] rows
+constexpr int WV = 32;   // voxels per k-step
+
+__global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
+                                                               const bf16_t *__restrict__ dY, float *__restrict__ ws,
+                                                               int64_t M, int64_t vps) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 64 * ROWB];   // dY^T | X^T, [64 ch][32 voxels]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int nco = g.Cout / 64;
+  const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
+  const int t = blockIdx.y, split = blockIdx.z;
+  const int k = g.k, taps = k * k * k;
+  const int dz = t / (k * k), dy = (t / k) % k, dx = t % k;
+  // transposed, stride 2: tap t only meets the output voxels of parity class (t + p) mod 2, so
+  // the slices run over that class's sub-grid
+  const bool cm = g.transposed && g.s == 2;
+  PClass pc{};
+  int64_t Mv = M, vs = vps;
+  if (cm) {
+    pc = pclass(g, (((dz + g.p) & 1) << 2) | (((dy + g.p) & 1) << 1) | ((dx + g.p) & 1));
+    Mv = g.B * pc.nz * pc.ny * pc.nx;
+    vs = ((Mv + gridDim.z - 1) / gridDim.z + WV - 1) / WV * WV;
+  }
+  const int64_t lo = (int64_t)split * vs, hi = pcs_min64(lo + vs, Mv);
+  const int sv = tid >> 3, q8 = tid & 7;   // staging: voxel row sv, 8 channels 8*q8 ..
+  char *tD = lds, *tX = lds + 64 * ROWB;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t v0 = lo; v0 < hi; v0 += WV) {
+    const int64_t u = v0 + sv;
+    u32x4 rd = mk_u32x4(0, 0, 0, 0), rx = mk_u32x4(0, 0, 0, 0);
+    if (u < hi) {
+      int b, z, y, x;
+      int64_t uo = u;
+      if (cm) {
+        decode_class(pc, u, b, z, y, x);
+        uo = (((int64_t)b * g.Do + z) * g.Ho + y) * g.Wo + x;
+      } else {
+        decode(g, u, b, z, y, x);
+      }
+      rd = *reinterpret_cast<const u32x4 *>(dY + uo * g.Cout + co0 + q8 * 8);
+      const int64_t iv = in_voxel(g, b, z, y, x, dz, dy, dx);
+      if (iv >= 0) rx = *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + ci0 + q8 * 8);
+    }
+    __syncthreads();   // the previous k-step's fragments have been read
+    // transposed stores: element (channel c, voxel sv) at row c, slot sv / 8, position sv % 8
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = q8 * 8 + e;
+      const int off = c * ROWB + cswz(c, sv >> 3) * 16 + (sv & 7) * 2;
+      const uint32_t wd = rd[e >> 1], wx = rx[e >> 1];
+      *reinterpret_cast<bf16_t *>(tD + off) = (bf16_t)((e & 1) ? wd >> 16 : wd & 0xffffu);
+      *reinterpret_cast<bf16_t *>(tX + off) = (bf16_t)((e & 1) ? wx >> 16 : wx & 0xffffu);
+    }
+    __syncthreads();
+    bf16x8 fd[2], fx[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wr * 32 + i * 16 + lr;
+      fd[i] = *reinterpret_cast<const bf16x8 *>(tD + r * ROWB + cswz(r, lg) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wc * 32 + j * 16 + lr;
+      fx[j] = *reinterpret_cast<const bf16x8 *>(tX + r * ROWB + cswz(r, lg) * 16);
+    }
+    // lane: dW rows co = 4 lg + v of tile i, column ci = lr of tile j
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
+  }
+  float *out = ws + (int64_t)split * g.Cout * taps * g.Cin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = ci0 + wc * 32 + j * 16 + lr;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+        out[((int64_t)co * taps + t) * g.Cin + ci] = acc[i][j][v];
+      }
+    }
+}
+
+// db partials: column sums of dY over one voxel slice, [split][Cout]
+__global__ __launch_bounds__(THREADS) void conv3d_bgrad_kernel(const bf16_t *__restrict__ dY, int Cout, int64_t M,
+                                                               int64_t vps, float *__restrict__ wsb) {
+  __shared__ float red[THREADS];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), r0 = threadIdx.x >> 6;
+  const int64_t lo = (int64_t)blockIdx.y * vps, hi = pcs_min64(lo + vps, M);
+  float s = 0.f;
+  for (int64_t u = lo + r0; u < hi; u += 4) s += bf2f(dY[u * Cout + c]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < 64)
+    wsb[(int64_t)blockIdx.y * Cout + c] = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
+}
+
+// out[i] = sum_s part[s * len + i], fixed order
+__global__ __launch_bounds__(256) void conv3d_reduce_kernel(const float *__restrict__ part, int64_t nsl, int64_t len,
+                                                            float *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  float s = 0.f;
+  for (int64_t sl = 0; sl < nsl; ++sl) s += part[sl * len + i];
+  out[i] = s;
+}
+
+__global__ __launch_bounds__(256) void conv3d_weight_t_kernel(const bf16_t *__restrict__ W, int Cout, int taps, int Cin,
+                                                              bf16_t *__restrict__ Wt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // index into Wt [Cin][taps][Cout]
+  const int64_t n = (int64_t)Cout * taps * Cin;
+  if (i >= n) return;
+  const int co = (int)(i % Cout);
+  const int64_t r = i / Cout;
+  const int t = (int)(r % taps), ci = (int)(r / taps);
+  Wt[i] = W[((int64_t)co * taps + t) * Cin + ci];
+}
+
+bool geom_ok(const pcs_conv3d_geom *g, const char **why) {
+  if (!g) { *why = "null geometry"; return false; }
+  if (g->B <= 0 || g->Di <= 0 || g->Hi <= 0 || g->Wi <= 0 || g->Do <= 0 || g->Ho <= 0 || g->Wo <= 0) {
+    *why = "empty grid";
+    return false;
+  }
+  if (g->k < 1 || g->k > 3 || (g->s != 1 && g->s != 2) || g->p < 0 || g->p >= g->k || (g->transposed != 0 && g->transposed != 1)) {
+    *why = "k in 1..3, s in {1, 2}, 0 <= p < k, transposed 0 or 1";
+    return false;
+  }
+  const int din[3] = {g->Di, g->Hi, g->Wi}, dout[3] = {g->Do, g->Ho, g->Wo};
+  for (int d = 0; d < 3; ++d) {
+    const int expect = g->transposed ? (din[d] - 1) * g->s - 2 * g->p + g->k : (din[d] + 2 * g->p - g->k) / g->s + 1;
+    if (dout[d] != expect || (!g->transposed && din[d] + 2 * g->p < g->k)) {
+      *why = "output grid must be (in + 2p - k)/s + 1 (conv) or (in - 1)s - 2p + k (transposed)";
+      return false;
+    }
+  }
+  if (g->B * g->Di * g->Hi * g->Wi >= ((int64_t)1 << 40) || g->B * g->Do * g->Ho * g->Wo >= ((int64_t)1 << 40)) {
+    *why = "grid too large";
+    return false;
+  }
+  return true;
+}
+
+int64_t out_voxels(const pcs_conv3d_geom &g) { return g.B * g.Do * g.Ho * g.Wo; }
+
+int64_t wgrad_splits(const pcs_conv3d_geom &g) {
+  const int64_t M = out_voxels(g);
+  const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * g.k * g.k * g.k;
+  int64_t sp = (2048 + tiles - 1) / tiles;
+  const int64_t maxsp = (M + 4 * WV - 1) / (4 * WV);   // at least 4 k-steps per slice
+  if (sp > maxsp) sp = maxsp;
+  return sp < 1 ? 1 : sp;
+}
+
+int64_t wgrad_vps(const pcs_conv3d_geom &g, int64_t sp) {
+  const int64_t M = out_voxels(g);
+  return ((M + sp - 1) / sp + WV - 1) / WV * WV;
+}
+
+}  // namespace
+
+extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W, const float *bias, void *Y,
+                          int32_t ydtype, pcs_stream_t stream) {
+  const char *why = nullptr;
+  if (!geom_ok(g, &why)) return pcs_set_einval("pcs_conv3d", why);
+  if (!X || !W || !Y) return pcs_set_einval("pcs_conv3d", "X, W and Y are required");
+  if (g->Cin % KS != 0 || g->Cout % BN != 0 || g->Cin <= 0 || g->Cout <= 0)
+    return pcs_set_einval("pcs_conv3d", "Cin must be a multiple of 32 and Cout of 64");
+  if (ydtype != PCS_F32 && ydtype != PCS_BF16) return pcs_set_einval("pcs_conv3d", "Y dtype: PCS_F32 or PCS_BF16");
+  const int64_t M = out_voxels(*g);
+  // transposed stride 2: 8 parity classes, tiles of the largest class's sub-grid each
+  const int64_t rows = g->transposed && g->s == 2
+                           ? 8 * ((g->B * ((g->Do + 1) / 2) * ((g->Ho + 1) / 2) * ((g->Wo + 1) / 2) + BM - 1) / BM)
+                           : (M + BM - 1) / BM;
+  if (rows <= 0 || rows > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
+  const dim3 grid((unsigned)rows, (unsigned)(g->Cout / BN));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ydtype == PCS_BF16)
+    hipLaunchKernelGGL(conv3d_kernel<true>, grid, dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X),
+                       static_cast<const bf16_t *>(W), bias, Y, M);
+  else
+    hipLaunchKernelGGL(conv3d_kernel<false>, grid, dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X),
+                       static_cast<const bf16_t *>(W), bias, Y, M);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t pcs_conv3d_wgrad_workspace(const pcs_conv3d_geom *g) {
+  const char *why = nullptr;
+  if (!geom_ok(g, &why)) return pcs_set_einval("pcs_conv3d_wgrad_workspace", why);
+  if (g->Cin % 64 != 0 || g->Cout % 64 != 0 || g->Cin <= 0 || g->Cout <= 0)
+    return pcs_set_einval("pcs_conv3d_wgrad_workspace", "Cin and Cout must be multiples of 64");
+  const int64_t sp = wgrad_splits(*g);
+  return sp * ((int64_t)g->Cout * g->k * g->k * g->k * g->Cin + g->Cout) * 4;
+}
+
+extern "C" int pcs_conv3d_wgrad(const pcs_conv3d_geom *g, const void *X, const void *dY, void *workspace,
+                                int64_t workspace_bytes, float *dW, float *db, pcs_stream_t stream) {
+  const int64_t need = pcs_conv3d_wgrad_workspace(g);
+  if (need < 0) return (int)need;
+  if (!X || !dY || !dW || !workspace || workspace_bytes < need)
+    return pcs_set_einval("pcs_conv3d_wgrad", "X, dY, dW and a pcs_conv3d_wgrad_workspace-sized workspace are required");
+  const int64_t M = out_voxels(*g), sp = wgrad_splits(*g), vps = wgrad_vps(*g, sp);
+  const int taps = g->k * g->k * g->k;
+  const int64_t wlen = (int64_t)g->Cout * taps * g->Cin;
+  float *ws = static_cast<float *>(workspace), *wsb = ws + sp * wlen;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(conv3d_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), (unsigned)taps, (unsigned)sp),
+                     dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, M, vps);
+  PCS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((wlen + 255) / 256)), dim3(256), 0, s, ws, sp, wlen, dW);
+  PCS_CHECK_LAUNCH();
+  if (db) {
+    hipLaunchKernelGGL(conv3d_bgrad_kernel, dim3((unsigned)(g->Cout / 64), (unsigned)sp), dim3(THREADS), 0, s,
+                       static_cast<const bf16_t *>(dY), g->Cout, M, vps, wsb);
+    PCS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((g->Cout + 255) / 256)), dim3(256), 0, s, wsb, sp,
+                       (int64_t)g->Cout, db);
+    PCS_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int pcs_conv3d_weight_t(const void *W, int32_t Cout, int32_t taps, int32_t Cin, void *Wt, pcs_stream_t stream) {
+  if (!W || !Wt || Cout <= 0 || taps <= 0 || taps > 27 || Cin <= 0)
+    return pcs_set_einval("pcs_conv3d_weight_t", "bad arguments (0 < taps <= 27)");
+  const int64_t n = (int64_t)Cout * taps * Cin;
+  hipLaunchKernelGGL(conv3d_weight_t_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), static_cast<const bf16_t *>(W), Cout, taps, Cin,
+                     static_cast<bf16_t *>(Wt));
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

@@ -15,6 +15,7 @@ semantics are build-defined ("not reference parity").
 """
 from __future__ import annotations
 
+import ctypes as ct
 from dataclasses import dataclass
 
 import torch
@@ -94,3 +95,134 @@ def to_points(voxel_logits: torch.Tensor, vb: VoxelBatch) -> torch.Tensor:
     out = torch.empty(T, C, dtype=torch.float32, device=out_dev)
     L.call("pcs_gather_rows", L.ptr(src), src.stride(0), L.ptr(idx), T, C, L.ptr(out), L.stream_ptr(out_dev))
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Dense 3-D convolutions on channels-last voxel grids (pcs_conv3d*, csrc/conv3d.hip): the north
+# star's U-Net building blocks -- the 3x3x3 stencil (k=3, s=1, p=1), the 2x2x2 stride-2
+# downsampling and its transposed upsampling.  Build-defined like the rest of this module: the
+# reference has no voxel grid, parity is against torch's conv3d / conv_transpose3d (fp64).
+# Activations are [B, D, H, W, C] bf16 (channels innermost); parameters keep torch's layouts
+# (Conv3d [Cout, Cin, k, k, k], ConvTranspose3d [Cin, Cout, k, k, k]) in fp32, cast to bf16 per
+# call by pcs_cast_weight.
+# ---------------------------------------------------------------------------------------------
+
+def _out_size(d, k, s, p, transposed):
+    return (d - 1) * s - 2 * p + k if transposed else (d + 2 * p - k) // s + 1
+
+
+def _geom(B, grid_in, cin, cout, k, s, p, transposed):
+    out = [_out_size(d, k, s, p, transposed) for d in grid_in]
+    if min(out) <= 0:
+        raise ValueError(f"empty output grid {out} for input {list(grid_in)}, k={k}, s={s}, p={p}")
+    return L.Conv3dGeom(B=B, Di=grid_in[0], Hi=grid_in[1], Wi=grid_in[2], Do=out[0], Ho=out[1], Wo=out[2],
+                        Cin=cin, Cout=cout, k=k, s=s, p=p, transposed=int(transposed))
+
+
+def _bf16_2d(t, rows, cols):
+    """bf16 copy of a [rows, cols] tensor on the device (pcs_cast_weight for fp32 input)."""
+    t = t.contiguous()
+    if t.dtype == torch.bfloat16:
+        return t
+    out = torch.empty(rows, cols, dtype=torch.bfloat16, device=t.device)
+    L.call("pcs_cast_weight", L.ptr(t.float()), rows, cols, cols, L.BF16, L.ptr(out), None, L.stream_ptr(t.device))
+    return out
+
+
+class _Conv3dFn(torch.autograd.Function):
+    """y = conv(x, w) + b with w in kernel layout [Cout, taps * Cin] (fp32 master)."""
+
+    @staticmethod
+    def forward(ctx, x, wk, bias, k, s, p, transposed, out_dtype):
+        if not x.is_cuda:
+            raise RuntimeError("pcs_amd conv3d runs on a HIP device only (no CPU fallback)")
+        if x.dtype != torch.bfloat16 or x.dim() != 5:
+            raise ValueError("x must be a bf16 [B, D, H, W, C] channels-last voxel grid")
+        x = x.contiguous()
+        B, D, H, W, cin = x.shape
+        cout = wk.shape[0]
+        g = _geom(B, (D, H, W), cin, cout, k, s, p, transposed)
+        wb = _bf16_2d(wk, cout, wk.shape[1])
+        y = torch.empty(B, g.Do, g.Ho, g.Wo, cout, dtype=out_dtype, device=x.device)
+        L.call("pcs_conv3d", ct.byref(g), L.ptr(x), L.ptr(wb),
+               L.ptr(bias.float().contiguous()) if bias is not None else None, L.ptr(y),
+               L.BF16 if out_dtype == torch.bfloat16 else L.F32, L.stream_ptr(x.device))
+        ctx.save_for_backward(x, wb)
+        ctx.cfg = (k, s, p, transposed, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        k, s, p, transposed, has_bias = ctx.cfg
+        B, D, H, W, cin = x.shape
+        cout = wb.shape[0]
+        taps = k ** 3
+        g = _geom(B, (D, H, W), cin, cout, k, s, p, transposed)
+        M = B * g.Do * g.Ho * g.Wo
+        dyb = _bf16_2d(dy.reshape(M, cout), M, cout)
+        dev, st = x.device, L.stream_ptr(x.device)
+        dx = dwk = db = None
+        if ctx.needs_input_grad[0]:
+            # the input gradient of a convolution is the transposed convolution of dy with W_t^T
+            # (and vice versa): same k, s, p, grids swapped
+            wt = torch.empty(cin, taps * cout, dtype=torch.bfloat16, device=dev)
+            L.call("pcs_conv3d_weight_t", L.ptr(wb), cout, taps, cin, L.ptr(wt), st)
+            gb = _geom(B, (g.Do, g.Ho, g.Wo), cout, cin, k, s, p, not transposed)
+            if (gb.Do, gb.Ho, gb.Wo) != (D, H, W):
+                raise ValueError("input gradient: the strided output grid does not map back onto the input grid")
+            dx = torch.empty_like(x)
+            L.call("pcs_conv3d", ct.byref(gb), L.ptr(dyb), L.ptr(wt), None, L.ptr(dx), L.BF16, st)
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            nbytes = L.load().pcs_conv3d_wgrad_workspace(ct.byref(g))
+            if nbytes < 0:
+                raise L.PcsError(L.load().pcs_last_error().decode())
+            ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            dwk = torch.empty(cout, taps * cin, dtype=torch.float32, device=dev)
+            db = torch.empty(cout, dtype=torch.float32, device=dev) if has_bias else None
+            L.call("pcs_conv3d_wgrad", ct.byref(g), L.ptr(x), L.ptr(dyb), L.ptr(ws), nbytes, L.ptr(dwk), L.ptr(db), st)
+        return dx, dwk, db, None, None, None, None, None
+
+
+def conv3d(x, weight, bias=None, stride=1, padding=0, out_dtype=torch.bfloat16):
+    """torch.nn.functional.conv3d on a channels-last bf16 grid x [B, D, H, W, Cin];
+    weight [Cout, Cin, k, k, k] (torch layout, fp32), bias [Cout] or None."""
+    cout, cin, k = weight.shape[0], weight.shape[1], weight.shape[2]
+    wk = weight.permute(0, 2, 3, 4, 1).reshape(cout, k ** 3 * cin)
+    return _Conv3dFn.apply(x, wk, bias, k, int(stride), int(padding), False, out_dtype)
+
+
+def conv_transpose3d(x, weight, bias=None, stride=2, padding=0, out_dtype=torch.bfloat16):
+    """torch.nn.functional.conv_transpose3d on a channels-last bf16 grid x [B, D, H, W, Cin];
+    weight [Cin, Cout, k, k, k] (torch layout, fp32), bias [Cout] or None."""
+    cin, cout, k = weight.shape[0], weight.shape[1], weight.shape[2]
+    wk = weight.permute(1, 2, 3, 4, 0).reshape(cout, k ** 3 * cin)
+    return _Conv3dFn.apply(x, wk, bias, k, int(stride), int(padding), True, out_dtype)
+
+
+class Conv3d(torch.nn.Module):
+    """nn.Conv3d(cin, cout, k, stride, padding) with torch's parameter layout and init, on
+    channels-last bf16 voxel grids (pcs_conv3d)."""
+
+    def __init__(self, cin, cout, kernel_size=3, stride=1, padding=1, bias=True):
+        super().__init__()
+        ref = torch.nn.Conv3d(cin, cout, kernel_size, stride, padding, bias=bias)
+        self.weight, self.bias = ref.weight, ref.bias
+        self.stride, self.padding = stride, padding
+
+    def forward(self, x, out_dtype=torch.bfloat16):
+        return conv3d(x, self.weight, self.bias, self.stride, self.padding, out_dtype)
+
+
+class ConvTranspose3d(torch.nn.Module):
+    """nn.ConvTranspose3d(cin, cout, k, stride, padding) with torch's parameter layout and init,
+    on channels-last bf16 voxel grids (pcs_conv3d, transposed form)."""
+
+    def __init__(self, cin, cout, kernel_size=2, stride=2, padding=0, bias=True):
+        super().__init__()
+        ref = torch.nn.ConvTranspose3d(cin, cout, kernel_size, stride, padding, bias=bias)
+        self.weight, self.bias = ref.weight, ref.bias
+        self.stride, self.padding = stride, padding
+
+    def forward(self, x, out_dtype=torch.bfloat16):
+        return conv_transpose3d(x, self.weight, self.bias, self.stride, self.padding, out_dtype)

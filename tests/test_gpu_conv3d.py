@@ -1,0 +1,140 @@
+"""Dense 3-D convolutions on channels-last voxel grids (csrc/conv3d.hip) against
+torch's conv3d / conv_transpose3d in fp64 on the same bf16-rounded operands, through the C ABI.
+
+Build-defined: the reference has no voxel grid, so this is not reference parity.  Products of
+bf16 operands are exact in fp32, so the forward and the fp32 weight gradients match fp64 to fp32
+summation error; the input gradient is stored in bf16.  Grids are ragged (odd, unequal sides)
+so the stencil's borders, the stride lattice and the partial last tiles are all exercised."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _ncdhw(x):            # [B, D, H, W, C] -> [B, C, D, H, W] fp64 on the host
+    return x.permute(0, 4, 1, 2, 3).double().cpu()
+
+
+def _rel(a, b):
+    return float((a.double().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+CASES = [
+    # (k, s, p, transposed, grid, cin, cout)
+    (3, 1, 1, False, (5, 6, 7), 64, 64),      # the U-Net stencil
+    (3, 1, 1, False, (4, 3, 9), 32, 128),     # Cin = one k-step
+    (2, 2, 0, False, (6, 4, 8), 64, 64),      # 2x2x2 stride-2 downsampling
+    (3, 2, 1, False, (7, 5, 7), 64, 64),      # strided stencil, odd grid
+    (2, 2, 0, True, (3, 2, 4), 64, 64),       # 2x2x2 stride-2 upsampling
+    (3, 1, 1, True, (4, 5, 3), 64, 64),       # transposed stencil (= flipped convolution)
+    (3, 2, 1, True, (3, 4, 2), 64, 128),      # strided transposed stencil
+    (3, 2, 1, True, (1, 4, 2), 64, 64),       # output depth 1: two parity classes are empty
+]
+
+
+def _operands(k, transposed, grid, cin, cout, B=2, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, *grid, cin, generator=g).to(torch.bfloat16)
+    shape = (cin, cout, k, k, k) if transposed else (cout, cin, k, k, k)
+    w = (torch.randn(*shape, generator=g) * 0.05).to(torch.bfloat16).float()   # bf16-exact fp32 master
+    b = torch.randn(cout, generator=g) * 0.1
+    return x, w, b
+
+
+def _ref(x, w, b, s, p, transposed):
+    f = F.conv_transpose3d if transposed else F.conv3d
+    return f(_ncdhw(x), w.double(), b.double(), stride=s, padding=p).permute(0, 2, 3, 4, 1)
+
+
+@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout", CASES)
+def test_forward_matches_torch(k, s, p, transposed, grid, cin, cout):
+    import pcs_amd.voxel as V
+    x, w, b = _operands(k, transposed, grid, cin, cout)
+    ref = _ref(x, w, b, s, p, transposed)
+    f = V.conv_transpose3d if transposed else V.conv3d
+    y = f(x.to(DEV), w.to(DEV), b.to(DEV), s, p, out_dtype=torch.float32)
+    yb = f(x.to(DEV), w.to(DEV), b.to(DEV), s, p, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == tuple(ref.shape)
+    assert _rel(y, ref) < 1e-5
+    assert _rel(yb.float(), ref) < 8e-3           # one bf16 rounding of the stored output
+
+
+@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout", CASES)
+def test_backward_matches_torch(k, s, p, transposed, grid, cin, cout):
+    import pcs_amd.voxel as V
+    if cin % 64:
+        pytest.skip("the weight gradient and the input gradient's GEMM need channels in multiples of 64")
+    x, w, b = _operands(k, transposed, grid, cin, cout, seed=1)
+    xr = _ncdhw(x).requires_grad_()
+    wr, br = w.double().requires_grad_(), b.double().requires_grad_()
+    f_ref = F.conv_transpose3d if transposed else F.conv3d
+    yr = f_ref(xr, wr, br, stride=s, padding=p)
+    g = torch.Generator().manual_seed(2)
+    dy = torch.randn(yr.shape, generator=g, dtype=torch.float64).to(torch.bfloat16).double()   # bf16-exact
+    yr.backward(dy)
+    xd = x.to(DEV).requires_grad_()
+    wd, bd = w.to(DEV).requires_grad_(), b.to(DEV).requires_grad_()
+    f = V.conv_transpose3d if transposed else V.conv3d
+    y = f(xd, wd, bd, s, p, out_dtype=torch.float32)
+    y.backward(dy.permute(0, 2, 3, 4, 1).float().to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(wd.grad, wr.grad) < 1e-5
+    assert _rel(bd.grad, br.grad) < 1e-5
+    assert _rel(xd.grad.float().permute(0, 4, 1, 2, 3), xr.grad) < 8e-3      # dx stored in bf16
+
+
+def test_wgrad_deterministic_and_validated():
+    import ctypes as ct
+    import pcs_amd._lib as L
+    import pcs_amd.voxel as V
+    x, w, _ = _operands(3, False, (9, 8, 7), 64, 64, B=3, seed=5)
+    g = V._geom(3, (9, 8, 7), 64, 64, 3, 1, 1, False)
+    dy = torch.randn(3, 9, 8, 7, 64).to(torch.bfloat16).to(DEV)
+    xd = x.to(DEV)
+    nb = L.load().pcs_conv3d_wgrad_workspace(ct.byref(g))
+    outs = []
+    for _ in range(2):
+        ws = torch.full((nb // 4,), float("nan"), device=DEV)
+        dw = torch.empty(64, 27 * 64, device=DEV)
+        db = torch.empty(64, device=DEV)
+        L.call("pcs_conv3d_wgrad", ct.byref(g), L.ptr(xd), L.ptr(dy), L.ptr(ws), nb, L.ptr(dw), L.ptr(db),
+               L.stream_ptr())
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = dy.double().reshape(-1, 64).sum(0).cpu()
+    assert _rel(outs[0][1], ref) < 1e-5
+    bad = V._geom(3, (9, 8, 7), 48, 64, 3, 1, 1, False)
+    with pytest.raises(L.PcsError):
+        L.call("pcs_conv3d_wgrad", ct.byref(bad), L.ptr(xd), L.ptr(dy), L.ptr(ws), nb, L.ptr(dw), None, L.stream_ptr())
+
+
+def test_unet_block_trains():
+    """A two-level channels-last U-Net block (stencil, 2x2x2 down, stencil, transposed up, skip
+    add, stencil) built from the modules: finite gradients and a falling loss over a few SGD steps."""
+    import pcs_amd.voxel as V
+    torch.manual_seed(0)
+    enc = V.Conv3d(64, 64).to(DEV)
+    down = V.Conv3d(64, 128, 2, 2, 0).to(DEV)
+    mid = V.Conv3d(128, 128).to(DEV)
+    up = V.ConvTranspose3d(128, 64, 2, 2, 0).to(DEV)
+    head = V.Conv3d(64, 64).to(DEV)
+    params = [p for m in (enc, down, mid, up, head) for p in m.parameters()]
+    opt = torch.optim.SGD(params, lr=0.05)
+    x = torch.randn(2, 8, 8, 8, 64, device=DEV).to(torch.bfloat16)
+    target = torch.randn(2, 8, 8, 8, 64, device=DEV) * 0.1
+    losses = []
+    for _ in range(8):
+        e = enc(x)
+        u = up(mid(down(e)))
+        y = head((e.float() + u.float()).to(torch.bfloat16), out_dtype=torch.float32)
+        loss = ((y - target) ** 2).mean()
+        opt.zero_grad()
+        loss.backward()
+        assert all(torch.isfinite(p.grad).all() for p in params)
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0]

@@ -74,3 +74,25 @@ def test_fused_dgrad_wgrad_validates_shapes_without_gpu():
     assert lib.pcs_dgrad_wgrad_workspace(ct.byref(a)) < 0
     a.Cout = 512
     assert lib.pcs_dgrad_wgrad_workspace(ct.byref(a)) == a.splits_per_scene * 512 * 64 * 4
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
+def test_conv3d_argument_validation_without_gpu():
+    """pcs_conv3d* reject bad geometries on the host, before any launch (no GPU needed)."""
+    import pcs_amd._lib as L
+    lib = L.load()
+
+    def geom(**kw):
+        d = dict(B=1, Di=8, Hi=8, Wi=8, Do=8, Ho=8, Wo=8, Cin=64, Cout=64, k=3, s=1, p=1, transposed=0)
+        d.update(kw)
+        return L.Conv3dGeom(**d)
+
+    ok = geom()
+    assert lib.pcs_conv3d_wgrad_workspace(ct.byref(ok)) > 0
+    for bad in (geom(Cin=48), geom(Cout=32), geom(Do=7), geom(k=4), geom(s=3), geom(p=3),
+                geom(transposed=1, Do=9)):
+        assert lib.pcs_conv3d(ct.byref(bad), 1, 1, None, 1, L.BF16, None) == -1000
+    assert lib.pcs_conv3d(ct.byref(ok), 1, 1, None, 1, L.F32 + 7, None) == -1000
+    assert lib.pcs_conv3d_wgrad_workspace(ct.byref(geom(Cin=32))) == -1000
+    up = geom(Di=4, Hi=4, Wi=4, k=2, s=2, p=0, transposed=1)     # 4^3 -> 8^3
+    assert lib.pcs_conv3d_wgrad_workspace(ct.byref(up)) > 0
