@@ -17,14 +17,14 @@
 // channels-last rows, so after the first tap the re-reads come from L2.  The next k-step is
 // loaded into registers while the MFMAs of this one run; one barrier per k-step.
 // conv3d_wgrad_kernel: dW_t = dY^T X_t over output voxels in 32-voxel k-steps, both operands
-// staged transposed ([channel][voxel]) so the MFMA's k runs over voxels; split over voxel
-// slices with fp32 partials summed in a fixed order (deterministic).
+// staged row-major and read transposed (ds_read_b64_tr_b16) so the MFMA's k runs over voxels;
+// split over voxel slices with fp32 partials summed in a fixed order (deterministic).
 #include "common.h"
 
 namespace {
 
 constexpr int THREADS = 256;
-constexpr int BM = 64, BN = 64, KS = 32;   // output tile (voxels x channels), k-step (bf16 elements)
+constexpr int BN = 64, KS = 32;   // output channels per tile, k-step (bf16 elements)
 constexpr int ROWB = KS * 2;               // 64 B per LDS operand row
 
 // 16-B slot swizzle of a 64-B LDS row: conflict-free ds_read_b128 fragment reads (rows 4 apart
@@ -51,7 +51,18 @@ PCS_DEV int64_t in_voxel(const pcs_conv3d_geom &g, int b, int z, int y, int x, i
   return (((int64_t)b * g.Di + iz) * g.Hi + iy) * g.Wi + ix;
 }
 
+// output voxel u -> (b, z, y, x); 32-bit divisions when u fits (a 64-bit division is ~10x dearer)
 PCS_DEV void decode(const pcs_conv3d_geom &g, int64_t u, int &b, int &z, int &y, int &x) {
+  if (u < ((int64_t)1 << 31)) {
+    uint32_t v = (uint32_t)u;
+    x = (int)(v % (uint32_t)g.Wo);
+    v /= (uint32_t)g.Wo;
+    y = (int)(v % (uint32_t)g.Ho);
+    v /= (uint32_t)g.Ho;
+    z = (int)(v % (uint32_t)g.Do);
+    b = (int)(v / (uint32_t)g.Do);
+    return;
+  }
   x = (int)(u % g.Wo);
   u /= g.Wo;
   y = (int)(u % g.Ho);
@@ -83,6 +94,16 @@ PCS_DEV PClass pclass(const pcs_conv3d_geom &g, int c) {
 
 // class row u (b, z', y', x' over the class sub-grid) -> output voxel (b, z, y, x)
 PCS_DEV void decode_class(const PClass &q, int64_t u, int &b, int &z, int &y, int &x) {
+  if (u < ((int64_t)1 << 31)) {
+    uint32_t v = (uint32_t)u;
+    x = 2 * (int)(v % (uint32_t)q.nx) + q.cx;
+    v /= (uint32_t)q.nx;
+    y = 2 * (int)(v % (uint32_t)q.ny) + q.cy;
+    v /= (uint32_t)q.ny;
+    z = 2 * (int)(v % (uint32_t)q.nz) + q.cz;
+    b = (int)(v / (uint32_t)q.nz);
+    return;
+  }
   x = 2 * (int)(u % q.nx) + q.cx;
   u /= q.nx;
   y = 2 * (int)(u % q.ny) + q.cy;
@@ -91,41 +112,56 @@ PCS_DEV void decode_class(const PClass &q, int64_t u, int &b, int &z, int &y, in
   b = (int)(u / q.nz);
 }
 
-template <bool OUT_BF16>
+// BMT = 64 or 128 output voxels per tile (4 waves as 2 x 2: wave tile BMT/2 x 32); KST = 32 or
+// 64 input channels per k-step (64: whole 128-B voxel rows per load, 2x the MFMAs per barrier)
+template <int BMT, int KST, bool OUT_BF16>
 __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                          const bf16_t *__restrict__ W, const float *__restrict__ bias,
                                                          void *__restrict__ Y, int64_t M) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2 * BM * ROWB];   // per buffer: A | B, 4 KB each
+  constexpr int RB = KST * 2;          // LDS row bytes
+  constexpr int CPR = KST / 8;         // 16-B chunks per row
+  constexpr int RPP = THREADS / CPR;   // rows staged per pass
+  constexpr int HA = BMT / RPP, HB = BN / RPP;
+  constexpr int TI = BMT / 32;         // 16-row MFMA tiles per wave
+  constexpr int KK = KST / 32;         // MFMA k-steps per k-step
+  __shared__ __attribute__((aligned(16))) char lds[2][(BMT + BN) * RB];   // per buffer: A | B
+  auto swzf = [](int row, int slot) { return KST == 32 ? cswz(row, slot) : (slot ^ ((row >> 1) & 7)); };
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
   // class mode (transposed, stride 2): blockIdx.x = tile * 8 + class, rows index the class sub-grid
   const bool cm = g.transposed && g.s == 2;
   PClass pc{};
   int64_t Mrows = M;
-  int64_t m0 = (int64_t)blockIdx.x * BM;
+  int64_t m0 = (int64_t)blockIdx.x * BMT;
   if (cm) {
     pc = pclass(g, blockIdx.x & 7);
     Mrows = g.B * pc.nz * pc.ny * pc.nx;
-    m0 = (int64_t)(blockIdx.x >> 3) * BM;
+    m0 = (int64_t)(blockIdx.x >> 3) * BMT;
     if (m0 >= Mrows) return;   // uniform: this class has fewer tiles than the largest
   }
   const int n0 = blockIdx.y * BN;
-  const int srow = tid >> 2, q = tid & 3;   // staging: one 16-B chunk of one row of A and of B
-  const int64_t u = m0 + srow;
-  const bool rvalid = u < Mrows;
-  int b = 0, z = 0, y = 0, x = 0;
-  if (rvalid) {
-    if (cm) decode_class(pc, u, b, z, y, x);
-    else decode(g, u, b, z, y, x);
+  const int srow = tid / CPR, q = tid % CPR;   // staging: chunk q of rows srow + RPP h
+  bool rv[HA];
+  int vb[HA], vz[HA], vy[HA], vx[HA];
+#pragma unroll
+  for (int h = 0; h < HA; ++h) {
+    const int64_t u = m0 + srow + RPP * h;
+    rv[h] = u < Mrows;
+    vb[h] = vz[h] = vy[h] = vx[h] = 0;
+    if (rv[h]) {
+      if (cm) decode_class(pc, u, vb[h], vz[h], vy[h], vx[h]);
+      else decode(g, u, vb[h], vz[h], vy[h], vx[h]);
+    }
   }
-  const int k = g.k, taps = k * k * k, cps = g.Cin / KS;
+  const int k = g.k, taps = k * k * k, cps = g.Cin / KST;
   const int ctaps = cm ? pc.ntz * pc.nty * pc.ntx : taps;   // taps this tile runs
   const int nks = ctaps * cps;
   const bf16_t *wrow = W + (int64_t)(n0 + srow) * taps * g.Cin + q * 8;
+  const int64_t wstep = (int64_t)RPP * taps * g.Cin;
 
-  u32x4 ra, rb;
+  u32x4 ra[HA], rb[HB];
   auto load = [&](int ks) {
-    const int j = ks / cps, c0 = (ks - j * cps) * KS;
+    const int j = ks / cps, c0 = (ks - j * cps) * KST;
     int dz, dy, dx;
     if (cm) {
       dz = pc.tz0 + 2 * (j / (pc.nty * pc.ntx));
@@ -135,19 +171,31 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
       dz = j / (k * k); dy = (j / k) % k; dx = j % k;
     }
     const int t = (dz * k + dy) * k + dx;
-    const int64_t iv = rvalid ? in_voxel(g, b, z, y, x, dz, dy, dx) : -1;
-    ra = iv >= 0 ? *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + c0 + q * 8) : mk_u32x4(0, 0, 0, 0);
-    rb = *reinterpret_cast<const u32x4 *>(wrow + (int64_t)t * g.Cin + c0);
+#pragma unroll
+    for (int h = 0; h < HA; ++h) {
+      const int64_t iv = rv[h] ? in_voxel(g, vb[h], vz[h], vy[h], vx[h], dz, dy, dx) : -1;
+      ra[h] = iv >= 0 ? *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + c0 + q * 8) : mk_u32x4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) rb[h] = *reinterpret_cast<const u32x4 *>(wrow + h * wstep + (int64_t)t * g.Cin + c0);
   };
   auto stage = [&](int buf) {
-    char *tA = lds[buf], *tB = lds[buf] + BM * ROWB;
-    *reinterpret_cast<u32x4 *>(tA + srow * ROWB + cswz(srow, q) * 16) = ra;
-    *reinterpret_cast<u32x4 *>(tB + srow * ROWB + cswz(srow, q) * 16) = rb;
+    char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
+#pragma unroll
+    for (int h = 0; h < HA; ++h) {
+      const int r = srow + RPP * h;
+      *reinterpret_cast<u32x4 *>(tA + r * RB + swzf(r, q) * 16) = ra[h];
+    }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) {
+      const int r = srow + RPP * h;
+      *reinterpret_cast<u32x4 *>(tB + r * RB + swzf(r, q) * 16) = rb[h];
+    }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[TI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (nks > 0) {
@@ -158,30 +206,33 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
   for (int ks = 0; ks < nks; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nks) load(ks + 1);
-    const char *tA = lds[buf], *tB = lds[buf] + BM * ROWB;
-    bf16x8 af[2], bw[2];
+    const char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wr * 32 + i * 16 + lr;
-      af[i] = *reinterpret_cast<const bf16x8 *>(tA + r * ROWB + cswz(r, lg) * 16);
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 af[TI], bw[2];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wr * (BMT / 2) + i * 16 + lr;
+        af[i] = *reinterpret_cast<const bf16x8 *>(tA + r * RB + swzf(r, kk * 4 + lg) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 32 + j * 16 + lr;
+        bw[j] = *reinterpret_cast<const bf16x8 *>(tB + r * RB + swzf(r, kk * 4 + lg) * 16);
+      }
+      // W rows as the MFMA A operand: each lane ends with 4 consecutive output channels of one voxel
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = wc * 32 + j * 16 + lr;
-      bw[j] = *reinterpret_cast<const bf16x8 *>(tB + r * ROWB + cswz(r, lg) * 16);
-    }
-    // W rows as the MFMA A operand: each lane ends with 4 consecutive output channels of one voxel
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
     if (ks + 1 < nks) stage(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
     __syncthreads();
   }
 
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int64_t uo = m0 + wr * 32 + i * 16 + lr;
+  for (int i = 0; i < TI; ++i) {
+    int64_t uo = m0 + wr * (BMT / 2) + i * 16 + lr;
     if (uo >= Mrows) continue;
     if (cm) {   // class row -> output voxel
       int ob, oz, oy, ox;
@@ -207,13 +258,35 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
 }
 
 // ---- weight gradient: dW[co][t][ci] = sum_o dY[o][co] X[in(o, t)][ci], one (co, ci) 64x64 tile
-// of one tap per workgroup and voxel slice; operands staged as [channel][32 voxels] rows
+// of one tap per workgroup and voxel slice.  Both operands are staged row-major ([32 voxels][64
+// channels], whole 128-B rows, double-buffered) and read as MFMA operands with k over voxels by
+// ds_read_b64_tr_b16 (4 voxels x 16 channels per 16-lane group, delivered column-major)
 constexpr int WV = 32;   // voxels per k-step
+constexpr int WIMG = WV * 128;   // one [32][64] bf16 image
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 16-B chunk swizzle of image row r (even values: a 32-B pair of chunks stays adjacent): the
+// eight rows a 32-lane half reads (8g + 4h + q, two groups) land on distinct 32-B bank slots
+PCS_DEV int wsw(int r) { return 2 * (((r >> 1) & 1) | ((r >> 2) & 2)); }
+PCS_DEV int woff(int r, int byte) { return r * 128 + ((((byte >> 4) ^ wsw(r)) << 4) | (byte & 15)); }
+
+// MFMA operand rows = channels cb .. cb+15 (lane & 15), k = voxels 8 (lane >> 4) .. + 8
+PCS_DEV bf16x8 wfrag(const char *img, int cb, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int byte = (cb + 4 * (i & 3)) * 2;   // this lane supplies row 8g (+4) + i/4, columns cb + 4 (i%4)
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + woff(8 * g + (i >> 2), byte)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(img + woff(8 * g + 4 + (i >> 2), byte)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                                const bf16_t *__restrict__ dY, float *__restrict__ ws,
                                                                int64_t M, int64_t vps) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 64 * ROWB];   // dY^T | X^T, [64 ch][32 voxels]
+  __shared__ __attribute__((aligned(16))) char lds[2][2 * WIMG];   // per buffer: dY image | X image
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
   const int nco = g.Cout / 64;
@@ -232,17 +305,19 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
     vs = ((Mv + gridDim.z - 1) / gridDim.z + WV - 1) / WV * WV;
   }
   const int64_t lo = (int64_t)split * vs, hi = pcs_min64(lo + vs, Mv);
-  const int sv = tid >> 3, q8 = tid & 7;   // staging: voxel row sv, 8 channels 8*q8 ..
-  char *tD = lds, *tX = lds + 64 * ROWB;
+  const int sv = tid >> 3, q8 = tid & 7;   // staging: voxel row sv, 16-B chunk q8 (channels 8 q8 ..)
 
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t v0 = lo; v0 < hi; v0 += WV) {
+  // the next k-step's rows are loaded into registers while this one's MFMAs run
+  u32x4 rd, rx;
+  auto load = [&](int64_t v0) {
     const int64_t u = v0 + sv;
-    u32x4 rd = mk_u32x4(0, 0, 0, 0), rx = mk_u32x4(0, 0, 0, 0);
+    rd = mk_u32x4(0, 0, 0, 0);
+    rx = mk_u32x4(0, 0, 0, 0);
     if (u < hi) {
       int b, z, y, x;
       int64_t uo = u;
@@ -256,33 +331,32 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
       const int64_t iv = in_voxel(g, b, z, y, x, dz, dy, dx);
       if (iv >= 0) rx = *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + ci0 + q8 * 8);
     }
-    __syncthreads();   // the previous k-step's fragments have been read
-    // transposed stores: element (channel c, voxel sv) at row c, slot sv / 8, position sv % 8
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = q8 * 8 + e;
-      const int off = c * ROWB + cswz(c, sv >> 3) * 16 + (sv & 7) * 2;
-      const uint32_t wd = rd[e >> 1], wx = rx[e >> 1];
-      *reinterpret_cast<bf16_t *>(tD + off) = (bf16_t)((e & 1) ? wd >> 16 : wd & 0xffffu);
-      *reinterpret_cast<bf16_t *>(tX + off) = (bf16_t)((e & 1) ? wx >> 16 : wx & 0xffffu);
-    }
-    __syncthreads();
+  };
+  auto stage = [&](int buf) {
+    *reinterpret_cast<u32x4 *>(lds[buf] + woff(sv, q8 * 16)) = rd;
+    *reinterpret_cast<u32x4 *>(lds[buf] + WIMG + woff(sv, q8 * 16)) = rx;
+  };
+  const int nks = (int)((hi - lo + WV - 1) / WV);   // uniform; 0 for an empty slice
+  if (nks > 0) {
+    load(lo);
+    stage(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nks) load(lo + (int64_t)(ks + 1) * WV);
     bf16x8 fd[2], fx[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wr * 32 + i * 16 + lr;
-      fd[i] = *reinterpret_cast<const bf16x8 *>(tD + r * ROWB + cswz(r, lg) * 16);
-    }
+    for (int i = 0; i < 2; ++i) fd[i] = wfrag(lds[buf], wr * 32 + i * 16, lane);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = wc * 32 + j * 16 + lr;
-      fx[j] = *reinterpret_cast<const bf16x8 *>(tX + r * ROWB + cswz(r, lg) * 16);
-    }
+    for (int j = 0; j < 2; ++j) fx[j] = wfrag(lds[buf] + WIMG, wc * 32 + j * 16, lane);
     // lane: dW rows co = 4 lg + v of tile i, column ci = lr of tile j
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
+    if (ks + 1 < nks) stage(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
+    __syncthreads();
   }
   float *out = ws + (int64_t)split * g.Cout * taps * g.Cin;
 #pragma unroll
@@ -385,19 +459,29 @@ extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W
     return pcs_set_einval("pcs_conv3d", "Cin must be a multiple of 32 and Cout of 64");
   if (ydtype != PCS_F32 && ydtype != PCS_BF16) return pcs_set_einval("pcs_conv3d", "Y dtype: PCS_F32 or PCS_BF16");
   const int64_t M = out_voxels(*g);
-  // transposed stride 2: 8 parity classes, tiles of the largest class's sub-grid each
-  const int64_t rows = g->transposed && g->s == 2
-                           ? 8 * ((g->B * ((g->Do + 1) / 2) * ((g->Ho + 1) / 2) * ((g->Wo + 1) / 2) + BM - 1) / BM)
-                           : (M + BM - 1) / BM;
-  if (rows <= 0 || rows > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
-  const dim3 grid((unsigned)rows, (unsigned)(g->Cout / BN));
+  // transposed stride 2: 8 parity classes, tiles of the largest class's sub-grid each.  128-voxel
+  // tiles (8 MFMAs per wave per barrier) once there are enough of them to fill the chip
+  const int64_t rows_cls = g->transposed && g->s == 2 ? g->B * ((g->Do + 1) / 2) * ((g->Ho + 1) / 2) * ((g->Wo + 1) / 2) : M;
+  const int64_t ncb = g->Cout / BN;
+  const int bmt = (rows_cls / 128) * ncb * (g->transposed && g->s == 2 ? 8 : 1) >= 2048 ? 128 : 64;
+  const int64_t tiles = (rows_cls + bmt - 1) / bmt * (g->transposed && g->s == 2 ? 8 : 1);
+  if (tiles <= 0 || tiles > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
+  const dim3 grid((unsigned)tiles, (unsigned)ncb);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (ydtype == PCS_BF16)
-    hipLaunchKernelGGL(conv3d_kernel<true>, grid, dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X),
-                       static_cast<const bf16_t *>(W), bias, Y, M);
-  else
-    hipLaunchKernelGGL(conv3d_kernel<false>, grid, dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X),
-                       static_cast<const bf16_t *>(W), bias, Y, M);
+  const bf16_t *Xb = static_cast<const bf16_t *>(X), *Wb = static_cast<const bf16_t *>(W);
+  const bool k64 = g->Cin % 64 == 0;
+#define PCS_C3(BMT, KST, OB) hipLaunchKernelGGL((conv3d_kernel<BMT, KST, OB>), grid, dim3(THREADS), 0, s, *g, Xb, Wb, bias, Y, M)
+#define PCS_C3K(BMT, OB) \
+  do {                   \
+    if (k64) PCS_C3(BMT, 64, OB); else PCS_C3(BMT, 32, OB); \
+  } while (0)
+  if (bmt == 128) {
+    if (ydtype == PCS_BF16) PCS_C3K(128, true); else PCS_C3K(128, false);
+  } else {
+    if (ydtype == PCS_BF16) PCS_C3K(64, true); else PCS_C3K(64, false);
+  }
+#undef PCS_C3K
+#undef PCS_C3
   PCS_CHECK_LAUNCH();
   return 0;
 }

@@ -62,6 +62,21 @@ def test_forward_matches_torch(k, s, p, transposed, grid, cin, cout):
     assert _rel(yb.float(), ref) < 8e-3           # one bf16 rounding of the stored output
 
 
+@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout", [(3, 1, 1, False, (41, 40, 40), 64, 128),
+                                                            (2, 2, 0, True, (32, 32, 32), 64, 128)])
+def test_forward_large_tiles(k, s, p, transposed, grid, cin, cout):
+    """Grids large enough for the 128-voxel tiles (pcs_conv3d switches at 2048 tiles), against
+    torch fp32 on the host (its own rounding is ~1e-6 of the output scale)."""
+    import pcs_amd.voxel as V
+    x, w, b = _operands(k, transposed, grid, cin, cout, seed=3)
+    f_ref = F.conv_transpose3d if transposed else F.conv3d
+    ref = f_ref(x.permute(0, 4, 1, 2, 3).float(), w, b, stride=s, padding=p).permute(0, 2, 3, 4, 1).double()
+    f = V.conv_transpose3d if transposed else V.conv3d
+    y = f(x.to(DEV), w.to(DEV), b.to(DEV), s, p, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert _rel(y, ref) < 2e-5
+
+
 @pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout", CASES)
 def test_backward_matches_torch(k, s, p, transposed, grid, cin, cout):
     import pcs_amd.voxel as V
