@@ -283,41 +283,54 @@ PCS_DEV bf16x8 wfrag(const char *img, int cb, int lane) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// One workgroup covers the dx taps of one (dz, dy) (all k of them, sharing the dY image; one tap
+// in class mode, where the dx taps meet different voxel sets)
+constexpr int TG = 3;
+
 __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                                const bf16_t *__restrict__ dY, float *__restrict__ ws,
                                                                int64_t M, int64_t vps) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2 * WIMG];   // per buffer: dY image | X image
+  __shared__ __attribute__((aligned(16))) char lds[2][(1 + TG) * WIMG];   // per buffer: dY | X per dx tap
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
   const int nco = g.Cout / 64;
   const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
-  const int t = blockIdx.y, split = blockIdx.z;
+  const int split = blockIdx.z;
   const int k = g.k, taps = k * k * k;
-  const int dz = t / (k * k), dy = (t / k) % k, dx = t % k;
   // transposed, stride 2: tap t only meets the output voxels of parity class (t + p) mod 2, so
-  // the slices run over that class's sub-grid
+  // the slices run over that class's sub-grid, one tap per workgroup
   const bool cm = g.transposed && g.s == 2;
+  int dz, dy, dx0, ntg;
+  if (cm) {
+    const int t = blockIdx.y;
+    dz = t / (k * k); dy = (t / k) % k; dx0 = t % k; ntg = 1;
+  } else {
+    dz = blockIdx.y / k; dy = blockIdx.y % k; dx0 = 0; ntg = k;
+  }
   PClass pc{};
   int64_t Mv = M, vs = vps;
   if (cm) {
-    pc = pclass(g, (((dz + g.p) & 1) << 2) | (((dy + g.p) & 1) << 1) | ((dx + g.p) & 1));
+    pc = pclass(g, (((dz + g.p) & 1) << 2) | (((dy + g.p) & 1) << 1) | ((dx0 + g.p) & 1));
     Mv = g.B * pc.nz * pc.ny * pc.nx;
     vs = ((Mv + gridDim.z - 1) / gridDim.z + WV - 1) / WV * WV;
   }
   const int64_t lo = (int64_t)split * vs, hi = pcs_min64(lo + vs, Mv);
   const int sv = tid >> 3, q8 = tid & 7;   // staging: voxel row sv, 16-B chunk q8 (channels 8 q8 ..)
 
-  f32x4 acc[2][2];
+  f32x4 acc[TG][2][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int a = 0; a < TG; ++a)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // the next k-step's rows are loaded into registers while this one's MFMAs run
-  u32x4 rd, rx;
+  u32x4 rd, rx[TG];
   auto load = [&](int64_t v0) {
     const int64_t u = v0 + sv;
     rd = mk_u32x4(0, 0, 0, 0);
-    rx = mk_u32x4(0, 0, 0, 0);
+#pragma unroll
+    for (int a = 0; a < TG; ++a) rx[a] = mk_u32x4(0, 0, 0, 0);
     if (u < hi) {
       int b, z, y, x;
       int64_t uo = u;
@@ -328,13 +341,20 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
         decode(g, u, b, z, y, x);
       }
       rd = *reinterpret_cast<const u32x4 *>(dY + uo * g.Cout + co0 + q8 * 8);
-      const int64_t iv = in_voxel(g, b, z, y, x, dz, dy, dx);
-      if (iv >= 0) rx = *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + ci0 + q8 * 8);
+#pragma unroll
+      for (int a = 0; a < TG; ++a) {
+        if (a < ntg) {
+          const int64_t iv = in_voxel(g, b, z, y, x, dz, dy, dx0 + a);
+          if (iv >= 0) rx[a] = *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + ci0 + q8 * 8);
+        }
+      }
     }
   };
   auto stage = [&](int buf) {
     *reinterpret_cast<u32x4 *>(lds[buf] + woff(sv, q8 * 16)) = rd;
-    *reinterpret_cast<u32x4 *>(lds[buf] + WIMG + woff(sv, q8 * 16)) = rx;
+#pragma unroll
+    for (int a = 0; a < TG; ++a)
+      if (a < ntg) *reinterpret_cast<u32x4 *>(lds[buf] + (1 + a) * WIMG + woff(sv, q8 * 16)) = rx[a];
   };
   const int nks = (int)((hi - lo + WV - 1) / WV);   // uniform; 0 for an empty slice
   if (nks > 0) {
@@ -345,31 +365,43 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
   for (int ks = 0; ks < nks; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nks) load(lo + (int64_t)(ks + 1) * WV);
-    bf16x8 fd[2], fx[2];
+    bf16x8 fd[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) fd[i] = wfrag(lds[buf], wr * 32 + i * 16, lane);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) fx[j] = wfrag(lds[buf] + WIMG, wc * 32 + j * 16, lane);
-    // lane: dW rows co = 4 lg + v of tile i, column ci = lr of tile j
+    for (int a = 0; a < TG; ++a) {
+      if (a < ntg) {   // uniform
+        bf16x8 fx[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) fx[j] = wfrag(lds[buf] + (1 + a) * WIMG, wc * 32 + j * 16, lane);
+        // lane: dW rows co = 4 lg + v of tile i, column ci = lr of tile j
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[a][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[a][i][j], 0, 0, 0);
+      }
+    }
     if (ks + 1 < nks) stage(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
     __syncthreads();
   }
   float *out = ws + (int64_t)split * g.Cout * taps * g.Cin;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int a = 0; a < TG; ++a) {
+    if (a >= ntg) continue;
+    const int t = (dz * k + dy) * k + dx0 + a;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ci = ci0 + wc * 32 + j * 16 + lr;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
-        out[((int64_t)co * taps + t) * g.Cin + ci] = acc[i][j][v];
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + wc * 32 + j * 16 + lr;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+          out[((int64_t)co * taps + t) * g.Cin + ci] = acc[a][i][j][v];
+        }
       }
-    }
+  }
 }
 
 // db partials: column sums of dY over one voxel slice, [split][Cout]
@@ -436,7 +468,7 @@ int64_t out_voxels(const pcs_conv3d_geom &g) { return g.B * g.Do * g.Ho * g.Wo; 
 
 int64_t wgrad_splits(const pcs_conv3d_geom &g) {
   const int64_t M = out_voxels(g);
-  const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * g.k * g.k * g.k;
+  const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * (g.transposed && g.s == 2 ? g.k * g.k * g.k : g.k * g.k);
   int64_t sp = (2048 + tiles - 1) / tiles;
   const int64_t maxsp = (M + 4 * WV - 1) / (4 * WV);   // at least 4 k-steps per slice
   if (sp > maxsp) sp = maxsp;
@@ -506,7 +538,8 @@ extern "C" int pcs_conv3d_wgrad(const pcs_conv3d_geom *g, const void *X, const v
   const int64_t wlen = (int64_t)g->Cout * taps * g->Cin;
   float *ws = static_cast<float *>(workspace), *wsb = ws + sp * wlen;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(conv3d_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), (unsigned)taps, (unsigned)sp),
+  const int groups = g->transposed && g->s == 2 ? taps : g->k * g->k;   // workgroups per (co, ci) tile and slice
+  hipLaunchKernelGGL(conv3d_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), (unsigned)groups, (unsigned)sp),
                      dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, M, vps);
   PCS_CHECK_LAUNCH();
   hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((wlen + 255) / 256)), dim3(256), 0, s, ws, sp, wlen, dW);

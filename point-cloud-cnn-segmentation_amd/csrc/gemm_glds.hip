@@ -162,6 +162,20 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   if (t_begin >= t_end) return;   // uniform across the workgroup
   const int nks = K / KT;
   const int total = (t_end - t_begin) * nks;
+  // FWD: the chunk's row tiles are visited in the order t -> (t * P) mod n (P prime, not dividing
+  // n): spatially ordered clouds make a column's running maximum grow tile after tile, which
+  // sends the pool epilogue down its slow path on most tiles; a strided order samples the whole
+  // chunk early, so the running maxima settle after a few tiles.  DGRAD keeps the identity.
+  const int ntl = t_end - t_begin;
+  int P = 1;
+  if (MODE == MODE_FWD && ntl > 8) {
+    constexpr int primes[6] = {97, 89, 83, 79, 73, 71};
+#pragma unroll
+    for (int i = 5; i >= 0; --i)
+      if (primes[i] < ntl && ntl % primes[i] != 0) P = primes[i];
+    P = __builtin_amdgcn_readfirstlane(P);
+  }
+  auto pnext = [&](int pt) { return pt + P >= ntl ? pt + P - ntl : pt + P; };   // perm(t + 1) from perm(t)
   const int64_t row0 = (int64_t)scene * N + (int64_t)t_begin * BM;
   const int64_t scene_end = (int64_t)(scene + 1) * N;
   const char *Ab = reinterpret_cast<const char *>(a.A);
@@ -340,7 +354,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   };
 
   // ---- prologue: K-tile 0 landed; A-lo, B-lo, B-hi of K-tile 1 in flight
-  const int tl1 = nks == 1 ? 1 : 0, kt1 = nks == 1 ? 0 : 1;   // K-tile 1
+  const int tl1 = nks == 1 ? pnext(0) : 0, kt1 = nks == 1 ? 0 : 1;   // K-tile 1 (row tile permuted)
   issue(0, 0, 0, 0); issue(0, 0, 0, 1); issue(0, 0, 0, 2); issue(0, 0, 0, 3);
   issue(1, tl1, kt1, 0); issue(1, tl1, kt1, 2); issue(1, tl1, kt1, 3);
   wait_vm<6>();
@@ -356,20 +370,23 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   // a region one phase after its last read safe across the stagger.
   if (wm == 1) barrier_raw();
 
-  int kt = 0, tcur = 0, ta = 0, ka = 0;   // (row tile, K-tile) of qs and of qs + 1
-  for (int qs = 0; qs < total; ++qs, kt = ka, tcur = ta) {
+  // (row tile, K-tile) of qs and of qs + 1; pcur / pa: their row tiles in visiting order
+  int kt = 0, tcur = 0, ta = 0, ka = 0, pcur = 0, pa = 0;
+  for (int qs = 0; qs < total; ++qs, kt = ka, tcur = ta, pcur = pa) {
     const int buf = qs & 1;
     // (row tile, K-tile) of qs + 1 and qs + 2
     const bool w1 = kt + 1 == nks;
     ta = w1 ? tcur + 1 : tcur;
+    pa = w1 ? pnext(pcur) : pcur;
     ka = w1 ? 0 : kt + 1;
     const bool w2 = ka + 1 == nks;
-    const int tb = w2 ? ta + 1 : ta, kb = w2 ? 0 : ka + 1;
+    const int kb = w2 ? 0 : ka + 1;
+    const int pb = w2 ? pnext(pa) : pa;
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
     read_a(buf, 0);
     read_b(buf, 2, 0);
     if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 0, kt - kq0, tcur & 1);
-    issue(qs + 1, ta, ka, 1);
+    issue(qs + 1, pa, ka, 1);
     // every counted wait assumes the five regions issued after the one it retires are in
     // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
     // regions actually issued (phase 1 retires B-hi(qs): newer are A-hi(qs) and, unless qs is
@@ -383,7 +400,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 2: (lo, hi); restage A-lo of K-tile qs+2
     read_b(buf, 3, 2);
-    issue(qs + 2, tb, kb, 0);
+    issue(qs + 2, pb, kb, 0);
     // retires A-hi(qs): newer are the four regions of qs+1 and A-lo(qs+2)
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<8>(); else wait_vm<0>();
     wait_lgkm0();
@@ -394,7 +411,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
-    issue(qs + 2, tb, kb, 2);
+    issue(qs + 2, pb, kb, 2);
     wait_lgkm0();
     barrier_raw();
     __builtin_amdgcn_s_setprio(1);
@@ -405,7 +422,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // in phase 3: B-lo's fragments are dead by now, which keeps the extraction's registers
     // out of the accumulators' way (A-hi(qs) is restaged only in phase 1 of qs+1)
     if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 1, kt - kq0, tcur & 1);
-    issue(qs + 2, tb, kb, 3);
+    issue(qs + 2, pb, kb, 3);
     // retires A-lo(qs+1), B-lo(qs+1): newer are B-hi(qs+1), A-hi(qs+1) and three of qs+2
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();
     barrier_raw();
@@ -416,8 +433,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 
     if (kt != nks - 1) continue;
 
-    // ===================== epilogue of row tile tcur =====================
-    const int64_t rb = row0 + (int64_t)tcur * BM;
+    // ===================== epilogue of row tile tcur (rows of tile pcur) =====================
+    const int64_t rb = row0 + (int64_t)pcur * BM;
     const int valid = (int)pcs_min64(BM, scene_end - rb);
     const int nvw = max(0, min(128, valid - wm * 128));   // valid rows of this wave's half
     // lane's columns c(j, r) = wn*64 + j*16 + 4*lg + r; rows m(i) = wm*128 + i*16 + lr
@@ -500,7 +517,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                 const float t0 = max3f(acc[0][j][r], acc[1][j][r], acc[2][j][r]);
                 const float t1 = max3f(acc[3][j][r], acc[4][j][r], acc[5][j][r]);
                 const float t2 = max3f(acc[6][j][r], acc[7][j][r], t0);
-                bj |= max2f(t1, t2) > cc[r];
+                bj |= max2f(t1, t2) >= cc[r];   // >=: an equal value may sit on an earlier row
               }
               beat |= (uint32_t)bj << j;
             }
@@ -519,7 +536,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                   if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, gg[r] * acc[i][j][r]);
-                bj |= mx > cc[r];
+                bj |= mx >= cc[r];
               }
               beat |= (uint32_t)bj << j;
             }
@@ -530,6 +547,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
             const float4 q = runp[cme];
             const float sgl = lsgn[cme - wm * BN];
             const float cur = sgl > 0.f ? q.x : -q.z;
+            const int curix = __float_as_int(sgl > 0.f ? q.y : q.w);
             float vx[4], sg[4];
             float mine = -__builtin_huge_valf();
 #pragma unroll
@@ -542,7 +560,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
               vx[r] = row_max(mx);
               if (lr == j * 4 + r) mine = vx[r];
             }
-            const bool upd = (lr >> 2) == j && mine > cur;
+            // tiles are not visited in row order: an equal value replaces the running one when
+            // its row is smaller (the first maximum, as in row order)
+            const bool upd = (lr >> 2) == j && mine >= cur;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               if (__builtin_amdgcn_ballot_w64(upd && (lr & 3) == r) == 0) continue;
@@ -553,7 +573,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                 if (((rowok >> i) & 1u) && v == vx[r]) ix = (int)(rb + wm * 128 + i * 16 + lr);
               }
               ix = row_mini(ix);
-              if (upd && (lr & 3) == r) {
+              if (upd && (lr & 3) == r && (mine > cur || ix < curix)) {
                 float4 u = q;
                 if (sgl > 0.f) { u.x = vx[r]; u.y = __int_as_float(ix); }
                 else { u.z = -vx[r]; u.w = __int_as_float(ix); }

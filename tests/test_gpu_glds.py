@@ -349,3 +349,52 @@ def test_glds_deterministic_and_tail_exact(mode):
             assert err < 1e-2 * dz.abs().max().item(), (b, err)
         err = float((out.double() - dz).abs().max())
         assert err < 1e-2 * dz.abs().max().item(), err
+
+
+@pytest.mark.parametrize("signed", [False, True])
+@pytest.mark.parametrize("data", ["ties", "trend"])
+def test_forward_pool_strided_tile_order(signed, data):
+    """Chunks of more than 97 row tiles visit their tiles in a strided order (gemm_glds.hip): the
+    max-pool must still report the first maximum in row order.  'ties': 37 distinct rows repeated
+    across the scene (every maximum is tied hundreds of times, identical bits); 'trend': values
+    rising along the rows (the spatially ordered case the order is for)."""
+    import pcs_amd._lib as L
+    B, N, K, cps = 1, 256 * 100 + 51, 512, 1
+    g = torch.Generator().manual_seed(11)
+    if data == "ties":
+        # tile 0 (visited first) holds zero rows, the first occurrences of the 37 rows sit in tile 1
+        # (visited late), duplicates in every later tile (tile P is visited second)
+        base = torch.relu(torch.randn(37, K, generator=g))
+        A = base[(torch.arange(N) * 7) % 37]
+        A[:256] = 0
+    else:
+        A = torch.relu(torch.randn(N, K, generator=g) + torch.linspace(0, 3, N)[:, None])
+    A = A.to(torch.bfloat16)
+    W = (torch.randn(K, K, generator=g) * 0.05).to(torch.bfloat16)
+    gamma = torch.randn(K, generator=g)
+    Wd = W.to(DEV)
+    if signed:
+        Ws = torch.empty_like(Wd)
+        L.call("pcs_sign_rows", L.ptr(Wd), L.BF16, K, K, L.ptr(gamma.to(DEV)), L.ptr(Ws), L.stream_ptr())
+        Wd = Ws
+    a, rpc = _args(L, B, N, K, K, L.BF16, L.PRO_RAW, L.EPI_FWD, L.FLAG_POOL_SIGNED_W if signed else 0, cps)
+    assert rpc // 256 > 97                                   # the strided order is in use
+    Ad, gd = A.to(DEV), gamma.to(DEV)
+    pool = torch.empty(B * a.chunks_per_scene, K, 4, device=DEV)
+    a.A, a.W, a.C, a.pool, a.es = Ad.data_ptr(), Wd.data_ptr(), None, pool.data_ptr(), gd.data_ptr()
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    torch.cuda.synchronize()
+    y = A.double() @ W.double().T
+    sgn = torch.where(gamma > 0, 1.0, -1.0).double()
+    pl = pool.cpu()
+    val = torch.where(gamma > 0, pl[0, :, 0], pl[0, :, 2]).double()
+    row = torch.where(gamma > 0, pl[0, :, 1], pl[0, :, 3]).view(torch.int32).long()
+    ext = (y * sgn).max(0).values * sgn
+    scl = y.abs().max().item()
+    assert float((val - ext).abs().max()) < 1e-5 * scl
+    at = y.gather(0, row[None, :]).squeeze(0)
+    assert float((at - ext).abs().max()) < 1e-5 * scl
+    if data == "ties":   # exact: the first row, in row order, holding the extremum
+        yb = y * sgn
+        first = (yb == yb.max(0).values).double().argmax(0)   # argmax returns the first maximum
+        assert torch.equal(row, first)
