@@ -257,6 +257,130 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
   }
 }
 
+// ---- 3x3x3 stride-1 stencil (both forms) with the input block's halo staged in LDS once per
+// 64-channel slice: a 4 x 4 x 8 block of output voxels reads its 6 x 6 x 10 input halo (360
+// voxel rows) from L2 once and every tap's A operand from LDS at a shifted row, instead of
+// 27 gathers; the 27 taps' 64 x 64 weight tiles stream through a double buffer.
+constexpr int SZ = 4, SY = 4, SX = 8;                      // output block: 128 voxels
+constexpr int GZ = SZ + 2, GY = SY + 2, GX = SX + 2;
+constexpr int HROWS = GZ * GY * GX;                        // 360 halo voxels
+constexpr int HIMG = HROWS * 128, WTILE = 64 * 128;        // halo image (64 ch), one tap's W tile
+
+PCS_DEV int swz8(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(THREADS) void stencil3_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
+                                                           const bf16_t *__restrict__ W, const float *__restrict__ bias,
+                                                           void *__restrict__ Y) {
+  __shared__ __attribute__((aligned(16))) char lds[HIMG + 2 * WTILE];   // 45 KB + 16 KB
+  char *halo = lds, *wt = lds + HIMG;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int nbx = (g.Wo + SX - 1) / SX, nby = (g.Ho + SY - 1) / SY, nbz = (g.Do + SZ - 1) / SZ;
+  uint32_t bid = blockIdx.x;
+  const int bx = (int)(bid % nbx); bid /= nbx;
+  const int by = (int)(bid % nby); bid /= nby;
+  const int bz = (int)(bid % nbz);
+  const int b = (int)(bid / nbz);
+  const int oz0 = bz * SZ, oy0 = by * SY, ox0 = bx * SX;
+  const bool tr = g.transposed;
+  // first halo voxel: conv reads o - p + t, the transposed form o + p - t (t = 0..2)
+  const int hz0 = tr ? oz0 + g.p - 2 : oz0 - g.p, hy0 = tr ? oy0 + g.p - 2 : oy0 - g.p,
+            hx0 = tr ? ox0 + g.p - 2 : ox0 - g.p;
+  const int n0 = blockIdx.y * 64, Cin = g.Cin, cps = Cin / 64;
+  // wave tile: output rows wr*64 .. +64 (4 MFMA tiles), channels wc*32 .. +32; row r = (rz, ry, rx)
+  int hrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wr * 64 + i * 16 + lr;
+    hrow[i] = ((r >> 5) * GY + ((r >> 3) & 3)) * GX + (r & 7);
+  }
+  u32x4 rw[2];   // W staging: 64 rows x 8 chunks, two per thread
+  auto loadw = [&](int t, int c0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = tid + THREADS * h, row = c >> 3, ch = c & 7;
+      rw[h] = *reinterpret_cast<const u32x4 *>(W + ((int64_t)(n0 + row) * 27 + t) * Cin + c0 + ch * 8);
+    }
+  };
+  auto stagew = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = tid + THREADS * h, row = c >> 3, ch = c & 7;
+      *reinterpret_cast<u32x4 *>(wt + buf * WTILE + row * 128 + swz8(row, ch) * 16) = rw[h];
+    }
+  };
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int cs = 0; cs < cps; ++cs) {
+    const int c0 = cs * 64;
+    __syncthreads();   // the previous slice's halo and W reads are done
+    for (int c = tid; c < HROWS * 8; c += THREADS) {
+      const int hr = c >> 3, ch = c & 7;
+      const int hx = hr % GX, hy = (hr / GX) % GY, hz = hr / (GX * GY);
+      const int iz = hz0 + hz, iy = hy0 + hy, ix = hx0 + hx;
+      u32x4 v = mk_u32x4(0, 0, 0, 0);
+      if (iz >= 0 && iy >= 0 && ix >= 0 && iz < g.Di && iy < g.Hi && ix < g.Wi)
+        v = *reinterpret_cast<const u32x4 *>(X + ((((int64_t)b * g.Di + iz) * g.Hi + iy) * g.Wi + ix) * Cin + c0 + ch * 8);
+      *reinterpret_cast<u32x4 *>(halo + hr * 128 + swz8(hr, ch) * 16) = v;
+    }
+    loadw(0, c0);
+    stagew(0);
+    __syncthreads();
+    for (int t = 0; t < 27; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < 27) loadw(t + 1, c0);
+      const int dz = t / 9, dy = (t / 3) % 3, dx = t % 3;
+      const int hoff = tr ? ((2 - dz) * GY + (2 - dy)) * GX + (2 - dx) : (dz * GY + dy) * GX + dx;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4], bw[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int h = hrow[i] + hoff;
+          af[i] = *reinterpret_cast<const bf16x8 *>(halo + h * 128 + swz8(h, kk * 4 + lg) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = wc * 32 + j * 16 + lr;
+          bw[j] = *reinterpret_cast<const bf16x8 *>(wt + buf * WTILE + r * 128 + swz8(r, kk * 4 + lg) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      if (t + 1 < 27) stagew(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wr * 64 + i * 16 + lr;
+    const int oz = oz0 + (r >> 5), oy = oy0 + ((r >> 3) & 3), ox = ox0 + (r & 7);
+    if (oz >= g.Do || oy >= g.Ho || ox >= g.Wo) continue;
+    const int64_t uo = (((int64_t)b * g.Do + oz) * g.Ho + oy) * g.Wo + ox;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = n0 + wc * 32 + j * 16 + 4 * lg;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        const float4 bb = *reinterpret_cast<const float4 *>(bias + co);
+        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      }
+      if constexpr (OUT_BF16) {
+        *reinterpret_cast<uint2 *>(reinterpret_cast<bf16_t *>(Y) + uo * g.Cout + co) =
+            make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      } else {
+        *reinterpret_cast<float4 *>(reinterpret_cast<float *>(Y) + uo * g.Cout + co) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
 // ---- weight gradient: dW[co][t][ci] = sum_o dY[o][co] X[in(o, t)][ci], one (co, ci) 64x64 tile
 // of one tap per workgroup and voxel slice.  Both operands are staged row-major ([32 voxels][64
 // channels], whole 128-B rows, double-buffered) and read as MFMA operands with k over voxels by
@@ -491,6 +615,17 @@ extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W
     return pcs_set_einval("pcs_conv3d", "Cin must be a multiple of 32 and Cout of 64");
   if (ydtype != PCS_F32 && ydtype != PCS_BF16) return pcs_set_einval("pcs_conv3d", "Y dtype: PCS_F32 or PCS_BF16");
   const int64_t M = out_voxels(*g);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (g->k == 3 && g->s == 1 && g->Cin % 64 == 0) {   // halo-staged stencil (both forms)
+    const int64_t nblk = g->B * ((g->Do + SZ - 1) / SZ) * ((g->Ho + SY - 1) / SY) * ((g->Wo + SX - 1) / SX);
+    if (nblk > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
+    const dim3 sg((unsigned)nblk, (unsigned)(g->Cout / BN));
+    const bf16_t *Xs = static_cast<const bf16_t *>(X), *Ws = static_cast<const bf16_t *>(W);
+    if (ydtype == PCS_BF16) hipLaunchKernelGGL(stencil3_kernel<true>, sg, dim3(THREADS), 0, s, *g, Xs, Ws, bias, Y);
+    else hipLaunchKernelGGL(stencil3_kernel<false>, sg, dim3(THREADS), 0, s, *g, Xs, Ws, bias, Y);
+    PCS_CHECK_LAUNCH();
+    return 0;
+  }
   // transposed stride 2: 8 parity classes, tiles of the largest class's sub-grid each.  128-voxel
   // tiles (8 MFMAs per wave per barrier) once there are enough of them to fill the chip
   const int64_t rows_cls = g->transposed && g->s == 2 ? g->B * ((g->Do + 1) / 2) * ((g->Ho + 1) / 2) * ((g->Wo + 1) / 2) : M;
@@ -499,7 +634,6 @@ extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W
   const int64_t tiles = (rows_cls + bmt - 1) / bmt * (g->transposed && g->s == 2 ? 8 : 1);
   if (tiles <= 0 || tiles > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
   const dim3 grid((unsigned)tiles, (unsigned)ncb);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bf16_t *Xb = static_cast<const bf16_t *>(X), *Wb = static_cast<const bf16_t *>(W);
   const bool k64 = g->Cin % 64 == 0;
 #define PCS_C3(BMT, KST, OB) hipLaunchKernelGGL((conv3d_kernel<BMT, KST, OB>), grid, dim3(THREADS), 0, s, *g, Xb, Wb, bias, Y, M)
