@@ -528,6 +528,116 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
   }
 }
 
+// ---- weight gradient of the 3x3x3 stride-1 stencil (both forms) on halo tiles: a workgroup owns
+// one (64 co x 64 ci) tile and one dz (9 taps, 144 accumulator VGPRs) and walks a range of 4 x 4 x 8
+// output blocks; per block it stages the block's dY rows [128][64] and the 4 input planes of the
+// halo it meets at this dz [4][6][10][64] once, and every tap's operand is a shifted set of halo
+// rows read transposed (k over the block's voxels)
+constexpr int XPL = SZ * GY * GX;   // 240 halo rows of one dz
+
+__global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
+                                                                 const bf16_t *__restrict__ dY, float *__restrict__ ws,
+                                                                 int64_t nblk, int64_t bps) {
+  __shared__ __attribute__((aligned(16))) char lds[(128 + XPL) * 128];   // dY image | halo planes (46 KB)
+  char *dimg = lds, *ximg = lds + 128 * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int nco = g.Cout / 64;
+  const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
+  const int dz = blockIdx.y, split = blockIdx.z;
+  const bool tr = g.transposed;
+  const int zoff = tr ? 2 - dz : dz;
+  const int nbx = (g.Wo + SX - 1) / SX, nby = (g.Ho + SY - 1) / SY, nbz = (g.Do + SZ - 1) / SZ;
+  const int64_t b0 = (int64_t)split * bps, b1 = pcs_min64(b0 + bps, nblk);
+  // transposed operand read: rows = 16 channels from cb (lane & 15), k = 8 voxels from 8 (lane >> 4)
+  // (4 per ds_read_b64_tr_b16); row_of(k) gives the image row of block voxel k
+  auto trfrag = [&](const char *img, int cb, int kb, int dyo, int dxo, bool halo) {
+    const int gq = lane >> 4, i = lane & 15;
+    const int byte = (cb + 4 * (i & 3)) * 2;
+    s16x4 part[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = kb + 8 * gq + 4 * h + (i >> 2);   // block voxel
+      const int row = halo ? (((r >> 5) * GY + ((r >> 3) & 3) + dyo) * GX + (r & 7) + dxo) : r;
+      part[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4 *)(img + row * 128 + ((((byte >> 4) ^ ((row >> 1) & 7)) << 4) | (byte & 15))));
+    }
+    const s16x8 v = {part[0][0], part[0][1], part[0][2], part[0][3], part[1][0], part[1][1], part[1][2], part[1][3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int a = 0; a < 9; ++a)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t blk = b0; blk < b1; ++blk) {
+    uint32_t q = (uint32_t)blk;
+    const int bx = (int)(q % nbx); q /= nbx;
+    const int by = (int)(q % nby); q /= nby;
+    const int bz = (int)(q % nbz);
+    const int b = (int)(q / nbz);
+    const int oz0 = bz * SZ, oy0 = by * SY, ox0 = bx * SX;
+    const int hz0 = (tr ? oz0 + g.p - 2 : oz0 - g.p) + zoff, hy0 = tr ? oy0 + g.p - 2 : oy0 - g.p,
+              hx0 = tr ? ox0 + g.p - 2 : ox0 - g.p;
+    __syncthreads();   // the previous block's reads are done
+    for (int c = tid; c < 128 * 8; c += THREADS) {   // dY rows of the block (zero outside the grid)
+      const int r = c >> 3, ch = c & 7;
+      const int oz = oz0 + (r >> 5), oy = oy0 + ((r >> 3) & 3), ox = ox0 + (r & 7);
+      u32x4 v = mk_u32x4(0, 0, 0, 0);
+      if (oz < g.Do && oy < g.Ho && ox < g.Wo)
+        v = *reinterpret_cast<const u32x4 *>(dY + ((((int64_t)b * g.Do + oz) * g.Ho + oy) * g.Wo + ox) * g.Cout + co0 + ch * 8);
+      *reinterpret_cast<u32x4 *>(dimg + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4)) = v;
+    }
+    for (int c = tid; c < XPL * 8; c += THREADS) {   // the 4 halo planes of this dz
+      const int hr = c >> 3, ch = c & 7;
+      const int hx = hr % GX, hy = (hr / GX) % GY, hz = hr / (GX * GY);
+      const int iz = hz0 + hz, iy = hy0 + hy, ix = hx0 + hx;
+      u32x4 v = mk_u32x4(0, 0, 0, 0);
+      if (iz >= 0 && iy >= 0 && ix >= 0 && iz < g.Di && iy < g.Hi && ix < g.Wi)
+        v = *reinterpret_cast<const u32x4 *>(X + ((((int64_t)b * g.Di + iz) * g.Hi + iy) * g.Wi + ix) * g.Cin + ci0 + ch * 8);
+      *reinterpret_cast<u32x4 *>(ximg + hr * 128 + ((ch ^ ((hr >> 1) & 7)) << 4)) = v;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kb = 0; kb < 128; kb += 32) {   // 32 block voxels per MFMA k-step
+      bf16x8 fd[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fd[i] = trfrag(dimg, wr * 32 + i * 16, kb, 0, 0, false);
+#pragma unroll
+      for (int a = 0; a < 9; ++a) {
+        const int ty = a / 3, tx = a % 3;
+        const int dyo = tr ? 2 - ty : ty, dxo = tr ? 2 - tx : tx;
+        bf16x8 fx[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fx[j] = trfrag(ximg, wc * 32 + j * 16, kb, dyo, dxo, true);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[a][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[a][i][j], 0, 0, 0);
+      }
+    }
+  }
+  float *out = ws + (int64_t)split * g.Cout * 27 * g.Cin;
+#pragma unroll
+  for (int a = 0; a < 9; ++a) {
+    const int t = dz * 9 + a;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + wc * 32 + j * 16 + lr;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+          out[((int64_t)co * 27 + t) * g.Cin + ci] = acc[a][i][j][v];
+        }
+      }
+  }
+}
+
 // db partials: column sums of dY over one voxel slice, [split][Cout]
 __global__ __launch_bounds__(THREADS) void conv3d_bgrad_kernel(const bf16_t *__restrict__ dY, int Cout, int64_t M,
                                                                int64_t vps, float *__restrict__ wsb) {
@@ -590,8 +700,19 @@ bool geom_ok(const pcs_conv3d_geom *g, const char **why) {
 
 int64_t out_voxels(const pcs_conv3d_geom &g) { return g.B * g.Do * g.Ho * g.Wo; }
 
+bool stencil3(const pcs_conv3d_geom &g) { return g.k == 3 && g.s == 1; }
+
+int64_t stencil_blocks(const pcs_conv3d_geom &g) {
+  return g.B * ((g.Do + SZ - 1) / SZ) * ((g.Ho + SY - 1) / SY) * ((g.Wo + SX - 1) / SX);
+}
+
 int64_t wgrad_splits(const pcs_conv3d_geom &g) {
   const int64_t M = out_voxels(g);
+  if (stencil3(g)) {   // halo-tile kernel: 3 dz workgroups per (co, ci) tile and block range
+    const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * 3;
+    const int64_t sp = (1024 + tiles - 1) / tiles, nb = stencil_blocks(g);
+    return sp > nb ? nb : sp;
+  }
   const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * (g.transposed && g.s == 2 ? g.k * g.k * g.k : g.k * g.k);
   int64_t sp = (2048 + tiles - 1) / tiles;
   const int64_t maxsp = (M + 4 * WV - 1) / (4 * WV);   // at least 4 k-steps per slice
@@ -672,9 +793,15 @@ extern "C" int pcs_conv3d_wgrad(const pcs_conv3d_geom *g, const void *X, const v
   const int64_t wlen = (int64_t)g->Cout * taps * g->Cin;
   float *ws = static_cast<float *>(workspace), *wsb = ws + sp * wlen;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int groups = g->transposed && g->s == 2 ? taps : g->k * g->k;   // workgroups per (co, ci) tile and slice
-  hipLaunchKernelGGL(conv3d_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), (unsigned)groups, (unsigned)sp),
-                     dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, M, vps);
+  if (stencil3(*g)) {
+    const int64_t nb = stencil_blocks(*g), bps = (nb + sp - 1) / sp;
+    hipLaunchKernelGGL(stencil3_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), 3u, (unsigned)sp),
+                       dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, nb, bps);
+  } else {
+    const int groups = g->transposed && g->s == 2 ? taps : g->k * g->k;   // workgroups per (co, ci) tile and slice
+    hipLaunchKernelGGL(conv3d_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), (unsigned)groups, (unsigned)sp),
+                       dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, M, vps);
+  }
   PCS_CHECK_LAUNCH();
   hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((wlen + 255) / 256)), dim3(256), 0, s, ws, sp, wlen, dW);
   PCS_CHECK_LAUNCH();
