@@ -607,13 +607,15 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         uint32_t pk[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int word = (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg));
+          // rows past the scene (a partial tile) get an all-zero mask word: their v is 0, so S1
+          // sums v unconditionally (one select per word, not one per element); they are not stored
+          const int word = ok ? (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg)) : 0;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
             v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
-            s1[j][r] += ok ? v[r] : 0.f;
+            s1[j][r] += v[r];
           }
           pk[j][0] = pack2bf(v[0], v[1]);
           pk[j][1] = pack2bf(v[2], v[3]);
