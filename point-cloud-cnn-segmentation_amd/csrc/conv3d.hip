@@ -638,18 +638,29 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
   }
 }
 
-// db partials: column sums of dY over one voxel slice, [split][Cout]
+// db partials: column sums of dY over one voxel slice, [split][Cout]; a thread sums 8 channels
+// (one 16-B chunk) of every 32nd row, then the 32 row groups are added in LDS in a fixed order
 __global__ __launch_bounds__(THREADS) void conv3d_bgrad_kernel(const bf16_t *__restrict__ dY, int Cout, int64_t M,
                                                                int64_t vps, float *__restrict__ wsb) {
-  __shared__ float red[THREADS];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), r0 = threadIdx.x >> 6;
+  __shared__ float red[32][64];
+  const int ch = threadIdx.x & 7, rg = threadIdx.x >> 3;   // channels c0 + 8 ch .., row group 0..31
+  const int c0 = blockIdx.x * 64;
   const int64_t lo = (int64_t)blockIdx.y * vps, hi = pcs_min64(lo + vps, M);
-  float s = 0.f;
-  for (int64_t u = lo + r0; u < hi; u += 4) s += bf2f(dY[u * Cout + c]);
-  red[threadIdx.x] = s;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t u = lo + rg; u < hi; u += 32) {
+    float v[8];
+    unpack_chunk(*reinterpret_cast<const u32x4 *>(dY + u * Cout + c0 + ch * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rg][ch * 8 + e] = s[e];
   __syncthreads();
-  if (threadIdx.x < 64)
-    wsb[(int64_t)blockIdx.y * Cout + c] = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+    for (int r = 0; r < 32; ++r) t += red[r][threadIdx.x];
+    wsb[(int64_t)blockIdx.y * Cout + c0 + threadIdx.x] = t;
+  }
 }
 
 // out[i] = sum_s part[s * len + i], fixed order
