@@ -143,42 +143,59 @@ __global__ __launch_bounds__(256) void fold_c_kernel(const float *__restrict__ W
   if (pr == 0 && n < Cin) c[n] = ((red[0][nn] + red[1][nn]) + red[2][nn]) + red[3][nn];
 }
 
-// H[i][j] = sum_k (W[k][i] gamma[k]) W[k][j]: 64 x 64 output tile per block, k in steps of 32
-// through LDS (rows of W are contiguous in i and j: coalesced), 4 x 4 outputs per thread
-template <typename T>
+// H[i][j] = sum_k (W[k][i] gamma[k]) W[k][j]: TILE x TILE output tile per block (32 for a
+// 1024-wide H: 1024 blocks instead of 256, 4x the latency hiding), k in steps of 32 through LDS
+// (rows of W are contiguous in i and j: coalesced), (TILE/16)^2 outputs per thread
+template <typename T, int TILE>
 __global__ __launch_bounds__(256) void fold_h_tiled_kernel(const float *__restrict__ W, int64_t ldw, int Cout,
                                                            int Cin, const float *__restrict__ gamma,
                                                            T *__restrict__ H) {
-  __shared__ float Xs[32][64 + 4];
-  __shared__ float Ys[32][64 + 4];
+  constexpr int R = TILE / 16;
+  __shared__ float Xs[32][TILE + 4];
+  __shared__ float Ys[32][TILE + 4];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < Cout; k0 += 32) {
-    for (int e = tid; e < 32 * 64; e += 256) {
-      const int kk = e >> 6, cc = e & 63, k = k0 + kk;
+  const int i0 = blockIdx.y * TILE, j0 = blockIdx.x * TILE;
+  float acc[R][R] = {};
+  // the next k-chunk is loaded into registers while this one is multiplied (few blocks per CU
+  // for the small H: nothing else hides the load latency)
+  constexpr int NE = 32 * TILE / 256;
+  float px[NE], py[NE];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u, kk = e / TILE, cc = e % TILE, k = k0 + kk;
       const bool ok = k < Cout;
-      Xs[kk][cc] = ok ? W[(int64_t)k * ldw + i0 + cc] * gamma[k] : 0.f;
-      Ys[kk][cc] = ok ? W[(int64_t)k * ldw + j0 + cc] : 0.f;
+      px[u] = ok ? W[(int64_t)k * ldw + i0 + cc] * gamma[k] : 0.f;
+      py[u] = ok ? W[(int64_t)k * ldw + j0 + cc] : 0.f;
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < Cout; k0 += 32) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      Xs[e / TILE][e % TILE] = px[u];
+      Ys[e / TILE][e % TILE] = py[u];
     }
     __syncthreads();
+    if (k0 + 32 < Cout) load(k0 + 32);
 #pragma unroll 8
     for (int kk = 0; kk < 32; ++kk) {
-      const float4 xv = *reinterpret_cast<const float4 *>(&Xs[kk][ty * 4]);
-      const float4 yv = *reinterpret_cast<const float4 *>(&Ys[kk][tx * 4]);
-      const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ya[4] = {yv.x, yv.y, yv.z, yv.w};
+      float xa[R], ya[R];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < R; ++p) { xa[p] = Xs[kk][ty * R + p]; ya[p] = Ys[kk][tx * R + p]; }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[p][q] = fmaf(xa[p], ya[q], acc[p][q]);
+      for (int p = 0; p < R; ++p)
+#pragma unroll
+        for (int q = 0; q < R; ++q) acc[p][q] = fmaf(xa[p], ya[q], acc[p][q]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
+  for (int p = 0; p < R; ++p)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t o = (int64_t)(i0 + ty * 4 + p) * Cin + j0 + tx * 4 + q;
+    for (int q = 0; q < R; ++q) {
+      const int64_t o = (int64_t)(i0 + ty * R + p) * Cin + j0 + tx * R + q;
       if constexpr (sizeof(T) == 2) H[o] = (T)(pack2bf(acc[p][q], 0.f) & 0xffffu);
       else H[o] = acc[p][q];
     }
@@ -376,8 +393,11 @@ void launch_fold(const float *W, int Cout, int Cin, int64_t ldw, const float *al
     hipLaunchKernelGGL(fold_wt_kernel<T>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, WsT);
   }
   hipLaunchKernelGGL(fold_c_kernel, dim3((Cin + 63) / 64), dim3(256), 0, st, W, ldw, Cout, Cin, beta, c);
-  if (Cin % 64 == 0)
-    hipLaunchKernelGGL(fold_h_tiled_kernel<T>, dim3(Cin / 64, Cin / 64), dim3(256), 0, st, W, ldw, Cout, Cin,
+  if (Cin % 64 == 0 && Cin >= 512)
+    hipLaunchKernelGGL((fold_h_tiled_kernel<T, 32>), dim3(Cin / 32, Cin / 32), dim3(256), 0, st, W, ldw, Cout, Cin,
+                       gamma, H);
+  else if (Cin % 64 == 0)   // small H (conv5's 128, seg_conv1's 64): 16 x 16 tiles, more blocks
+    hipLaunchKernelGGL((fold_h_tiled_kernel<T, 16>), dim3(Cin / 16, Cin / 16), dim3(256), 0, st, W, ldw, Cout, Cin,
                        gamma, H);
   else
     hipLaunchKernelGGL(fold_h_kernel<T>, dim3(Cin), dim3(256), 0, st, W, ldw, Cout, Cin, gamma, H);
