@@ -18,48 +18,62 @@ namespace {
 
 constexpr int TILE = 64, KC = 32, THREADS = 256;
 
-template <typename T>
+// TL x TL output tile per block (32 for the wide layer: 4x the blocks of 64), W and G chunks of
+// KC along j through LDS with the next chunk prefetched in registers, (TL/16)^2 outputs per thread
+template <typename T, int TL>
 __global__ __launch_bounds__(THREADS) void gram_wgrad_kernel(
     const float *__restrict__ G, const float *__restrict__ S, const float *__restrict__ W, int64_t ldwin,
     const float *__restrict__ beta, const float *__restrict__ gamma, const float *__restrict__ sp,
     const int *__restrict__ am, const T *__restrict__ Y, const float *__restrict__ s,
     const float *__restrict__ t, int B, int Cout, int Cin, const float *__restrict__ R,
     const float *__restrict__ alpha, float *__restrict__ dW, int64_t ldw) {
-  __shared__ float Ws[TILE][KC + 1];
-  __shared__ float Gs[KC][TILE];
+  constexpr int RR = TL / 16, NE = TL * KC / THREADS;
+  __shared__ float Ws[TL][KC + 1];
+  __shared__ float Gs[KC][TL];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-  const int c0 = blockIdx.y * TILE, k0 = blockIdx.x * TILE;
-  float acc[4][4] = {};
+  const int c0 = blockIdx.y * TL, k0 = blockIdx.x * TL;
+  float acc[RR][RR] = {};
+  float pw[NE], pg[NE];
+  auto load = [&](int j0) {
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + THREADS * u;
+      pw[u] = W[(int64_t)(c0 + e / KC) * ldwin + j0 + e % KC];
+      pg[u] = G[(int64_t)(j0 + e / TL) * Cin + k0 + e % TL];
+    }
+  };
+  load(0);
   for (int j0 = 0; j0 < Cin; j0 += KC) {
-    for (int e = tid; e < TILE * KC; e += THREADS) {
-      const int r = e / KC, q = e % KC;
-      Ws[r][q] = W[(int64_t)(c0 + r) * ldwin + j0 + q];
-      const int gr = e / TILE, gq = e % TILE;
-      Gs[gr][gq] = G[(int64_t)(j0 + gr) * Cin + k0 + gq];
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + THREADS * u;
+      Ws[e / KC][e % KC] = pw[u];
+      Gs[e / TL][e % TL] = pg[u];
     }
     __syncthreads();
+    if (j0 + KC < Cin) load(j0 + KC);
 #pragma unroll 8
     for (int q = 0; q < KC; ++q) {
-      float wv[4], gv[4];
+      float wv[RR], gv[RR];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) wv[i] = Ws[ty * 4 + i][q];
+      for (int i = 0; i < RR; ++i) wv[i] = Ws[ty * RR + i][q];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) gv[j] = Gs[q][tx * 4 + j];
+      for (int j = 0; j < RR; ++j) gv[j] = Gs[q][tx * RR + j];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < RR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(wv[i], gv[j], acc[i][j]);
+        for (int j = 0; j < RR; ++j) acc[i][j] = fmaf(wv[i], gv[j], acc[i][j]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = c0 + ty * 4 + i;
+  for (int i = 0; i < RR; ++i) {
+    const int c = c0 + ty * RR + i;
     const float gc = gamma[c], bc = beta[c];
-    float o[4];
+    float o[RR];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + tx * 4 + j;
+    for (int j = 0; j < RR; ++j) {
+      const int k = k0 + tx * RR + j;
       o[j] = fmaf(gc, acc[i][j], bc * S[k]);
       if (R) o[j] = fmaf(alpha[c], R[(int64_t)c * Cin + k], o[j]);
     }
@@ -67,12 +81,13 @@ __global__ __launch_bounds__(THREADS) void gram_wgrad_kernel(
       const float w = sp[(int64_t)b * Cout + c];
       const int64_t m = am[(int64_t)b * Cout + c];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + tx * 4 + j;
+      for (int j = 0; j < RR; ++j) {
+        const int k = k0 + tx * RR + j;
         o[j] = fmaf(w, fmaxf(fmaf(load_elem(Y, m * Cin + k), s[k], t[k]), 0.f), o[j]);
       }
     }
-    *reinterpret_cast<float4 *>(dW + (int64_t)c * ldw + k0 + tx * 4) = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+    for (int j = 0; j < RR; ++j) dW[(int64_t)c * ldw + k0 + tx * RR + j] = o[j];
   }
 }
 
@@ -89,17 +104,17 @@ extern "C" int pcs_gram_wgrad(const float *G, const float *S, const float *W, in
   if (Cout % TILE || Cin % TILE || num_scenes <= 0 || ldw % 4 || ldw < Cin || ldw_in < Cin)
     return pcs_set_einval("pcs_gram_wgrad", "Cout/Cin must be multiples of 64, ldw >= Cin (multiple of 4)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid(Cin / TILE, Cout / TILE);
+  const dim3 grid(Cin / 32, Cout / 32);   // 32 x 32 tiles: enough blocks for the wide layer and conv5
   if (dtype == PCS_BF16)
-    hipLaunchKernelGGL(gram_wgrad_kernel<bf16_t>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
+    hipLaunchKernelGGL((gram_wgrad_kernel<bf16_t, 32>), grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
                        sp, am, reinterpret_cast<const bf16_t *>(Y), s, t, (int)num_scenes, Cout, Cin, R, alpha,
                        dW, ldw);
   else if (dtype == PCS_F32)
-    hipLaunchKernelGGL(gram_wgrad_kernel<float>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
+    hipLaunchKernelGGL((gram_wgrad_kernel<float, 32>), grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
                        sp, am, reinterpret_cast<const float *>(Y), s, t, (int)num_scenes, Cout, Cin, R, alpha,
                        dW, ldw);
   else if (dtype == PCS_FP8)   // the fp8 path's e4m3 a5 (max-pool rows' term)
-    hipLaunchKernelGGL(gram_wgrad_kernel<fp8_t>, grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
+    hipLaunchKernelGGL((gram_wgrad_kernel<fp8_t, 32>), grid, dim3(THREADS), 0, st, G, S, W, ldw_in, beta, gamma,
                        sp, am, reinterpret_cast<const fp8_t *>(Y), s, t, (int)num_scenes, Cout, Cin, R, alpha,
                        dW, ldw);
   else
