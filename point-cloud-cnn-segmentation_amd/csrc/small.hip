@@ -54,28 +54,38 @@ __global__ __launch_bounds__(THREADS) void conv1_fwd_kernel(pcs_gemm_args a, int
   for (int e = 0; e < EPC; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
   const int64_t r_begin = (int64_t)cis * tiles_per_chunk * C1_BM;
   const int64_t r_end = pcs_min64(r_begin + (int64_t)tiles_per_chunk * C1_BM, N);
-  for (int64_t r = r_begin + r0; r < r_end; r += RPP) {
-    const int64_t grow = scene * N + r;
-    float x[KD];
-    load_xrow<KD>(X, grow, x);
-    float v[EPC];
+  // four rows per thread per pass: their input loads are issued together (one dependent load
+  // -> compute -> store chain per row left the kernel waiting on memory 80 % of its cycles);
+  // the rows are still folded into the statistics in the same order
+  constexpr int U = 4;
+  for (int64_t r = r_begin + r0; r < r_end; r += U * RPP) {
+    float x[U][KD];
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      float acc = bias[e];
+    for (int u = 0; u < U; ++u)
+      if (r + u * RPP < r_end) load_xrow<KD>(X, scene * N + r + u * RPP, x[u]);
 #pragma unroll
-      for (int k = 0; k < KD; ++k) acc = fmaf(w[e][k], x[k], acc);
-      v[e] = acc;
-    }
-    const u32x4 packed = pack_chunk(v);
-    st16(Cg + grow * COLS + c0, packed);
-    unpack_chunk(packed, v);  // statistics of the stored (rounded) values
-    cnt += 1.f;
-    const float rn = 1.f / cnt;
+    for (int u = 0; u < U; ++u) {
+      if (r + u * RPP >= r_end) break;
+      const int64_t grow = scene * N + r + u * RPP;
+      float v[EPC];
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      const float d = v[e] - mean[e];
-      mean[e] = fmaf(d, rn, mean[e]);
-      m2[e] = fmaf(d, v[e] - mean[e], m2[e]);
+      for (int e = 0; e < EPC; ++e) {
+        float acc = bias[e];
+#pragma unroll
+        for (int k = 0; k < KD; ++k) acc = fmaf(w[e][k], x[u][k], acc);
+        v[e] = acc;
+      }
+      const u32x4 packed = pack_chunk(v);
+      st16(Cg + grow * COLS + c0, packed);
+      unpack_chunk(packed, v);  // statistics of the stored (rounded) values
+      cnt += 1.f;
+      const float rn = 1.f / cnt;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        const float d = v[e] - mean[e];
+        mean[e] = fmaf(d, rn, mean[e]);
+        m2[e] = fmaf(d, v[e] - mean[e], m2[e]);
+      }
     }
   }
   if (!a.stats) return;
