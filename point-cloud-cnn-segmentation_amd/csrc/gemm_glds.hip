@@ -736,44 +736,70 @@ __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, 
                                                             int Ncols, const int32_t *__restrict__ idx,
                                                             const float *__restrict__ coef, const float *__restrict__ Wp,
                                                             int64_t ldw, int P, float *__restrict__ stats, int cps) {
-  __shared__ int rows[PR_MAXC], srow[PR_MAXC];
-  __shared__ int sch[PR_MAXC];
+  // (row, channel) pairs sorted by row, then channel, as 64-bit keys row << 11 | channel:
+  // a bitonic sort in LDS (55 compare-exchange passes; the O(P^2) rank sort it replaces was
+  // most of this kernel's time)
+  __shared__ unsigned long long keys[PR_MAXC];
   const int b = blockIdx.y, part = blockIdx.z, parts = gridDim.z, tid = threadIdx.x;
   const int n = blockIdx.x * 256 + tid;
-  for (int c = tid; c < P; c += 256) rows[c] = idx[(int64_t)b * P + c];
+  int Pp = 1;
+  while (Pp < P) Pp <<= 1;
+  for (int c = tid; c < Pp; c += 256)
+    keys[c] = c < P ? ((unsigned long long)(uint32_t)idx[(int64_t)b * P + c] << 11) | (unsigned)c : ~0ull;
   __syncthreads();
-  for (int c = tid; c < P; c += 256) {   // stable rank sort by row
-    const int r = rows[c];
-    int rank = 0;
-    for (int q = 0; q < P; ++q) {
-      const int rq = rows[q];
-      rank += rq < r || (rq == r && q < c);
+  for (int k = 2; k <= Pp; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < Pp; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long x = keys[i], y = keys[ixj];
+          if ((x > y) == ((i & k) == 0)) { keys[i] = y; keys[ixj] = x; }
+        }
+      }
+      __syncthreads();
     }
-    srow[rank] = r;
-    sch[rank] = c;
   }
-  __syncthreads();
+  auto srow_at = [&](int q) { return (int)(keys[q] >> 11); };
+  auto sch_at = [&](int q) { return (int)(keys[q] & 2047u); };
   // this part's range [p0, p1): the nominal cut points moved forward to a row boundary
   auto cut = [&](int j) {
     int p = (int)((int64_t)j * P / parts);
-    while (p > 0 && p < P && srow[p] == srow[p - 1]) ++p;
+    while (p > 0 && p < P && srow_at(p) == srow_at(p - 1)) ++p;
     return p;
   };
   const int p0 = cut(part), p1 = cut(part + 1);
   if (n >= Ncols || p0 >= p1) return;
   float ds1 = 0.f, v = 0.f;
-  for (int p = p0; p < p1; ++p) {
-    const int c = sch[p];
-    v = fmaf(coef[(int64_t)b * P + c], Wp[(int64_t)c * ldw + n], v);
-    if (p + 1 == p1 || srow[p + 1] != srow[p]) {   // last pair of this row: apply
-      const int64_t o = (int64_t)srow[p] * Ncols + n;
-      if (load_elem(Yp, o) > 0.f) {
-        const float d = load_elem(dz, o) + v;
-        if constexpr (sizeof(T) == 2) dz[o] = (T)(pack2bf(d, 0.f) & 0xffffu);
-        else dz[o] = d;
-        ds1 += v;
+  // 8 pairs' coefficients and W entries are loaded together (a 64-pair range walked one load
+  // at a time made this kernel latency-bound); the sums still run in pair order
+  constexpr int U = 8;
+  for (int p = p0; p < p1; p += U) {
+    float cf[U], wv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cf[u] = 0.f;
+      wv[u] = 0.f;
+      if (p + u < p1) {
+        const int c = sch_at(p + u);
+        cf[u] = coef[(int64_t)b * P + c];
+        wv[u] = Wp[(int64_t)c * ldw + n];
       }
-      v = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = p + u;
+      if (q >= p1) break;
+      v = fmaf(cf[u], wv[u], v);
+      if (q + 1 == p1 || srow_at(q + 1) != srow_at(q)) {   // last pair of this row: apply
+        const int64_t o = (int64_t)srow_at(q) * Ncols + n;
+        if (load_elem(Yp, o) > 0.f) {
+          const float d = load_elem(dz, o) + v;
+          if constexpr (sizeof(T) == 2) dz[o] = (T)(pack2bf(d, 0.f) & 0xffffu);
+          else dz[o] = d;
+          ds1 += v;
+        }
+        v = 0.f;
+      }
     }
   }
   if (stats) stats[(((int64_t)b * cps + part) * Ncols + n) * 2] += ds1;

@@ -1,5 +1,5 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fused_bwd.py tests/test_gpu_gram.py tests/test_gpu_fp8.py > gpurun_out/t16.log 2>&1
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fused_bwd.py tests/test_gpu_gram.py tests/test_gpu_fp8.py tests/test_gpu_glds.py > gpurun_out/t16.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof16 -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-timing > gpurun_out/prof16.log 2>&1
