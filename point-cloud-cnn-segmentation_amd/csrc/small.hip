@@ -340,27 +340,47 @@ __global__ void pool_bwd_dw_kernel(pcs_pool_bwd_args a) {
 // dg = W_g^T csum; dz_g = dg*(g>0); bn_global backward from the B sparse entries.
 // Block: 64 channels k x 4 parts of the n reduction (fixed-order combine through LDS).
 constexpr int PBC_MAXB = 64;
-__global__ __launch_bounds__(256) void pool_bwd_coef_kernel(pcs_pool_bwd_args a) {
-  __shared__ float part[4][PBC_MAXB][64];
+// 16 parts of seg_conv1's 512 rows per column (1024 threads), 8 scenes per pass: each W entry is
+// loaded once per pass and feeds 8 accumulators (was 4 parts, one scene at a time: a 512-long
+// dependent load chain per thread on 16 workgroups)
+constexpr int PBC_PARTS = 16, PBC_SB = 8;
+__global__ __launch_bounds__(1024) void pool_bwd_coef_kernel(pcs_pool_bwd_args a) {
+  __shared__ float part[PBC_PARTS][PBC_SB][64];
+  __shared__ float dgall[PBC_MAXB][64];
   const int kk = threadIdx.x & 63, pr = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + kk;
   const int B = (int)a.num_scenes;
-  const int n0 = (int)((int64_t)a.Cs * pr / 4), n1 = (int)((int64_t)a.Cs * (pr + 1) / 4);
-  if (k < a.Cg) {
-    for (int b = 0; b < B; ++b) {
-      float dg = 0.f;
-      for (int n = n0; n < n1; ++n)
-        dg = fmaf(a.W_s1[(int64_t)n * a.ldw + a.col_off + k], a.csum[(int64_t)b * a.Cs + n], dg);
-      part[pr][b][kk] = dg;
+  const int n0 = (int)((int64_t)a.Cs * pr / PBC_PARTS), n1 = (int)((int64_t)a.Cs * (pr + 1) / PBC_PARTS);
+  for (int b0 = 0; b0 < B; b0 += PBC_SB) {
+    float dg[PBC_SB];
+#pragma unroll
+    for (int u = 0; u < PBC_SB; ++u) dg[u] = 0.f;
+    if (k < a.Cg) {
+      for (int n = n0; n < n1; ++n) {
+        const float w = a.W_s1[(int64_t)n * a.ldw + a.col_off + k];
+#pragma unroll
+        for (int u = 0; u < PBC_SB; ++u)
+          if (b0 + u < B) dg[u] = fmaf(w, a.csum[(int64_t)(b0 + u) * a.Cs + n], dg[u]);
+      }
     }
+#pragma unroll
+    for (int u = 0; u < PBC_SB; ++u) part[pr][u][kk] = dg[u];
+    __syncthreads();
+    if (pr == 0) {
+      for (int u = 0; u < PBC_SB && b0 + u < B; ++u) {
+        float t = 0.f;
+        for (int q = 0; q < PBC_PARTS; ++q) t += part[q][u][kk];
+        dgall[b0 + u][kk] = t;
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (pr != 0 || k >= a.Cg) return;
   const double M = (double)(a.num_scenes * a.scene_rows);
   const double r = a.g_rstd[k], gm = a.g_gamma[k], mu = a.g_mean[k];
   double S1 = 0, S2 = 0, Sy = 0;
   for (int b = 0; b < B; ++b) {
-    const float dg = ((part[0][b][kk] + part[1][b][kk]) + part[2][b][kk]) + part[3][b][kk];
+    const float dg = dgall[b][kk];
     const float dz = a.g[(int64_t)b * a.Cg + k] > 0.f ? dg : 0.f;
     a.sp[(int64_t)b * a.Cg + k] = dz;  // scaled by alpha below
     S1 += dz;
@@ -1006,7 +1026,7 @@ extern "C" int pcs_pool_bwd(const pcs_pool_bwd_args *ap, pcs_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(pool_bwd_csum_kernel, dim3(blocks_for(a.num_scenes * a.Cs, 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(pool_bwd_dw_kernel, dim3(blocks_for((int64_t)a.Cs * a.Cg, 256)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(pool_bwd_coef_kernel, dim3(blocks_for(a.Cg, 64)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pool_bwd_coef_kernel, dim3(blocks_for(a.Cg, 64)), dim3(1024), 0, s, a);
   PCS_CHECK_LAUNCH();
   return 0;
 }
