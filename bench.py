@@ -10,7 +10,12 @@ activation a5 and global_feat's GEMMs in e4m3 on MX-scaled MFMA.
 Prints ONE JSON line (rank 0).  value = points processed by all ranks / max-over-ranks
 wall time of K steps (bracketed by barrier + synchronize).  ``roofline`` describes the
 dominant kernel from HIP events recorded on its launch stream inside the timed region;
-``cpu_baseline`` times the numpy oracle (the reference restated) on the host cores.
+``cpu_baseline`` times the pure-PyTorch CPU restatement of the reference step (and the numpy
+oracle) on the host cores.
+
+``--gpus N`` with N > 1 and no torch.distributed environment starts N ranks itself (a
+torch.distributed.run child, one process per GPU, RCCL); under a launcher WORLD_SIZE must equal
+N, and an RCCL run refuses to start with fewer than N visible GPUs.
 """
 from __future__ import annotations
 
@@ -63,22 +68,35 @@ TAG_KERNEL = {
 GRAM_TILE_FRACTION = 10.0 / 16.0   # upper 256-tiles of the symmetric 1024 x 1024 Gram
 
 
+def lib_sha16():
+    """First 16 hex digits of the SHA-256 of the HIP library this process runs (the build a
+    PMC summary must describe for its counters to be quoted against this run)."""
+    import hashlib
+    path = os.path.join(REPO, "point-cloud-cnn-segmentation_amd", "csrc", "libpcs.so")
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_traffic(tag, dtype, workload, points):
     """HBM bytes per launch of the kernel behind ``tag``, from a committed PMC summary
     (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tools/profile_round.sh) whose
-    recorded workload, dtype and points per step match this run; None when no such profile
-    exists (the number would describe a different launch)."""
+    recorded workload, dtype, points per step AND libpcs.so hash match this run; None when no
+    such profile exists (the number would describe a different launch or another build)."""
     import glob
     sym = TAG_KERNEL.get(tag)
     if sym is None:
         return None
     sym = sym.format(f="true" if dtype == "fp8" else "false")
+    lib = lib_sha16()
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)
         meta = rec.get("meta") if isinstance(rec, dict) else None
-        if not meta or (meta.get("workload"), meta.get("dtype"), meta.get("points_per_step")) != \
-                (workload, dtype, points):
+        if not meta or (meta.get("workload"), meta.get("dtype"), meta.get("points_per_step"),
+                        meta.get("lib_sha16")) != (workload, dtype, points, lib) or lib is None:
             continue
         ent = rec.get("kernels", {}).get(sym, {})
         if "hbm_bytes_per_launch" in ent:
@@ -161,34 +179,87 @@ def northstar_64(kernels, M, dtype):
             "hbm_frac": round(t_hbm / ms, 4)}
 
 
-def cpu_baseline(max_seconds=12.0):
-    """Numpy oracle (fp32) fwd+bwd on the reference's CPU-runnable case (B=4, N=4096, C=2)."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import pointnet_oracle as orc
+def _cpu_threads():
+    """(threads used, cores in this process's affinity mask, BLAS pool size)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    threads = min(aff, omp) if omp > 0 else aff
+    blas = None
     try:
         from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()
-                     if i.get("user_api") == "blas"] or [1])
+        blas = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [0]) or None
     except Exception:  # pragma: no cover
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        pass
+    return threads, aff, blas
+
+
+def cpu_baseline(max_seconds=10.0):
+    """the pure-PyTorch CPU restatement of the reference step (oracle/torch_cpu.py,
+    pinned to the reference goldens) in fp32, train mode, dropout on, fwd + weighted CE + bwd, on
+    the reference's CPU-runnable case (B=4, N=4096, C=2), torch threads = the cores this process
+    may use.  Also times the numpy oracle (``numpy`` field) for continuity with earlier rounds."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pointnet_oracle as orc
+    import torch_cpu as tc
+    threads, aff, blas = _cpu_threads()
     B, N = 4, 4096
     sd = orc.init_params(2, 7)
     pts, lab, _ = synthetic_batch(1234, [N] * B, 2, grid=32)
-    masks = orc.dropout_masks(3, B * N)
     w = np.array([0.5, 1.5], np.float32)
-    orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32)   # warm-up
-    t0 = time.perf_counter()
-    steps = 0
-    while True:
-        orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= max_seconds or steps >= 20:
-            break
-    return {"value": B * N * steps / el / 1e6, "unit": "M points/s", "cores": int(cores),
-            "kind": "port",
-            "sample": f"numpy fp32 oracle fwd+CE+bwd, B=4 x N=4096 (32^3 lattice), C=2, "
-                      f"{steps} steps in {el:.1f}s after 1 warm-up"}
+
+    def timed(fn):
+        fn()   # warm-up
+        t0 = time.perf_counter()
+        steps = 0
+        while True:
+            fn()
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= max_seconds or steps >= 20:
+                return steps, el
+
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        T = tc.to_tensors(sd)
+        xt, yt, wt = torch.from_numpy(pts), torch.from_numpy(lab), torch.from_numpy(w)
+        steps, el = timed(lambda: tc.train_step(T, xt, yt, wt))
+    finally:
+        torch.set_num_threads(prev)
+    masks = orc.dropout_masks(3, B * N)
+    nsteps, nel = timed(lambda: orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32))
+    return {"value": B * N * steps / el / 1e6, "unit": "M points/s", "cores": int(threads),
+            "kind": "port", "affinity_cores": int(aff), "torch_threads": int(threads),
+            "sample": f"pure-PyTorch CPU restatement of the reference step (oracle/torch_cpu.py: "
+                      f"ATen conv1d / batch_norm / dropout / cross_entropy + autograd, fp32, train "
+                      f"mode, dropout on), B=4 x N=4096 (32^3 lattice), C=2, {steps} steps in "
+                      f"{el:.1f}s after 1 warm-up, {threads} torch threads",
+            "numpy": {"value": B * N * nsteps / nel / 1e6, "unit": "M points/s",
+                      "blas_threads": blas,
+                      "sample": f"numpy fp32 oracle fwd+CE+bwd, same batch, {nsteps} steps in {nel:.1f}s"}}
+
+
+def launch_ranks(n):
+    """``--gpus N`` (N > 1) without a torch.distributed environment: start N ranks, one process
+    per GPU, with torch.distributed.run as a CHILD process and return its exit code.  This
+    process never initialises the GPU (device_count() does not, on this image) and never execs."""
+    import socket
+    import subprocess
+    backend = os.environ.get("PCS_DIST_BACKEND", "nccl")
+    have = torch.cuda.device_count()
+    if backend == "nccl" and have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs for one RCCL rank per GPU, found {have}",
+              file=sys.stderr)
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -208,15 +279,28 @@ def main():
                          "padded on the device inside every timed step")
     ap.add_argument("--occupancy", type=float, default=0.02)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"{world}-rank run as {args.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
     # RCCL ("nccl") is the data-parallel backend; PCS_DIST_BACKEND=gloo rehearses the N>1
     # code path with several ranks sharing the GPUs a box has (device = local rank mod count)
     backend = os.environ.get("PCS_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
     if backend == "gloo":
-        local %= max(1, torch.cuda.device_count())
+        local %= max(1, ndev)
+    elif local >= ndev:
+        print(f"bench.py: rank {rank} (local {local}) has no GPU of its own: {ndev} visible",
+              file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -297,10 +381,16 @@ def main():
     loss_v = float(loss.item())
 
     M = B * N
+    devices = [local]
     if world > 1:
         t = torch.tensor([real_points], device=dev, dtype=torch.int64)
         dist.all_reduce(t)
         real_points = int(t.item())
+        d = torch.zeros(world, dtype=torch.int64, device=dev)
+        d[rank] = local
+        dist.all_reduce(d)
+        devices = [int(v) for v in d.tolist()]
+        world = dist.get_world_size()
     total_points = real_points * args.steps
     roof = None
     kernels, full = {}, {}
@@ -359,7 +449,9 @@ def main():
                       "training step: forward + weighted CE + backward + Adam)",
             "value": round(total_points / el / 1e6, 3),
             "unit": "M points/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world, "world_size": world, "rank_devices": devices,
+            "dist_backend": backend if world > 1 else None,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp8 e4m3 (global_feat, a5) + bf16" if args.dtype == "fp8" else args.dtype,
@@ -381,6 +473,7 @@ def main():
             "step_roofline": step_roofline(M, C, args.dtype, el / args.steps * 1e3),
             "northstar_64x64": northstar_64(full, M, args.dtype) if kernels else None,
             "cpu_baseline": cpu,
+            "lib_sha16": lib_sha16(),
         }
         print(json.dumps(rec))
     if world > 1:

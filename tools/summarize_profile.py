@@ -54,6 +54,10 @@ def bench_meta(argv):
     ap.add_argument("--workload", default="cfg2")
     a, _ = ap.parse_known_args(argv)
     meta = {"workload": a.workload, "dtype": a.dtype, "command": "bench.py " + " ".join(argv)}
+    # the build the counters describe: bench.py quotes "traffic" only for this exact libpcs.so
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import lib_sha16
+    meta["lib_sha16"] = lib_sha16()
     if a.workload == "cfg2":
         meta["points_per_step"] = a.scenes * a.grid ** 3
     return meta
