@@ -431,7 +431,8 @@ int pcs_gram_wgrad(const float *G, const float *S, const float *W, int64_t ldw_i
  *   c = W^T beta [Cin] (fp32),  H = W^T diag(gamma) W [Cin, Cin] (dtype).
  * Two pcs_gemm launches then give dA without reading y (conv5 backward, P:110 at P:254).
  * WsT (and alpha) may be NULL: global_feat's dz is the sparse max-pool gradient, whose rows
- * pcs_gemm adds in its EPI_DGRAD epilogue (pool_w).
+ * pcs_gemm adds in its EPI_DGRAD epilogue (pool_w).  c (and beta) may be NULL when the caller
+ * forms the constant row itself (pcs_dgrad_wgrad_folded's per-scene cvec).
  */
 int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const float *alpha,
                 const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
@@ -496,6 +497,11 @@ int pcs_argmax(const float *logits, int64_t ld, int64_t M, int32_t C, int64_t *o
 int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale,
                         float *out, int64_t out_stride_rows, int64_t row_len,
                         pcs_stream_t stream);
+
+/* grouped form, one launch: out[g*len + i] = scale * sum_s partial[(g*nslabs + s)*len + i] for
+ * g < ngroups (e.g. per-scene sums of scene-aligned chunk partials), fixed order */
+int pcs_reduce_partials_grouped(const float *partial, int64_t ngroups, int64_t nslabs, int64_t len,
+                                float scale, float *out, pcs_stream_t stream);
 
 /* fp32 [rows, cols] (row stride ldw) -> dtype copies W ([rows, cols] contiguous) and W^T
  * ([cols, rows]); either output may be NULL */

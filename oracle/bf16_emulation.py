@@ -79,19 +79,30 @@ def _stats(Y):
     return mean, var / Y.shape[0]
 
 
-def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_logits=False):
+def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_logits=False, exact=(), pool_idx=None, info=None):
     """One reference training step (without the optimizer).  Returns (loss, grads) with
     grads keyed by state-dict parameter name (float64 arrays); conv biases that BN cancels
-    are returned as zeros (analytically ~0 in every path)."""
-    R = round_bf16 if store in ("bf16", "fp8") else (lambda a: np.ascontiguousarray(a, dtype=F32))
+    are returned as zeros (analytically ~0 in every path).
+
+    ``exact``: names of rounding sites left in fp32 (the ablation of tools/bf16_ablation.py):
+    "W" (every GEMM weight), "Y" (stored pre-BN outputs), "A" (GEMM input activations except
+    a5), "a5", "dz" (stored BN-output gradients), "dy" (GEMM operands dy), "DZ5", "H" (folded
+    global_feat H), "fold5" (conv5's folded operands), "dA2", "dA4".  ``pool_idx`` [B, 1024]
+    replaces the max-pool's argmax rows (the value pooled is still this path's own); a dict
+    ``info`` receives this step's own argmax rows under "pool_idx"."""
+    R0 = round_bf16 if store in ("bf16", "fp8") else (lambda a: np.ascontiguousarray(a, dtype=F32))
+    exact = set(exact)
+
+    def R(a, site=None):
+        return np.ascontiguousarray(a, dtype=F32) if site in exact else R0(a)
     fp8 = store == "fp8"
     B, N, D = x.shape
     M = B * N
     X = x.reshape(M, D).astype(F32)
     W = {n: _w(sd, n, F32) for n in ("conv1", "conv2", "conv3", "conv4", "conv5", "global_feat",
                                     "seg_conv1", "seg_conv2", "seg_conv3", "seg_conv4")}
-    Wr = {n: R(W[n]) for n in ("conv2", "conv3", "conv4", "conv5", "global_feat", "seg_conv2", "seg_conv3")}
-    Wr["seg_conv1_l"] = R(W["seg_conv1"][:, :64])
+    Wr = {n: R(W[n], "W") for n in ("conv2", "conv3", "conv4", "conv5", "global_feat", "seg_conv2", "seg_conv3")}
+    Wr["seg_conv1_l"] = R(W["seg_conv1"][:, :64], "W")
     if fp8:
         Wr["global_feat"] = quant_rows_e4m3(W["global_feat"])
     Wg1 = np.ascontiguousarray(W["seg_conv1"][:, 64:])     # global half: fp32 (pcs_scene_gemv)
@@ -116,39 +127,41 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
         return a * k if k is not None else a
 
     def layer(A, bn, Wt):
-        Y = R(A @ Wt.T)                                  # stored pre-BN (bias cancels in BN)
+        Y = R(A @ Wt.T, "Y")                                  # stored pre-BN (bias cancels in BN)
         cache[bn + "_st"] = bn_coef(bn, *_stats(Y))
         return Y
 
     # ---------------- forward (P:103-131)
-    Y1 = R(X @ W["conv1"].T)
+    Y1 = R(X @ W["conv1"].T, "Y")
     cache["bn1_st"] = bn_coef("bn1", *_stats(Y1))
-    Y2 = layer(R(act(Y1, "bn1")), "bn2", Wr["conv2"])
-    A2 = R(act(Y2, "bn2"))                               # point_feat (conv3 / seg_conv1 input)
+    Y2 = layer(R(act(Y1, "bn1"), "A"), "bn2", Wr["conv2"])
+    A2 = R(act(Y2, "bn2"), "A")                               # point_feat (conv3 / seg_conv1 input)
     Y3 = layer(A2, "bn3", Wr["conv3"])
-    A3 = R(act(Y3, "bn3"))
+    A3 = R(act(Y3, "bn3"), "A")
     Y4 = layer(A3, "bn4", Wr["conv4"])
-    A4 = R(act(Y4, "bn4"))
+    A4 = R(act(Y4, "bn4"), "A")
     y5 = A4 @ Wr["conv5"].T                              # fp32 accumulators
     cache["bn5_st"] = bn_coef("bn5", *_stats(y5))
-    a5 = round_e4m3(act(y5, "bn5")) if fp8 else R(act(y5, "bn5"))
+    a5 = round_e4m3(act(y5, "bn5")) if fp8 else R(act(y5, "bn5"), "a5")
     del y5
     yg = a5 @ Wr["global_feat"].T
     mg, vg = _stats(yg)
     sg, tg = bn_coef("bn_global", mg, vg)
     cache["bn_global_st"] = (sg, tg)
     zg = (yg * sg + tg).reshape(B, N, -1)
-    idx = zg.argmax(axis=1)                              # first max of relu(bn(y)) (P:114)
+    idx = zg.argmax(axis=1) if pool_idx is None else np.asarray(pool_idx)   # first max (P:114)
+    if info is not None:
+        info["pool_idx"] = zg.argmax(axis=1)
     g = np.maximum(np.take_along_axis(zg, idx[:, None, :], 1)[:, 0, :], 0).astype(np.float64)
     ysel = np.take_along_axis(yg.reshape(B, N, -1), idx[:, None, :], 1)[:, 0, :].astype(np.float64)
     del yg, zg
     sb = g @ Wg1.T.astype(np.float64)                    # per-scene bias (P:117-123), centred
     sb -= sb.mean(axis=0)
-    Ys1 = R((A2 @ Wr["seg_conv1_l"].T).reshape(B, N, -1) + sb[:, None, :].astype(F32)).reshape(M, -1)
+    Ys1 = R((A2 @ Wr["seg_conv1_l"].T).reshape(B, N, -1) + sb[:, None, :].astype(F32), "Y").reshape(M, -1)
     cache["bn_seg1_st"] = bn_coef("bn_seg1", *_stats(Ys1))
-    As1 = R(act(Ys1, "bn_seg1", k1))
+    As1 = R(act(Ys1, "bn_seg1", k1), "A")
     Ys2 = layer(As1, "bn_seg2", Wr["seg_conv2"])
-    As2 = R(act(Ys2, "bn_seg2", k2))
+    As2 = R(act(Ys2, "bn_seg2", k2), "A")
     Ys3 = layer(As2, "bn_seg3", Wr["seg_conv3"])
     as3 = act(Ys3, "bn_seg3")                            # head: fp32
     logits = as3 @ W["seg_conv4"].T + sd["seg_conv4.bias"].astype(F32)
@@ -187,11 +200,11 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
         S2 = (dz * xh).sum(axis=0)
         grads[f"{bn}.weight"], grads[f"{bn}.bias"] = S2, S1
         al = gam[bn] * rstd
-        dy = (al * (R(dz).astype(np.float64) - S1 / M - xh * (S2 / M))).astype(F32)
+        dy = (al * (R(dz, "dz").astype(np.float64) - S1 / M - xh * (S2 / M))).astype(F32)
         return dy, S1, S2
 
     def conv_back(conv, dy, Ain, Wt, need_dx=True):
-        dyr = R(dy)
+        dyr = R(dy, "dy")
         grads[f"{conv}.weight"] = (dyr.T.astype(np.float64) @ Ain)[:, :, None]
         grads[f"{conv}.bias"] = np.zeros(dy.shape[1])
         return dyr @ Wt if need_dx else None
@@ -203,12 +216,12 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     dys1, _, _ = bn_back(dA, Ys1, "bn_seg1", k1)
     del dA
     # seg_conv1 = local GEMM + per-scene global GEMV: dW = [dy^T A2 | sum_b csum_b g_b^T]
-    dyr = R(dys1)
+    dyr = R(dys1, "dy")
     dWl = dyr.T.astype(np.float64) @ A2
     csum = dys1.reshape(B, N, -1).sum(axis=1, dtype=np.float64)    # fp32 sums (pcs_pool_bwd)
     grads["seg_conv1.weight"] = np.concatenate([dWl, csum.T @ g], axis=1)[:, :, None]
     grads["seg_conv1.bias"] = np.zeros(dys1.shape[1])
-    dA2 = R(dyr @ Wr["seg_conv1_l"])                                  # stored (conv3 addend)
+    dA2 = R(dyr @ Wr["seg_conv1_l"], "dA2")                                  # stored (conv3 addend)
     del dys1, dyr
     # max-pool + bn_global backward (sparse rows), folded dA5 = a5 H + c + sparse
     dg = csum @ Wg1.astype(np.float64)                                # [B, 1024]
@@ -223,7 +236,7 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     gc = -al * rstd * S2 / M
     bc = -al * S1 / M - gc * mean
     Wgr = Wr["global_feat"].astype(np.float64)
-    H = quant_rows_e4m3((Wgr.T * gc) @ Wgr) if fp8 else R((Wgr.T * gc) @ Wgr)
+    H = quant_rows_e4m3((Wgr.T * gc) @ Wgr) if fp8 else R((Wgr.T * gc) @ Wgr, "H")
     cvec = (Wgr.T @ bc).astype(F32)
     dA5 = a5 @ H + cvec
     rows = idx + (np.arange(B) * N)[:, None]
@@ -234,7 +247,7 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     dz5 = np.where(a5 > 0, dA5, F32(0))
     del dA5
     S1_5 = dz5.sum(axis=0, dtype=np.float64)
-    DZ5 = R(dz5)
+    DZ5 = R(dz5, "DZ5")
     del dz5
     G5 = (a5.T @ a5).astype(np.float64)                               # fp32 accumulation
     S5 = a5.sum(axis=0, dtype=np.float64)
@@ -254,10 +267,10 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     al5 = gam["bn5"] * rstd
     ga5 = -al5 * rstd * S2_5 / M
     be5 = -al5 * S1_5 / M - ga5 * mean
-    Ws = R(al5[:, None] * W5r)
-    h4 = R((W5r.T * ga5) @ W5r)
+    Ws = R(al5[:, None] * W5r, "fold5")
+    h4 = R((W5r.T * ga5) @ W5r, "fold5")
     c5 = (W5r.T @ be5).astype(F32)
-    dA4 = R(DZ5 @ Ws + c5) + A4 @ h4
+    dA4 = R(DZ5 @ Ws + c5, "dA4") + A4 @ h4
     del DZ5
     G4 = A4.T.astype(np.float64) @ A4
     S4 = A4.sum(axis=0, dtype=np.float64)
@@ -268,7 +281,7 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     dy, _, _ = bn_back(dA, Y3, "bn3")
     dA = conv_back("conv3", dy, A2, Wr["conv3"]) + dA2
     dy, _, _ = bn_back(dA, Y2, "bn2")
-    A1 = R(act(Y1, "bn1"))
+    A1 = R(act(Y1, "bn1"), "A")
     dA = conv_back("conv2", dy, A1, Wr["conv2"])
     mean, rstd = cache["bn1"]
     s, t = cache["bn1_st"]
@@ -277,7 +290,7 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     S1 = dz.sum(axis=0, dtype=np.float64)
     S2 = (dz * xh).sum(axis=0)
     grads["bn1.weight"], grads["bn1.bias"] = S2, S1
-    dy = gam["bn1"] * rstd * (R(dz).astype(np.float64) - S1 / M - xh * (S2 / M))   # conv1 wgrad: fp32 dy
+    dy = gam["bn1"] * rstd * (R(dz, "dz").astype(np.float64) - S1 / M - xh * (S2 / M))   # conv1 wgrad: fp32 dy
     grads["conv1.weight"] = (dy.T @ X.astype(np.float64))[:, :, None]
     grads["conv1.bias"] = np.zeros(64)
     if return_logits:

@@ -118,6 +118,7 @@ SIGNATURES = [
     ("pcs_ce_weight_sum", ct.c_int, [_vp, _i64, _vp, _i32, _vp, _vp, _vp]),
     ("pcs_dropout_bits", ct.c_int, [ct.c_uint64, ct.c_uint64, _i64, _i32, _f, _vp, _vp]),
     ("pcs_reduce_partials", ct.c_int, [_vp, _i64, _i64, _f, _vp, _i64, _i64, _vp]),
+    ("pcs_reduce_partials_grouped", ct.c_int, [_vp, _i64, _i64, _i64, _f, _vp, _vp]),
     ("pcs_cast_weight", ct.c_int, [_vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     ("pcs_adam", ct.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _f, _i64, _vp]),
     ("pcs_colstats_geometry", _i64, [_i64, _i64, _i32, ct.POINTER(_i32)]),

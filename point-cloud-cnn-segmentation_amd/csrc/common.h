@@ -171,6 +171,10 @@ bool pcs_gemm_wres_applicable(const pcs_gemm_args &a);
 int pcs_gemm_wres_launch(const pcs_gemm_args &g, int64_t rows_per_chunk, hipStream_t s);
 int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                          hipStream_t s);
+// fused seg_conv2 / seg_conv3 input + weight gradient (fused_seg.hip)
+bool pcs_seg_bwd_applicable(const pcs_gemm_args &a);
+int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a);
+int pcs_seg_bwd_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);
 // wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)
 bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a);
 int pcs_wgrad_big_splits(const pcs_wgrad_args &a);

@@ -748,6 +748,7 @@ int launch_bn(const pcs_gemm_args &a, float *wpart, int64_t rps, hipStream_t s) 
 // 4.96 vs 4.73 ms, seg_conv2 12.8 vs 12.6 ms: 2 TB/s, latency-bound at one workgroup per
 // CU with the dy slab staged once per column block), so they stay on the pair.
 struct BnShape { int cout, cin, cb, ms; };
+// (seg_conv2 and seg_conv3 now go to the LDS-DMA stream of fused_seg.hip instead)
 constexpr BnShape kBnShapes[] = {{64, 64, 64, 64}, {128, 64, 64, 64}};
 
 const BnShape *bn_shape(int K, int Ncols) {
@@ -760,6 +761,10 @@ const BnShape *bn_shape(int K, int Ncols) {
 
 extern "C" int64_t pcs_dgrad_wgrad_bn_workspace(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_dgrad_wgrad_bn_workspace", "bad geometry");
+  if (pcs_seg_bwd_applicable(*a)) {   // seg_conv2 / seg_conv3: LDS-DMA stream (fused_seg.hip)
+    pcs_seg_bwd_geometry(a);
+    return (int64_t)a->num_scenes * a->chunks_per_scene * a->K * a->Ncols * 4;
+  }
   const BnShape *sh = bn_shape(a->K, a->Ncols);
   if (a->dtype != PCS_BF16 || !sh || (a->flags & PCS_FLAG_GENERIC))
     return pcs_set_einval("pcs_dgrad_wgrad_bn_workspace",
@@ -786,6 +791,12 @@ extern "C" int pcs_dgrad_wgrad_bn(const pcs_gemm_args *ap, float *partial, float
     return pcs_set_einval("pcs_dgrad_wgrad_bn", "missing operand (A, A2, pa, pb, pc, W, C, Yp, es, et, emean, "
                                                 "erstd, stats)");
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31) return pcs_set_einval("pcs_dgrad_wgrad_bn", "M must be < 2^31");
+  if (pcs_seg_bwd_applicable(a)) {
+    const int rc = pcs_seg_bwd_launch(a, partial, reinterpret_cast<hipStream_t>(stream));
+    if (rc) return rc;
+    const int nslab = (int)(a.num_scenes * a.chunks_per_scene);
+    return pcs_reduce_partials(partial, nslab, (int64_t)a.K * a.Ncols, 1.0f, dW, ldw ? ldw : a.Ncols, a.Ncols, stream);
+  }
   const BnShape *sh = bn_shape(a.K, a.Ncols);
   const int64_t rps = ((a.scene_rows + a.chunks_per_scene - 1) / a.chunks_per_scene + sh->ms - 1) / sh->ms * sh->ms;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

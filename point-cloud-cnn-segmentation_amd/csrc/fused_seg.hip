@@ -1,0 +1,465 @@
+// Fused input + weight gradient of seg_conv2 (512 -> 256) and seg_conv3 (256 -> 128)
+// (autograd of P:125-127 at P:254), on an LDS-DMA stream:
+//
+//   dy   = alpha * dZ + beta + gamma * Y                 ([M, COUT], bn_seg{2,3} backward)
+//   g    = dy . W                                        ([M, CIN])
+//   dz'  = (es * Yp + et > 0) * keep * ks * g             (stored; S1 = sum dz', S2 = sum dz' Yp)
+//   dW  += dy^T . x,   x = relu(es * Yp + et) * keep * ks ([COUT, CIN])
+//
+// Separately (pcs_gemm DGRAD + pcs_wgrad) the pair reads dZ, Y and Yp twice and measured
+// 10.4 ms (seg_conv2) / 4.6 ms (seg_conv3) at cfg2, 4.1-4.3 TB/s each.  Here one pass moves
+// dZ, Y, Yp and the dropout bits in and dz' out.
+//
+// * A workgroup (8 waves) owns a CB = 128 column block of CIN for a scene-aligned row slice:
+//   the CIN / CB workgroups of a slice are consecutive, so they run on one XCD and the dZ / Y
+//   rows they all stream come from that XCD's L2 after the first read.
+// * Rows stream in MS = 32-row steps through an NST-stage LDS ring filled by LDS-DMA
+//   (global_load_lds): dZ and Y (COUT wide), the block's Yp (128 wide) and its dropout bits.
+//   Every wave issues the same number of pieces per step (5 or 3 of 1 KB, plus one 256-B
+//   piece of the bits), always -- past the slice end the rows are clamped and the data never
+//   read -- so one compile-time vmcnt count serves every wave and every step.  The 16-B slots
+//   of an LDS row hold the source chunks XOR-permuted by (row & 15) (the permutation is put on
+//   the DMA source address, since the DMA writes LDS linearly): the fragment reads and the
+//   transposed reads below are then bank-conflict free.
+// * Per step: the transform of step t+1 (dy, in place over its dZ slab; x into a double
+//   buffer) by all 512 threads, each element once; the input gradient of step t from the
+//   registers' W^T block (loaded once) and dy fragments; the weight gradient of step t from
+//   transposed reads (ds_read_b64_tr_b16) of dy and x; then the epilogue in registers (mask,
+//   S1 / S2, 16-B stores widened with v_permlane16_swap).  Two barriers per step.
+// * dW partial per workgroup (fp32, the slice's slab) and per-slice S1 / S2, reduced by the
+//   caller's pcs_reduce_partials as pcs_dgrad_wgrad_bn's other shapes.
+#include "common.h"
+
+namespace {
+
+constexpr int THREADS = 512;
+constexpr int CB = 128;   // CIN columns per workgroup
+constexpr int MS = 32;    // rows per step
+
+template <int COUT> struct SegCfg {
+  static constexpr int NST = COUT == 256 ? 3 : 4;          // ring stages
+  static constexpr int DZB = MS * COUT * 2;                 // raw dZ / Y slab bytes (rows unpadded)
+  static constexpr int YPB = MS * CB * 2;                   // raw Yp slab (XOR-swizzled slots)
+  static constexpr int MKB = MS * CB / 8;                   // dropout bits (512 B)
+  static constexpr int STAGE = 2 * DZB + YPB + MKB;
+  static constexpr int DYR = COUT * 2 + 32;                 // dy row stride (32-B pad, prow rows)
+  static constexpr int XR = CB * 2 + 32;                    // x row stride
+  static constexpr int OFF_DY = NST * STAGE;                // dy [MS][DYR]
+  static constexpr int OFF_X = OFF_DY + MS * DYR;           // x [MS][XR]
+  static constexpr int OFF_CF = OFF_X + MS * XR;            // alpha | beta | gamma [COUT], es | et [CB]
+  static constexpr int BYTES = OFF_CF + (3 * COUT + 2 * CB) * 4;
+  static_assert(BYTES <= 160 * 1024, "LDS budget");
+  static constexpr int KS = COUT / 32;                      // dgrad k-steps (32 deep)
+  static constexpr int OBW = COUT / 128;                    // wgrad 16-row output tiles per wave
+  static constexpr int SPR = COUT / 8;                      // 16-B slots per dZ row
+  static constexpr int DZP = DZB / 1024;                    // 1-KB pieces per dZ slab
+  static constexpr int YPP = YPB / 1024;                    // 1-KB pieces per Yp slab (8)
+  static constexpr int NPW = (2 * DZP + YPP) / 8;           // 1-KB pieces per wave per step
+  static_assert((2 * DZP + YPP) % 8 == 0, "uniform pieces per wave");
+  static constexpr int VM_STEP = NPW + 1;                   // vector-memory loads per wave per step
+  static constexpr int DY_RPT = MS * SPR / THREADS;         // dy slots per thread per step
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+PCS_DEV int xcd_remap(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+// LDS-DMA: 64 lanes x 16 B (or x 4 B) from sbase + voff (per lane) to lds_dst + lane * size
+PCS_DEV void glds16(const char *sbase, uint32_t voff, char *lds_dst) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t *)lds_dst;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(m0v)
+               : "memory");
+}
+PCS_DEV void glds4(const char *sbase, uint32_t voff, char *lds_dst) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t *)lds_dst;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(m0v)
+               : "memory");
+}
+template <int N> PCS_DEV void wait_vm() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+PCS_DEV void barrier_lds() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS layouts.  The raw ring slabs are written by LDS-DMA (linear per piece): dZ / Y rows stay
+// unpadded (the transform reads them lane-linearly, conflict free); Yp's 16-B slots are
+// XOR-permuted by (row & 15) on the DMA source address, so the epilogue's 8-B reads of 16 rows
+// at one column hit 16 distinct slots.  dy and x are written by the transform, so they get the
+// layout of fused_bwd.hip: rows padded by 32 B and permuted (row bits 2 <-> 3), which makes the
+// ds_read_b128 fragment reads and the transposed ds_read_b64_tr_b16 reads conflict free.
+PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+PCS_DEV int fyp(int row) { return row & 15; }
+
+PCS_DEV bf16x8 tr_frag2(const char *p0, const char *p1) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)p0);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)p1);
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
+  const float4 x = *reinterpret_cast<const float4 *>(p);
+  const float4 y = *reinterpret_cast<const float4 *>(p + 4);
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
+PCS_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+PCS_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+template <int COUT, int CIN, bool MASK>
+__global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float *__restrict__ wpart,
+                                                          int64_t rows_per_split) {
+  typedef SegCfg<COUT> F;
+  constexpr int NBLK = CIN / CB;
+  __shared__ __attribute__((aligned(16))) char lds[F::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // (divisions by runtime values run on the VALU: the results are made provably uniform, so
+  // the DMA bases below stay in SGPRs instead of waterfall loops around every piece)
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = __builtin_amdgcn_readfirstlane(L / NBLK), n0 = __builtin_amdgcn_readfirstlane((L % NBLK) * CB);
+  const int sps = a.chunks_per_scene;
+  const int scene = __builtin_amdgcn_readfirstlane(chunk / sps), sis = __builtin_amdgcn_readfirstlane(chunk % sps);
+  const int64_t N = a.scene_rows;
+  const int64_t lo = (int64_t)sis * rows_per_split;
+  const int64_t hi = pcs_min64(lo + rows_per_split, N);
+  const int64_t sbase = (int64_t)scene * N;
+  const int nsteps = (int)((hi - lo + MS - 1) / MS);   // >= 1 (no empty slices)
+  const char *dZg = reinterpret_cast<const char *>(a.A);
+  const char *Yg = reinterpret_cast<const char *>(a.A2);
+  const char *Ypg = reinterpret_cast<const char *>(a.Yp) + n0 * 2;
+  const char *Mkg = MASK ? reinterpret_cast<const char *>(a.c_mask) + n0 / 8 : nullptr;
+  const bf16_t *Wt = reinterpret_cast<const bf16_t *>(a.W);   // W^T [CIN][COUT]
+  bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
+  const float ks = MASK ? a.c_keep_scale : 1.f;
+
+  // ---- DMA of step s into ring stage s % NST.  Piece j = wid + 8 i of the step: dZ [0, DZP),
+  // Y [DZP, 2 DZP), Yp [2 DZP, 2 DZP + YPP), then one dword piece of the dropout bits (waves
+  // 0 / 1 take its two halves; the others repeat them, writing the same bytes, so that every
+  // wave issues the same count; without bits they read Yp's rows, never used).  Per-lane
+  // offsets relative to the step's first row; rows past the slice clamp to its last row.
+  auto piece_off = [&](int i, int lastr) -> uint32_t {
+    const int j = wid + 8 * i;
+    if (j < 2 * F::DZP) {
+      const int pj = j < F::DZP ? j : j - F::DZP;
+      const int r = pj * (1024 / (COUT * 2)) + lane / F::SPR;
+      return (uint32_t)(min(r, lastr) * COUT * 2 + (lane % F::SPR) * 16);
+    }
+    const int r = (j - 2 * F::DZP) * 4 + (lane >> 4);
+    return (uint32_t)(min(r, lastr) * CIN * 2 + (((lane & 15) ^ fyp(r)) << 4));
+  };
+  auto mask_off = [&](int lastr) -> uint32_t {
+    const int r = 16 * (wid & 1) + (lane >> 2);
+    return (uint32_t)(min(r, lastr) * (MASK ? CIN / 8 : CIN * 2) + (lane & 3) * 4);
+  };
+  uint32_t voff[F::NPW + 1];
+#pragma unroll
+  for (int i = 0; i < F::NPW; ++i) voff[i] = piece_off(i, MS - 1);
+  voff[F::NPW] = mask_off(MS - 1);
+  auto dma_step = [&](int s) {
+    char *st = lds + (s % F::NST) * F::STAGE;
+    const int64_t m0 = pcs_min64(lo + (int64_t)s * MS, hi - 1);
+    const int lastr = (int)pcs_min64(hi - 1 - m0, MS - 1);
+    uint32_t vo[F::NPW + 1];
+    if (lastr == MS - 1) {   // uniform: a full step
+#pragma unroll
+      for (int i = 0; i <= F::NPW; ++i) vo[i] = voff[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < F::NPW; ++i) vo[i] = piece_off(i, lastr);
+      vo[F::NPW] = mask_off(lastr);
+    }
+#pragma unroll
+    for (int i = 0; i < F::NPW; ++i) {
+      const int j = wid + 8 * i;
+      if (j < F::DZP)
+        glds16(dZg + (sbase + m0) * (COUT * 2), vo[i], st + j * 1024);
+      else if (j < 2 * F::DZP)
+        glds16(Yg + (sbase + m0) * (COUT * 2), vo[i], st + F::DZB + (j - F::DZP) * 1024);
+      else
+        glds16(Ypg + (sbase + m0) * (CIN * 2), vo[i], st + 2 * F::DZB + (j - 2 * F::DZP) * 1024);
+    }
+    if constexpr (MASK)
+      glds4(Mkg + (sbase + m0) * (CIN / 8), vo[F::NPW], st + 2 * F::DZB + F::YPB + (wid & 1) * 256);
+    else
+      glds4(Ypg + (sbase + m0) * (CIN * 2), vo[F::NPW], st + 2 * F::DZB + F::YPB + (wid & 1) * 256);
+  };
+
+  // ---- per-thread constants: transform coefficients (registers), W^T fragments of this wave's
+  // dgrad column tile (ct = wave), epilogue coefficients of this lane's 4 columns
+  const int dlc = tid % F::SPR, drr = tid / F::SPR;   // dy slot: chunk, first row
+  const int xlc = tid & 15, xrr = tid >> 4;             // x slot: chunk, row
+  {   // transform coefficients in LDS (registers go to the MFMA operand pipelines)
+    float *cf = reinterpret_cast<float *>(lds + F::OFF_CF);
+    for (int i = tid; i < COUT; i += THREADS) { cf[i] = a.pa[i]; cf[COUT + i] = a.pb[i]; cf[2 * COUT + i] = a.pc[i]; }
+    if (tid < CB) { cf[3 * COUT + tid] = a.es[n0 + tid]; cf[3 * COUT + CB + tid] = a.et[n0 + tid]; }
+  }
+  const float *cfd = reinterpret_cast<const float *>(lds + F::OFF_CF) + dlc * 8;
+  const float *cfx = reinterpret_cast<const float *>(lds + F::OFF_CF) + 3 * COUT + xlc * 8;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int ct = wid;
+  const int cc = 16 * ct + 4 * g;   // block-local column of this lane's 4 (epilogue)
+  float es4[4], et4[4];
+  load_vec<4>(a.es, n0 + cc, es4);
+  load_vec<4>(a.et, n0 + cc, et4);
+  u32x4 wfr[F::KS];
+#pragma unroll
+  for (int kk = 0; kk < F::KS; ++kk)
+    wfr[kk] = *reinterpret_cast<const u32x4 *>(Wt + (int64_t)(n0 + ct * 16 + l16) * COUT + (4 * kk + g) * 8);
+
+  // loop-invariant LDS offsets (the k-steps / tiles / passes then differ by immediates)
+  const int o_tr = tid * 16;                                           // raw dZ / Y, pass i: + i 8 KB
+  const int o_dyw = F::OFF_DY + prow(drr) * F::DYR + dlc * 16;         // dy write, pass i: + 16 i rows
+  const int o_ypx = 2 * F::DZB + xrr * (CB * 2) + ((xlc ^ fyp(xrr)) << 4);
+  const int o_mkx = 2 * F::DZB + F::YPB + xrr * 16 + xlc;
+  const int o_xw = F::OFF_X + prow(xrr) * F::XR + xlc * 16;
+  const int o_ype = 2 * F::DZB + l16 * (CB * 2) + ((((cc >> 3) ^ l16) << 4) | ((cc & 7) << 1));   // + u 4 KB
+  const int o_mke = 2 * F::DZB + F::YPB + l16 * 16 + (cc >> 3);                                     // + u 256
+  const int o_dg = F::OFF_DY + prow(l16) * F::DYR + g * 16;   // dgrad: + u 16 rows, + kk 64 B
+  const int q = (lane >> 2) & 3, p = lane & 3;                 // transposed-read lane roles
+  const int tr0 = prow(8 * g + q), tr1 = prow(8 * g + 4 + q);
+  const int o_ty0 = F::OFF_DY + tr0 * F::DYR + (16 * F::OBW * wid + 4 * p) * 2;   // + ob 32 B
+  const int o_ty1 = F::OFF_DY + tr1 * F::DYR + (16 * F::OBW * wid + 4 * p) * 2;
+  const int o_tx0 = F::OFF_X + tr0 * F::XR + 8 * p;   // + u 32 B
+  const int o_tx1 = F::OFF_X + tr1 * F::XR + 8 * p;
+
+  f32x4 accw[F::OBW][8];
+#pragma unroll
+  for (int o = 0; o < F::OBW; ++o)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) accw[o][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float s1[4], s2[4];   // this lane's 4 columns, both row tiles
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { s1[r] = 0.f; s2[r] = 0.f; }
+
+  // ---- transform of step s (its DMA landed, barrier passed): dy and x (zeros past the slice)
+  auto transform = [&](int s) {
+    const char *st = lds + (s % F::NST) * F::STAGE;
+    const int64_t m0 = lo + (int64_t)s * MS;
+    float ca[8], cb[8], cg[8];
+    lds_vec8(cfd, ca);
+    lds_vec8(cfd + COUT, cb);
+    lds_vec8(cfd + 2 * COUT, cg);
+#pragma unroll
+    for (int i = 0; i < F::DY_RPT; ++i) {
+      const int r = drr + i * (THREADS / F::SPR);
+      float v[8], y[8];
+      unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o_tr + i * THREADS * 16), v);
+      unpack_chunk(*reinterpret_cast<const u32x4 *>(st + F::DZB + o_tr + i * THREADS * 16), y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+      const u32x4 out = pack_chunk(v);
+      *reinterpret_cast<u32x4 *>(lds + o_dyw + i * (THREADS / F::SPR) * F::DYR) =
+          m0 + r < hi ? out : mk_u32x4(0, 0, 0, 0);
+    }
+    float v[8], xs[8], xt[8];
+    lds_vec8(cfx, xs);
+    lds_vec8(cfx + CB, xt);
+    unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o_ypx), v);
+    const uint32_t mb = MASK ? (uint32_t)(uint8_t)st[o_mkx] : 0xffu;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+      v[e] = ((mb >> e) & 1u) ? x * ks : 0.f;
+    }
+    const u32x4 out = pack_chunk(v);
+    *reinterpret_cast<u32x4 *>(lds + o_xw) = m0 + xrr < hi ? out : mk_u32x4(0, 0, 0, 0);
+  };
+
+  // ---- output rows of one step through a buffer descriptor (range: the slice's rows from m0)
+  auto store_rows = [&](int64_t m0, int vo, u32x4 v) {
+    const int64_t vr = pcs_max64(hi - m0, 0);
+    const uint32_t nbytes = vr > 0 ? (uint32_t)((vr - 1) * CIN * 2 + CB * 2) : 0u;
+    char *base = reinterpret_cast<char *>(Cg + (sbase + pcs_min64(m0, hi - 1)) * CIN + n0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, vo, 0, 0);
+  };
+  const int o_st = (16 * (g & 1) + l16) * (CIN * 2) + (16 * ct + 8 * (g >> 1)) * 2;
+
+  // ---- prologue: steps 0 .. NST-2 in flight (each followed by a store the range check drops,
+  // as every loop step's DMA is followed by its epilogue store), step 0 landed and transformed
+#pragma unroll
+  for (int s = 0; s < F::NST - 1; ++s) {
+    dma_step(s);
+    store_rows(hi, 0, mk_u32x4(0, 0, 0, 0));
+  }
+  wait_vm<1 + (F::NST - 2) * (F::VM_STEP + 1)>();
+  barrier_lds();
+  transform(0);
+  barrier_lds();
+
+  for (int t = 0; t < nsteps; ++t) {
+    const int64_t m0 = lo + (int64_t)t * MS;
+    dma_step(t + F::NST - 1);   // into the stage step t-1 used (free since the last barrier)
+    const char *st = lds + (t % F::NST) * F::STAGE;
+    // input gradient out[m = 16 u + l16][c = 16 ct + 4 g + r] (both row tiles u), then the weight
+    // gradient dW[o = 16 (OBW wid + ob) + l16][c = 16 u + 4 g + r] over the step's 32 rows.  The
+    // LDS operand reads run PD k-steps ahead of the MFMAs (explicit ring; the scheduling
+    // barriers keep the compiler from collapsing it under register pressure).
+    // (the epilogue's Yp values and dropout bits, read up front)
+    uint2 ype[2];
+    uint32_t kbe[2] = {0xFu, 0xFu};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ype[u] = *reinterpret_cast<const uint2 *>(st + o_ype + u * 16 * (CB * 2));
+      if constexpr (MASK) kbe[u] = (uint32_t)(uint8_t)st[o_mke + u * 256];
+    }
+    f32x4 accd[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    {
+      constexpr int PD = 3;
+      bf16x8 yf[PD + 1][2];
+      bf16x8 yt[F::OBW], xf[PD + 1];
+      auto rd_dg = [&](int kk, bf16x8 (&d)[2]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) d[u] = *reinterpret_cast<const bf16x8 *>(lds + o_dg + u * 16 * F::DYR + kk * 64);
+      };
+      auto rd_x = [&](int u) { return tr_frag2(lds + o_tx0 + u * 32, lds + o_tx1 + u * 32); };
+#pragma unroll
+      for (int kk = 0; kk < PD; ++kk) rd_dg(kk, yf[kk]);
+#pragma unroll
+      for (int kk = 0; kk < F::KS; ++kk) {
+        if (kk + PD < F::KS) rd_dg(kk + PD, yf[(kk + PD) % (PD + 1)]);
+        if (kk + PD == F::KS) {   // the weight gradient's first operands
+#pragma unroll
+          for (int ob = 0; ob < F::OBW; ++ob) yt[ob] = tr_frag2(lds + o_ty0 + ob * 32, lds + o_ty1 + ob * 32);
+        }
+        if (kk + PD > F::KS && kk + PD - F::KS - 1 < PD) xf[kk + PD - F::KS - 1] = rd_x(kk + PD - F::KS - 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          accd[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wfr[kk]), yf[kk % (PD + 1)][u],
+                                                           accd[u], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // (x fragments 0 .. PD-2 were issued above; keep PD-1 ahead)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u + PD - 1 < 8) xf[(u + PD - 1) % (PD + 1)] = rd_x(u + PD - 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ob = 0; ob < F::OBW; ++ob)
+          accw[ob][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u % (PD + 1)], yt[ob], accw[ob][u], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // epilogue: previous layer's ReLU / dropout masks, S1 / S2, 16-B stores
+    {
+      uint32_t pk[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool live = m0 + 16 * u + l16 < hi;
+        const uint2 yp = ype[u];
+        const float y[4] = {bf_lo(yp.x), bf_hi(yp.x), bf_lo(yp.y), bf_hi(yp.y)};
+        const uint32_t kb = MASK ? (kbe[u] >> (cc & 7)) & 0xFu : 0xFu;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // (non-short-circuit: selects, no branches)
+          const bool keep = live & (((kb >> r) & 1u) != 0u) & (fmaf(y[r], es4[r], et4[r]) > 0.f);
+          v[r] = keep ? accd[u][r] * ks : 0.f;
+          s1[r] += v[r];
+          s2[r] = fmaf(v[r], y[r], s2[r]);
+        }
+        pk[u][0] = pack2bf(v[0], v[1]);
+        pk[u][1] = pack2bf(v[2], v[3]);
+      }
+      // lane groups 2h / 2h+1 trade row tiles: each lane then holds 8 consecutive columns
+      // (8 (g >> 1) ..) of row 16 (g & 1) + l16
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][h], pk[1][h], false, false);
+        pk[0][h] = sw[0];
+        pk[1][h] = sw[1];
+      }
+      // a buffer store whose range ends at the slice's last row: rows past it are dropped by
+      // the hardware, so every wave issues exactly one store per step (the counted waits)
+      store_rows(m0, o_st, mk_u32x4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]));
+    }
+    // step t+1 landed: every older DMA done (the newer: the store above, step t+NST-1's
+    // pieces, and the NST-2 steps' loads + stores in between)
+    wait_vm<1 + (F::NST - 2) * (F::VM_STEP + 1)>();
+    barrier_lds();
+    if (t + 1 < nsteps) transform(t + 1);
+    barrier_lds();
+  }
+  wait_vm<0>();   // the clamped DMAs past the end
+
+  // ---- dW partial (this slice's slab, columns n0 ..)
+  float *out = wpart + (int64_t)chunk * COUT * CIN + n0;
+#pragma unroll
+  for (int ob = 0; ob < F::OBW; ++ob)
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      *reinterpret_cast<float4 *>(out + (int64_t)(16 * (F::OBW * wid + ob) + l16) * CIN + 16 * u + 4 * g) =
+          make_float4(accw[ob][u][0], accw[ob][u][1], accw[ob][u][2], accw[ob][u][3]);
+
+  // ---- S1 / S2: over the 16 lanes (rows) of each column; the wave owns its columns
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      s1[r] += __shfl_xor(s1[r], o);
+      s2[r] += __shfl_xor(s2[r], o);
+    }
+  if (l16 == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * ct + 4 * g + r;
+      *reinterpret_cast<float2 *>(a.stats + ((int64_t)chunk * CIN + n0 + c) * 2) =
+          make_float2(s1[r], a.erstd[n0 + c] * (s2[r] - a.emean[n0 + c] * s1[r]));
+    }
+  }
+}
+
+}  // namespace
+
+// Shapes served: (Cout, Cin) = K x Ncols in {256 x 512 (seg_conv2), 128 x 256 (seg_conv3)}, bf16,
+// PRO_BWD / EPI_DGRAD with dropout bits and no addend.
+bool pcs_seg_bwd_applicable(const pcs_gemm_args &a) {
+  return a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && !a.addend &&
+         ((a.K == 256 && a.Ncols == 512) || (a.K == 128 && a.Ncols == 256));
+}
+
+int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a) {
+  const int nblk = a->Ncols / CB;
+  int64_t sps = (256 + a->num_scenes * nblk - 1) / (a->num_scenes * nblk);   // one WG per CU
+  const int64_t max_sps = (a->scene_rows + 4 * MS - 1) / (4 * MS);
+  if (sps > max_sps) sps = max_sps;
+  if (sps < 1) sps = 1;
+  const int64_t rps = ((a->scene_rows + sps - 1) / sps + MS - 1) / MS * MS;
+  a->chunks_per_scene = (int32_t)((a->scene_rows + rps - 1) / rps);   // no empty slices
+  return rps;
+}
+
+int pcs_seg_bwd_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s) {
+  pcs_gemm_args g = a;
+  const int64_t rps = pcs_seg_bwd_geometry(&g);
+  if (g.chunks_per_scene != a.chunks_per_scene)
+    return pcs_set_einval("pcs_dgrad_wgrad_bn", "chunks_per_scene must come from pcs_dgrad_wgrad_bn_workspace");
+  const int nb = (int)(a.num_scenes * a.chunks_per_scene) * (a.Ncols / CB);
+#define PCS_SEG(CO, CI, MK) \
+  hipLaunchKernelGGL((seg_bwd_kernel<CO, CI, MK>), dim3(nb), dim3(THREADS), 0, s, a, wpart, rps)
+  if (a.K == 256) {
+    if (a.c_mask) PCS_SEG(256, 512, true); else PCS_SEG(256, 512, false);
+  } else {
+    if (a.c_mask) PCS_SEG(128, 256, true); else PCS_SEG(128, 256, false);
+  }
+#undef PCS_SEG
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

@@ -407,7 +407,7 @@ void launch_fold(const float *W, int Cout, int Cin, int64_t ldw, const float *al
     const int nb = (int)pcs_min64(1024, ((int64_t)Cout * Cin + 255) / 256);
     hipLaunchKernelGGL(fold_wt_kernel<T>, dim3(nb), dim3(256), 0, st, W, ldw, Cout, Cin, alpha, WsT);
   }
-  hipLaunchKernelGGL(fold_c_kernel, dim3((Cin + 63) / 64), dim3(256), 0, st, W, ldw, Cout, Cin, beta, c);
+  if (c) hipLaunchKernelGGL(fold_c_kernel, dim3((Cin + 63) / 64), dim3(256), 0, st, W, ldw, Cout, Cin, beta, c);
   if (Cin % 64 == 0 && Cin >= 512)
     hipLaunchKernelGGL((fold_h_tiled_kernel<T, 32>), dim3(Cin / 32, Cin / 32), dim3(256), 0, st, W, ldw, Cout, Cin,
                        gamma, H);
@@ -421,7 +421,7 @@ void launch_fold(const float *W, int Cout, int Cin, int64_t ldw, const float *al
 extern "C" int pcs_bn_fold(const float *W, int32_t Cout, int32_t Cin, int64_t ldw, const float *alpha,
                            const float *beta, const float *gamma, int32_t dtype, void *WsT, float *c, void *H,
                            pcs_stream_t stream) {
-  if (!W || !beta || !gamma || (WsT && !alpha) || !c || !H || Cout <= 0 || Cin <= 0 || ldw < Cin)
+  if (!W || !gamma || (WsT && !alpha) || (c && !beta) || !H || Cout <= 0 || Cin <= 0 || ldw < Cin)
     return pcs_set_einval("pcs_bn_fold", "bad arguments");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == PCS_BF16)

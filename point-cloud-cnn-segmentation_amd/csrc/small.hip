@@ -810,6 +810,8 @@ __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbyt
 template <int TPO>
 __global__ void reduce_partials_kernel(const float *partial, int64_t nslabs, int64_t len, float scale,
                                        float *out, int64_t ldo, int64_t row_len) {
+  partial += (int64_t)blockIdx.y * nslabs * len;   // grouped form: group y's slabs / outputs
+  out += (int64_t)blockIdx.y * len;
   const int sub = threadIdx.x % TPO;
   const int64_t i4 = ((int64_t)blockIdx.x * (blockDim.x / TPO) + threadIdx.x / TPO) * 4;
   const bool vec = (row_len & 3) == 0 && i4 + 4 <= len;
@@ -1131,6 +1133,31 @@ extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32
                      reinterpret_cast<hipStream_t>(stream), seed, offset, nbytes, thr, bits);
   PCS_CHECK_LAUNCH();
   return 0;
+}
+
+namespace {
+int reduce_partials_launch(const float *partial, int64_t ngroups, int64_t nslabs, int64_t len, float scale,
+                           float *out, int64_t ldo, int64_t row_len, hipStream_t st) {
+  const int64_t n4 = (len + 3) / 4;
+  const dim3 g256(blocks_for(n4, 256 / 32), (unsigned)ngroups), g8(blocks_for(n4, 256 / 8), (unsigned)ngroups),
+      g1(blocks_for(n4, 256), (unsigned)ngroups);
+  if (nslabs >= 64)
+    hipLaunchKernelGGL(reduce_partials_kernel<32>, g256, dim3(256), 0, st, partial, nslabs, len, scale, out, ldo,
+                       row_len);
+  else if (nslabs >= 8)
+    hipLaunchKernelGGL(reduce_partials_kernel<8>, g8, dim3(256), 0, st, partial, nslabs, len, scale, out, ldo, row_len);
+  else
+    hipLaunchKernelGGL(reduce_partials_kernel<1>, g1, dim3(256), 0, st, partial, nslabs, len, scale, out, ldo, row_len);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+}  // namespace
+
+extern "C" int pcs_reduce_partials_grouped(const float *partial, int64_t ngroups, int64_t nslabs, int64_t len,
+                                           float scale, float *out, pcs_stream_t stream) {
+  if (!partial || !out || len <= 0 || nslabs <= 0 || ngroups <= 0 || ngroups > 65535)
+    return pcs_set_einval("pcs_reduce_partials_grouped", "bad arguments (0 < ngroups <= 65535)");
+  return reduce_partials_launch(partial, ngroups, nslabs, len, scale, out, len, len, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int pcs_reduce_partials(const float *partial, int64_t nslabs, int64_t len, float scale, float *out,

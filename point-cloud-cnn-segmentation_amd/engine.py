@@ -457,9 +457,7 @@ class Engine:
                          L.ptr(G5), s)
             # per-scene column sums of a5 from conv5's per-chunk partials (chunks are scene-aligned)
             Sb2 = torch.empty(B, 1024, 2, dtype=torch.float32, device=dev)
-            for b in range(B):
-                L.call("pcs_reduce_partials", L.ptr(sv.a5_colsum[b * cps5c:]), cps5c, 2048, 1.0, L.ptr(Sb2[b]),
-                       2048, 2048, s)
+            L.call("pcs_reduce_partials_grouped", L.ptr(sv.a5_colsum), B, cps5c, 2048, 1.0, L.ptr(Sb2), s)
             Sb = Sb2[..., 0].contiguous()
             st = torch.empty(B, 1024, 2, dtype=torch.float32, device=dev)
             qbytes = L.load().pcs_bn_stats_from_gram_scenes_workspace(1024, 1024)
@@ -713,9 +711,9 @@ class Engine:
             Ws1_r = self._rounded(Ws1)     # the W_l the forward GEMM used
             WaT = torch.empty(64, 512, dtype=self.tdt, device=dev)
             Hs1 = torch.empty(64, 64, dtype=self.tdt, device=dev)
-            cf1 = torch.empty(64, dtype=torch.float32, device=dev)
+            # no cvec output: the folded kernel forms its per-scene cvec_b itself (folded_cvec_kernel)
             L.call("pcs_bn_fold", L.ptr(Ws1_r), 512, 64, Ws1.shape[1], L.ptr(a1), L.ptr(b1), L.ptr(g1), self.dt,
-                   L.ptr(WaT), L.ptr(cf1), L.ptr(Hs1), s)
+                   L.ptr(WaT), None, L.ptr(Hs1), s)
             fa = L.WgradArgs(num_scenes=B, scene_rows=N, Cout=512, Cin=64, dtype=self.dt,
                              splits_per_scene=0, dy_mode=L.PRO_RAW, x_mode=L.PRO_BNRELU,
                              x_keep_scale=1.0, dW=L.ptr(G("seg_conv1.weight")), ldw=Ws1.shape[1],
@@ -729,7 +727,7 @@ class Engine:
             fa.partial = ws1.data_ptr()
             self._launch("dgrad+wgrad:seg_conv1", "pcs_dgrad_wgrad_folded", ct.byref(fa), L.ptr(WaT), L.ptr(Hs1),
                          L.ptr(Ws1_r), L.ptr(sv.sbias_s1), L.ptr(dA2), s)
-            keepalive.append((ws1, Ws1_r, WaT, Hs1, cf1))
+            keepalive.append((ws1, Ws1_r, WaT, Hs1))
         else:
             self._gemm(B, N, 512, 64, L.PRO_BWD, L.EPI_RAW, dz_s1, wc["seg_conv1"][1], dA2,
                        A2=ys["seg_conv1"], pa=a1, pb=b1, pc=g1, tag="dgrad:seg_conv1")
@@ -774,8 +772,10 @@ class Engine:
             # epilogue), then their sparse term (pcs_pool_rows_add)
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
                        stats=st5, tag="dgrad:global_feat")
+            # the max-pool rows with the W the forward GEMM used (as the fp8 branch and the
+            # Gram-form weight gradient do)
             L.call("pcs_pool_rows_add", L.ptr(bufB), self.dt, L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am),
-                   L.ptr(sp), L.ptr(Wg), Wg.shape[1], 1024, L.ptr(st5), cps5, s)
+                   L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
         else:
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
                        pool_idx=sv.am, pool_coef=sp, pool_w=Wg, pool_ldw=Wg.shape[1], pool_c=1024,

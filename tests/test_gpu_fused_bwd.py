@@ -114,9 +114,12 @@ def test_dgrad_wgrad_rejects_other_shapes():
 
 @pytest.mark.parametrize("cout,cin,variant,B,N", [
     (64, 64, "plain", 3, 1000), (64, 64, "addend", 2, 4096 + 33), (128, 64, "plain", 4, 4096),
-    (128, 64, "plain", 1, 64 * 40 + 5), (128, 64, "mask", 3, 777)])
+    (128, 64, "plain", 1, 64 * 40 + 5), (128, 64, "mask", 3, 777),
+    # seg_conv2 / seg_conv3 (LDS-DMA stream, csrc/fused_seg.hip): ragged slices, one-step slices
+    (256, 512, "mask", 2, 4096 + 33), (256, 512, "plain", 1, 70), (256, 512, "mask", 4, 65536 + 100),
+    (128, 256, "mask", 3, 1000), (128, 256, "plain", 2, 64 * 40 + 5), (128, 256, "mask", 1, 31)])
 def test_dgrad_wgrad_bn_matches_torch(cout, cin, variant, B, N):
-    """pcs_dgrad_wgrad_bn (conv2/3/4) vs torch fp32 on the same bf16 inputs:
+    """pcs_dgrad_wgrad_bn (conv2/3/4, seg_conv2/3) vs torch fp32 on the same bf16 inputs:
     dz' = (es*Yp + et > 0) * keep * ks * (dy W + addend), its per-chunk S1 / S2 statistics
     (S2 = rstd * (sum dz' Yp - mean * S1)) and dW = dy^T x."""
     import pcs_amd._lib as L
