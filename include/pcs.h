@@ -316,7 +316,7 @@ enum { PCS_HEAD_FWD = 0, PCS_HEAD_CE = 1, PCS_HEAD_BWD = 2 };
 typedef struct {
   int64_t num_scenes, scene_rows;
   int32_t Cin;          /* 128 */
-  int32_t num_classes;  /* 1 <= C <= 64 */
+  int32_t num_classes;  /* 1 <= C <= 256 (C > 64: the wide head, 16-row tiles) */
   int32_t dtype, mode;
   int32_t chunks_per_scene; /* 0 = auto */
   const void *Y;        /* [M, Cin] y_seg3 */
@@ -340,7 +340,7 @@ int pcs_head(const pcs_head_args *args, pcs_stream_t stream);
 
 /* sum of class_weight[label] over labels != -1 (the CE denominator, P:216) -> out[0] (f32),
  * count of valid labels -> out[1], 1/out[0] -> out[2].  Exact: integer class counts (counts_ws[C], int64
- * workspace) times the weights, summed in fp64. */
+ * workspace) times the weights, summed in fp64.  1 <= C <= 256. */
 int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weight,
                       int32_t C, int64_t *counts_ws, float *out, pcs_stream_t stream);
 
@@ -485,7 +485,7 @@ int pcs_bn_s2_from_r(float *stats, int64_t num_chunks, int32_t C, const float *R
  * Confusion matrix of argmax predictions (P:261-266 accuracy, P:314-346 F1 / mIoU inputs):
  * cm[y, argmax_c logits[m, c]] += 1 for every point m with 0 <= labels[m] < C (labels -1 =
  * padding are skipped).  logits: fp32 rows of stride ld; cm: int64 [C, C], accumulated
- * (zero it once per epoch).  C <= 32.
+ * (zero it once per epoch).  1 <= C <= 256 (LDS histogram up to 64 classes, global atomics above).
  */
 int pcs_confusion(const float *logits, int64_t ld, const int64_t *labels, int64_t M, int32_t C,
                   int64_t *cm, pcs_stream_t stream);
@@ -577,10 +577,12 @@ int pcs_gather_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_
  * (0, 2, 3, 4, 1); ConvTranspose3d weight permuted (1, 2, 3, 4, 0)), bias [Cout] f32 or NULL,
  * Y [B, Do, Ho, Wo, Cout] in ydtype (PCS_F32 | PCS_BF16), fp32 accumulation:
  *   transposed = 0:  Y[o] = b + sum_t W_t X[o s - p + t]                  Do = (Di + 2p - k) / s + 1
- *   transposed = 1:  Y[o] = b + sum_t W_t X[(o + p - t) / s] (exact only)  Do = (Di - 1) s - 2p + k
- * k in 1..3, s in {1, 2}, 0 <= p < k.  pcs_conv3d: Cin % 32 == 0, Cout % 64 == 0.  The input
- * gradient of either form is the other form applied to dY with pcs_conv3d_weight_t(W) and the
- * grids swapped.  pcs_conv3d_wgrad: dW [Cout, k, k, k, Cin] f32 = sum_o dY[o] (x) X[in(o, t)]
+ *   transposed = 1:  Y[o] = b + sum_t W_t X[(o + p - t) / s] (exact only)  Do = (Di - 1) s - 2p + k + op
+ * (op = torch's output_padding, 0 <= op < s, taken from the Do / Ho / Wo given).
+ * k in 1..3, s in {1, 2}, 0 <= p < k.  pcs_conv3d: Cin % 32 == 0, Cout % 64 == 0 (the Python
+ * layer zero-pads other channel counts to multiples of 64).  The input gradient of either form is
+ * the other form applied to dY with pcs_conv3d_weight_t(W) and the grids swapped (a strided
+ * convolution's skipped trailing input planes come back as the transposed form's op).  pcs_conv3d_wgrad: dW [Cout, k, k, k, Cin] f32 = sum_o dY[o] (x) X[in(o, t)]
  * over the forward's index map, db [Cout] f32 = sum_o dY[o] (may be NULL); Cin, Cout % 64 == 0;
  * fp32 partials summed in a fixed order (deterministic).
  */

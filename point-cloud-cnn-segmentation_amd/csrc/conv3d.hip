@@ -696,9 +696,11 @@ bool geom_ok(const pcs_conv3d_geom *g, const char **why) {
   }
   const int din[3] = {g->Di, g->Hi, g->Wi}, dout[3] = {g->Do, g->Ho, g->Wo};
   for (int d = 0; d < 3; ++d) {
+    // transposed: + output_padding in [0, s) (torch's; the extra planes are plain gather rows)
     const int expect = g->transposed ? (din[d] - 1) * g->s - 2 * g->p + g->k : (din[d] + 2 * g->p - g->k) / g->s + 1;
-    if (dout[d] != expect || (!g->transposed && din[d] + 2 * g->p < g->k)) {
-      *why = "output grid must be (in + 2p - k)/s + 1 (conv) or (in - 1)s - 2p + k (transposed)";
+    const int slack = g->transposed ? g->s - 1 : 0;
+    if (dout[d] < expect || dout[d] > expect + slack || (!g->transposed && din[d] + 2 * g->p < g->k)) {
+      *why = "output grid must be (in + 2p - k)/s + 1 (conv) or (in - 1)s - 2p + k + op, 0 <= op < s (transposed)";
       return false;
     }
   }

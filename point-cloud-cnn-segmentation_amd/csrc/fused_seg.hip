@@ -114,11 +114,19 @@ PCS_DEV bf16x8 tr_frag2(const char *p0, const char *p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
-  const float4 x = *reinterpret_cast<const float4 *>(p);
-  const float4 y = *reinterpret_cast<const float4 *>(p + 4);
-  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+// 8 coefficients of one 16-B data slot from the split LDS layout: elements 0-3 of every slot
+// first, then elements 4-7 (lanes reading consecutive slots then read consecutive 16 B: no bank
+// conflicts; the interleaved [slot][8] layout would put two lanes on every bank)
+PCS_DEV void lds_vec8(const char *p, int half_bytes, float (&v)[8]) {
+  const u32x4 x = *reinterpret_cast<const u32x4 *>(p);
+  const u32x4 y = *reinterpret_cast<const u32x4 *>(p + half_bytes);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = __uint_as_float(x[e]);
+    v[4 + e] = __uint_as_float(y[e]);
+  }
 }
+PCS_DEV int split_idx(int i, int n) { return ((i & 7) >> 2) * (n / 2) + (i >> 3) * 4 + (i & 3); }
 PCS_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 PCS_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
@@ -207,11 +215,20 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
   const int xlc = tid & 15, xrr = tid >> 4;             // x slot: chunk, row
   {   // transform coefficients in LDS (registers go to the MFMA operand pipelines)
     float *cf = reinterpret_cast<float *>(lds + F::OFF_CF);
-    for (int i = tid; i < COUT; i += THREADS) { cf[i] = a.pa[i]; cf[COUT + i] = a.pb[i]; cf[2 * COUT + i] = a.pc[i]; }
-    if (tid < CB) { cf[3 * COUT + tid] = a.es[n0 + tid]; cf[3 * COUT + CB + tid] = a.et[n0 + tid]; }
+    for (int i = tid; i < COUT; i += THREADS) {
+      const int j = split_idx(i, COUT);
+      cf[j] = a.pa[i];
+      cf[COUT + j] = a.pb[i];
+      cf[2 * COUT + j] = a.pc[i];
+    }
+    if (tid < CB) {
+      const int j = split_idx(tid, CB);
+      cf[3 * COUT + j] = a.es[n0 + tid];
+      cf[3 * COUT + CB + j] = a.et[n0 + tid];
+    }
   }
-  const float *cfd = reinterpret_cast<const float *>(lds + F::OFF_CF) + dlc * 8;
-  const float *cfx = reinterpret_cast<const float *>(lds + F::OFF_CF) + 3 * COUT + xlc * 8;
+  const char *cfd = lds + F::OFF_CF + dlc * 16;
+  const char *cfx = lds + F::OFF_CF + 3 * COUT * 4 + xlc * 16;
   const int l16 = lane & 15, g = lane >> 4;
   const int ct = wid;
   const int cc = 16 * ct + 4 * g;   // block-local column of this lane's 4 (epilogue)
@@ -253,9 +270,9 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
     const char *st = lds + (s % F::NST) * F::STAGE;
     const int64_t m0 = lo + (int64_t)s * MS;
     float ca[8], cb[8], cg[8];
-    lds_vec8(cfd, ca);
-    lds_vec8(cfd + COUT, cb);
-    lds_vec8(cfd + 2 * COUT, cg);
+    lds_vec8(cfd, COUT * 2, ca);
+    lds_vec8(cfd + COUT * 4, COUT * 2, cb);
+    lds_vec8(cfd + 2 * COUT * 4, COUT * 2, cg);
 #pragma unroll
     for (int i = 0; i < F::DY_RPT; ++i) {
       const int r = drr + i * (THREADS / F::SPR);
@@ -269,8 +286,8 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
           m0 + r < hi ? out : mk_u32x4(0, 0, 0, 0);
     }
     float v[8], xs[8], xt[8];
-    lds_vec8(cfx, xs);
-    lds_vec8(cfx + CB, xt);
+    lds_vec8(cfx, CB * 2, xs);
+    lds_vec8(cfx + CB * 4, CB * 2, xt);
     unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o_ypx), v);
     const uint32_t mb = MASK ? (uint32_t)(uint8_t)st[o_mkx] : 0xffu;
 #pragma unroll

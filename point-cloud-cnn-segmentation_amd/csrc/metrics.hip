@@ -6,14 +6,18 @@
 
 namespace {
 
-constexpr int THREADS = 256, CMAX = 64;
+constexpr int THREADS = 256, CMAX = 64, CMAX_ALL = 256;
 
+// LDS = true: per-block histogram in LDS (C <= 64); otherwise straight to the global matrix
+template <bool LDS>
 __global__ __launch_bounds__(THREADS) void confusion_kernel(const float *__restrict__ logits, int64_t ld,
                                                             const int64_t *__restrict__ labels, int64_t M,
                                                             int C, unsigned long long *__restrict__ cm) {
-  __shared__ unsigned int hist[CMAX * CMAX];
-  for (int i = threadIdx.x; i < C * C; i += THREADS) hist[i] = 0u;
-  __syncthreads();
+  __shared__ unsigned int hist[LDS ? CMAX * CMAX : 1];
+  if constexpr (LDS) {
+    for (int i = threadIdx.x; i < C * C; i += THREADS) hist[i] = 0u;
+    __syncthreads();
+  }
   for (int64_t m = (int64_t)blockIdx.x * THREADS + threadIdx.x; m < M; m += (int64_t)gridDim.x * THREADS) {
     const int64_t y = labels[m];
     if (y < 0 || y >= C) continue;
@@ -24,23 +28,30 @@ __global__ __launch_bounds__(THREADS) void confusion_kernel(const float *__restr
       const float v = z[c];
       if (v > bz) { bz = v; best = c; }
     }
-    atomicAdd(&hist[(int)y * C + best], 1u);
+    if constexpr (LDS) atomicAdd(&hist[(int)y * C + best], 1u);
+    else atomicAdd(&cm[(int)y * C + best], 1ull);
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C * C; i += THREADS)
-    if (hist[i]) atomicAdd(&cm[i], (unsigned long long)hist[i]);
+  if constexpr (LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * C; i += THREADS)
+      if (hist[i]) atomicAdd(&cm[i], (unsigned long long)hist[i]);
+  }
 }
 
 }  // namespace
 
 extern "C" int pcs_confusion(const float *logits, int64_t ld, const int64_t *labels, int64_t M, int32_t C,
                              int64_t *cm, pcs_stream_t stream) {
-  if (!logits || !labels || !cm || M < 0 || C < 1 || C > CMAX || ld < C)
-    return pcs_set_einval("pcs_confusion", "bad arguments (1 <= C <= 64, ld >= C)");
+  if (!logits || !labels || !cm || M < 0 || C < 1 || C > CMAX_ALL || ld < C)
+    return pcs_set_einval("pcs_confusion", "bad arguments (1 <= C <= 256, ld >= C)");
   if (M == 0) return 0;
   const int nb = (int)pcs_min64(2048, (M + THREADS - 1) / THREADS);
-  hipLaunchKernelGGL(confusion_kernel, dim3(nb), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
-                     logits, ld, labels, M, C, reinterpret_cast<unsigned long long *>(cm));
+  if (C <= CMAX)
+    hipLaunchKernelGGL(confusion_kernel<true>, dim3(nb), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                       logits, ld, labels, M, C, reinterpret_cast<unsigned long long *>(cm));
+  else
+    hipLaunchKernelGGL(confusion_kernel<false>, dim3(nb), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                       logits, ld, labels, M, C, reinterpret_cast<unsigned long long *>(cm));
   PCS_CHECK_LAUNCH();
   return 0;
 }

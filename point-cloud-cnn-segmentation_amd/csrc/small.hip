@@ -571,6 +571,233 @@ __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tile
   }
 }
 
+// Wide head for 64 < C <= 256 classes (the reference takes any class count, P:83 / P:153).
+// 16 rows per tile, 16 threads per row (8 channels each); the whole fp32 W (C x 128) stays in
+// LDS.  Each thread keeps the logits of its own classes (c = 16 j + q): max / sum-exp and the
+// label's logit come from 16-lane reductions, so no thread holds all C logits.  The dW / db
+// partials are register-blocked, 8 classes x 16 channels per thread.  Same arguments, output
+// layout and numerics (fp32 accumulation, the same operation order per logit up to the
+// reduction tree) as head_kernel.
+constexpr int HW_R = 16, HW_TPR = 16, HW_QCH = HEAD_CIN / HW_TPR, HW_MAXC = 256;
+constexpr int HW_AL = HEAD_CIN + 4;   // a row stride (floats; 16-B aligned rows)
+constexpr int HW_DL = HW_MAXC + 4;    // dl row stride
+static_assert(HW_R * HW_TPR == THREADS && HW_QCH == 8, "wide head geometry");
+
+PCS_DEV float grp16_max(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+PCS_DEV float grp16_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(THREADS) void head_wide_kernel(pcs_head_args a, int tiles_per_scene,
+                                                            int tiles_per_chunk) {
+  constexpr int EPC = Elem<T>::EPC;
+  constexpr int NJ = HW_MAXC / HW_TPR;   // own classes per thread
+  __shared__ __attribute__((aligned(16))) float wl[HW_MAXC * HEAD_CIN];
+  __shared__ __attribute__((aligned(16))) float av[HW_R * HW_AL];
+  __shared__ __attribute__((aligned(16))) float dl[HW_R * HW_DL];
+  __shared__ float lred[THREADS / 64];
+  const int tid = threadIdx.x;
+  const int C = a.num_classes;
+  const int cps = a.chunks_per_scene;
+  const int scene = blockIdx.x / cps, cis = blockIdx.x % cps;
+  const int64_t N = a.scene_rows;
+  const int r = tid / HW_TPR, q = tid % HW_TPR, ch0 = q * HW_QCH;
+  const int cbk = tid >> 3, chb = tid & 7;   // dW ownership: classes 8 cbk .., channels 16 chb ..
+  const bool own_w = 8 * cbk < C;
+  const T *Y = reinterpret_cast<const T *>(a.Y);
+  T *dZ = reinterpret_cast<T *>(a.dZ);
+
+  for (int i = tid; i < C * HEAD_CIN; i += THREADS) wl[i] = a.W[i];
+  float s1[HW_QCH], s2[HW_QCH];
+#pragma unroll
+  for (int e = 0; e < HW_QCH; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  float wacc[8][16], bacc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    bacc[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) wacc[i][j] = 0.f;
+  }
+  float loss_acc = 0.f;
+  __syncthreads();
+
+  const int t_begin = cis * tiles_per_chunk;
+  const int t_end = min(t_begin + tiles_per_chunk, tiles_per_scene);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int64_t row_base = scene * N + (int64_t)tile * HW_R;
+    const int valid = (int)pcs_min64(HW_R, N - (int64_t)tile * HW_R);
+    const bool rv = r < valid;
+    const int64_t grow = row_base + r;
+    // phase 1: a = relu(y s + t) (registers + LDS), xhat (registers)
+    float ar[HW_QCH], xr[HW_QCH];
+#pragma unroll
+    for (int e = 0; e < HW_QCH; ++e) { ar[e] = 0.f; xr[e] = 0.f; }
+    if (rv) {
+#pragma unroll
+      for (int c = 0; c < HW_QCH; c += EPC) {
+        float y[EPC], sv[EPC], tv[EPC], mu[EPC], rs[EPC];
+        unpack_chunk(*reinterpret_cast<const u32x4 *>(Y + grow * HEAD_CIN + ch0 + c), y);
+        load_vec<EPC>(a.s, ch0 + c, sv); load_vec<EPC>(a.t, ch0 + c, tv);
+        if constexpr (MODE != PCS_HEAD_FWD) { load_vec<EPC>(a.mean, ch0 + c, mu); load_vec<EPC>(a.rstd, ch0 + c, rs); }
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          ar[c + e] = fmaxf(fmaf(y[e], sv[e], tv[e]), 0.f);
+          if constexpr (MODE != PCS_HEAD_FWD) xr[c + e] = (y[e] - mu[e]) * rs[e];
+        }
+      }
+    }
+    *reinterpret_cast<float4 *>(av + r * HW_AL + ch0) = make_float4(ar[0], ar[1], ar[2], ar[3]);
+    *reinterpret_cast<float4 *>(av + r * HW_AL + ch0 + 4) = make_float4(ar[4], ar[5], ar[6], ar[7]);
+    // phase 2: logits of the thread's own classes c = 16 j + q
+    float own[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float v = 0.f;
+      if (16 * j < C) {   // block-uniform
+        for (int i = 0; i < 16; ++i) {
+          const int c = 16 * j + i;
+          float p = 0.f;
+          if (c < C) {
+            const float4 w0 = *reinterpret_cast<const float4 *>(wl + c * HEAD_CIN + ch0);
+            const float4 w1 = *reinterpret_cast<const float4 *>(wl + c * HEAD_CIN + ch0 + 4);
+            p = fmaf(ar[0], w0.x, p); p = fmaf(ar[1], w0.y, p); p = fmaf(ar[2], w0.z, p); p = fmaf(ar[3], w0.w, p);
+            p = fmaf(ar[4], w1.x, p); p = fmaf(ar[5], w1.y, p); p = fmaf(ar[6], w1.z, p); p = fmaf(ar[7], w1.w, p);
+          }
+          p = grp16_sum(p);
+          v = i == q ? p : v;
+        }
+      }
+      const int c = 16 * j + q;
+      own[j] = c < C ? v + a.bias[c] : -__builtin_huge_valf();
+    }
+    if (rv && a.logits) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (16 * j + q < C) a.logits[grow * C + 16 * j + q] = own[j];
+    }
+    if constexpr (MODE == PCS_HEAD_CE) {
+      float mx = -__builtin_huge_valf();
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) mx = fmaxf(mx, own[j]);
+      mx = grp16_max(mx);
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) se += 16 * j + q < C ? expf(own[j] - mx) : 0.f;
+      const float lse = mx + logf(grp16_sum(se));
+      const int64_t lab = rv ? a.labels[grow] : -1;
+      const bool ok = lab >= 0 && lab < C;
+      const float w = ok ? a.class_weight[lab] : 0.f;
+      const float gsc = a.wsum ? 1.f / *a.wsum : 1.f;
+      if (ok && (int)(lab & 15) == q) {
+        float zl = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) zl = j == (int)(lab >> 4) ? own[j] : zl;
+        loss_acc += w * (lse - zl);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = 16 * j + q;
+        if (c < C) dl[r * HW_DL + c] = ok ? w * gsc * (expf(own[j] - lse) - (c == lab ? 1.f : 0.f)) : 0.f;
+      }
+    } else if constexpr (MODE == PCS_HEAD_BWD) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = 16 * j + q;
+        if (c < C) dl[r * HW_DL + c] = rv ? a.dlogits[grow * a.dl_stride_row + c * a.dl_stride_col] : 0.f;
+      }
+    }
+    if constexpr (MODE != PCS_HEAD_FWD) {
+      __syncthreads();
+      // phase 3: dA = dl W for the thread's 8 channels, dz = relu'(z) dA, store, S1 / S2
+      if (rv) {
+        float d[HW_QCH];
+#pragma unroll
+        for (int e = 0; e < HW_QCH; ++e) d[e] = 0.f;
+        for (int k = 0; k < C; ++k) {
+          const float dk = dl[r * HW_DL + k];
+          const float4 w0 = *reinterpret_cast<const float4 *>(wl + k * HEAD_CIN + ch0);
+          const float4 w1 = *reinterpret_cast<const float4 *>(wl + k * HEAD_CIN + ch0 + 4);
+          d[0] = fmaf(dk, w0.x, d[0]); d[1] = fmaf(dk, w0.y, d[1]); d[2] = fmaf(dk, w0.z, d[2]); d[3] = fmaf(dk, w0.w, d[3]);
+          d[4] = fmaf(dk, w1.x, d[4]); d[5] = fmaf(dk, w1.y, d[5]); d[6] = fmaf(dk, w1.z, d[6]); d[7] = fmaf(dk, w1.w, d[7]);
+        }
+#pragma unroll
+        for (int c = 0; c < HW_QCH; c += EPC) {
+          float v[EPC];
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            const float dz = ar[c + e] > 0.f ? d[c + e] : 0.f;
+            v[e] = dz;
+            s1[c + e] += dz;
+            s2[c + e] = fmaf(dz, xr[c + e], s2[c + e]);
+          }
+          st16(dZ + grow * HEAD_CIN + ch0 + c, pack_chunk(v));
+        }
+      }
+      // phase 4: dW / db partials over the tile's rows, 8 classes x 16 channels per thread
+      if (own_w) {
+        for (int rr = 0; rr < valid; ++rr) {
+          float dv[8], xv[16];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dv[i] = 8 * cbk + i < C ? dl[rr * HW_DL + 8 * cbk + i] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; j += 4) {
+            const float4 x4 = *reinterpret_cast<const float4 *>(av + rr * HW_AL + 16 * chb + j);
+            xv[j] = x4.x; xv[j + 1] = x4.y; xv[j + 2] = x4.z; xv[j + 3] = x4.w;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            bacc[i] += dv[i];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) wacc[i][j] = fmaf(dv[i], xv[j], wacc[i][j]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (MODE != PCS_HEAD_FWD) {
+    if (t_begin >= t_end) return;
+    // S1 / S2: reduce the 16 row-threads of each channel (dl reused: [2][16][128])
+#pragma unroll
+    for (int e = 0; e < HW_QCH; ++e) {
+      dl[r * HEAD_CIN + ch0 + e] = s1[e];
+      dl[HW_R * HEAD_CIN + r * HEAD_CIN + ch0 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < HEAD_CIN) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int j = 0; j < HW_R; ++j) { a1 += dl[j * HEAD_CIN + tid]; a2 += dl[HW_R * HEAD_CIN + j * HEAD_CIN + tid]; }
+      *reinterpret_cast<float2 *>(a.stats + ((int64_t)blockIdx.x * HEAD_CIN + tid) * 2) = make_float2(a1, a2);
+    }
+    // layout [C * Cin weights | C biases] = flat parameter order of seg_conv4
+    float *wp = a.wpartial + (int64_t)blockIdx.x * C * (HEAD_CIN + 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = 8 * cbk + i;
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < 16; j += 4)
+          *reinterpret_cast<float4 *>(wp + c * HEAD_CIN + 16 * chb + j) =
+              make_float4(wacc[i][j], wacc[i][j + 1], wacc[i][j + 2], wacc[i][j + 3]);
+        if (chb == 0) wp[C * HEAD_CIN + c] = bacc[i];
+      }
+    }
+    if constexpr (MODE == PCS_HEAD_CE) {
+      const float ls = wave_sum(loss_acc);
+      if ((tid & 63) == 0) lred[tid >> 6] = ls;
+      __syncthreads();
+      if (tid == 0) a.loss_partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
+    }
+  }
+}
+
 // Register-resident head for C <= 4 classes: 16 threads per point (one 8-channel bf16 /
 // 4-channel fp32 chunk each; 2 chunks per thread for fp32), logits all-reduced across
 // those 16 lanes by shuffles, seg_conv4 weights, dW/db partials and bn_seg3 S1/S2 kept
@@ -741,15 +968,16 @@ __global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, in
 // misc
 // ---------------------------------------------------------------------------------------
 __global__ void ce_count_kernel(const int64_t *labels, int64_t M, int C, unsigned long long *counts) {
-  __shared__ unsigned int h[HEAD_MAXC];
-  if (threadIdx.x < HEAD_MAXC) h[threadIdx.x] = 0;
+  __shared__ unsigned int h[HW_MAXC];
+  for (int i = threadIdx.x; i < HW_MAXC; i += blockDim.x) h[i] = 0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = labels[i];
     if (l >= 0 && l < C) atomicAdd(&h[l], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < C && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+  for (int i = threadIdx.x; i < C; i += blockDim.x)
+    if (h[i]) atomicAdd(&counts[i], (unsigned long long)h[i]);
 }
 
 __global__ void ce_wsum_kernel(const unsigned long long *counts, const float *w, int C, float *out) {
@@ -1047,7 +1275,7 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
   if (!ap) return pcs_set_einval("pcs_head", "null args");
   pcs_head_args a = *ap;
   if (a.Cin != HEAD_CIN) return pcs_set_einval("pcs_head", "head input must have 128 channels");
-  if (a.num_classes < 1 || a.num_classes > HEAD_MAXC) return pcs_set_einval("pcs_head", "1 <= C <= 64");
+  if (a.num_classes < 1 || a.num_classes > HW_MAXC) return pcs_set_einval("pcs_head", "1 <= C <= 256");
   if (!a.Y || !a.s || !a.t || !a.W || !a.bias) return pcs_set_einval("pcs_head", "missing operand");
   if (a.mode == PCS_HEAD_CE && (!a.labels || !a.class_weight || !a.loss_partial))
     return pcs_set_einval("pcs_head", "CE mode needs labels, class_weight, loss_partial");
@@ -1085,7 +1313,10 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
   }
 #define PCS_HEAD_LAUNCH(T, MODE)                                                                  \
   do {                                                                                            \
-    if (a.num_classes <= 16)                                                                      \
+    if (a.num_classes > HEAD_MAXC)                                                                \
+      hipLaunchKernelGGL((head_wide_kernel<T, MODE>), dim3(nb), dim3(THREADS), 0, s, a,           \
+                         (int)((a.scene_rows + HW_R - 1) / HW_R), (int)(rpc / HW_R));             \
+    else if (a.num_classes <= 16)                                                                 \
       hipLaunchKernelGGL((head_kernel<T, MODE, 16>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc); \
     else                                                                                          \
       hipLaunchKernelGGL((head_kernel<T, MODE, 64>), dim3(nb), dim3(THREADS), 0, s, a, tps, tpc); \
@@ -1108,7 +1339,7 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
 
 extern "C" int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weight, int32_t C,
                                  int64_t *counts_ws, float *out, pcs_stream_t stream) {
-  if (!labels || !class_weight || !counts_ws || !out || C < 1 || C > HEAD_MAXC)
+  if (!labels || !class_weight || !counts_ws || !out || C < 1 || C > HW_MAXC)
     return pcs_set_einval("pcs_ce_weight_sum", "bad arguments");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e = hipMemsetAsync(counts_ws, 0, sizeof(int64_t) * C, s);

@@ -28,7 +28,7 @@ from . import _lib as L
 
 BN_EPS = 1e-5
 MAX_INPUT_DIM = 8     # conv1 kernels (csrc/small.hip) are instantiated for K = 1..8
-MAX_CLASSES = 64      # head kernel (csrc/small.hip: 16- and 64-class instantiations)
+MAX_CLASSES = 256     # head kernels (csrc/small.hip: 16 / 64 classes, and the wide head up to 256)
 BN_MOMENTUM = 0.1
 DROPOUT_P = 0.3
 
@@ -101,8 +101,8 @@ def bucket_ranges(num_classes: int, input_dim: int = 4):
 
 def check_dims(num_classes: int, input_dim: int):
     """The reference accepts any input_dim / num_classes (P:66-83; num_classes comes from the
-    data, P:153); the kernels cover input_dim 1..8 (conv1 is unrolled over K) and 1..64
-    classes (the head keeps a row's logits in registers and seg_conv4 in LDS)."""
+    data, P:153); the kernels cover input_dim 1..8 (conv1 is unrolled over K) and 1..256
+    classes (the head keeps seg_conv4's fp32 weight in LDS: 128 KB at 256 classes)."""
     if not 1 <= int(input_dim) <= MAX_INPUT_DIM:
         raise ValueError(f"pcs_amd supports input_dim 1..{MAX_INPUT_DIM} (the reference's points carry "
                          f"4: x, y, z, e); got {input_dim}")

@@ -107,12 +107,18 @@ def to_points(voxel_logits: torch.Tensor, vb: VoxelBatch) -> torch.Tensor:
 # call by pcs_cast_weight.
 # ---------------------------------------------------------------------------------------------
 
-def _out_size(d, k, s, p, transposed):
-    return (d - 1) * s - 2 * p + k if transposed else (d + 2 * p - k) // s + 1
+def _out_size(d, k, s, p, transposed, op=0):
+    return (d - 1) * s - 2 * p + k + op if transposed else (d + 2 * p - k) // s + 1
 
 
-def _geom(B, grid_in, cin, cout, k, s, p, transposed):
-    out = [_out_size(d, k, s, p, transposed) for d in grid_in]
+def _geom(B, grid_in, cin, cout, k, s, p, transposed, op=(0, 0, 0)):
+    """Conv3dGeom of one call.  op = torch's output_padding (transposed form only, 0 <= op < s per
+    dimension): the trailing output planes a strided convolution's floor division skips, which the
+    input gradient of that convolution needs to cover its whole input grid."""
+    op = (op,) * 3 if isinstance(op, int) else tuple(op)
+    if any(o < 0 or o >= max(s, 1) for o in op) or (any(op) and not transposed):
+        raise ValueError(f"output_padding {op} must satisfy 0 <= op < stride = {s} (transposed form only)")
+    out = [_out_size(d, k, s, p, transposed, o) for d, o in zip(grid_in, op)]
     if min(out) <= 0:
         raise ValueError(f"empty output grid {out} for input {list(grid_in)}, k={k}, s={s}, p={p}")
     return L.Conv3dGeom(B=B, Di=grid_in[0], Hi=grid_in[1], Wi=grid_in[2], Do=out[0], Ho=out[1], Wo=out[2],
@@ -129,59 +135,99 @@ def _bf16_2d(t, rows, cols):
     return out
 
 
+CH_ALIGN = 64   # channel multiple of the conv3d kernels' 64-wide tiles (forward, input and weight gradients)
+
+
+def _ceil(c, m=CH_ALIGN):
+    return (c + m - 1) // m * m
+
+
+def _pad_channels(t, c_to):
+    """[..., C] -> [..., c_to] with zero channels appended (a device copy; no-op when C == c_to)."""
+    if t.shape[-1] == c_to:
+        return t.contiguous()
+    out = t.new_zeros(*t.shape[:-1], c_to)
+    out[..., : t.shape[-1]] = t
+    return out
+
+
 class _Conv3dFn(torch.autograd.Function):
-    """y = conv(x, w) + b with w in kernel layout [Cout, taps * Cin] (fp32 master)."""
+    """y = conv(x, w) + b with w in kernel layout [Cout, taps * Cin] (fp32 master).
+
+    Channel counts that are not multiples of 64 (a first layer on raw point features, a 32-channel
+    U-Net level) run on zero-padded channels: x and W^T get zero input channels, W and b zero
+    output channels, and the padded output / gradient channels are sliced off.  Zero channels
+    contribute exact zeros, so results equal the unpadded convolution's."""
 
     @staticmethod
-    def forward(ctx, x, wk, bias, k, s, p, transposed, out_dtype):
+    def forward(ctx, x, wk, bias, k, s, p, transposed, out_dtype, op):
         if not x.is_cuda:
             raise RuntimeError("pcs_amd conv3d runs on a HIP device only (no CPU fallback)")
         if x.dtype != torch.bfloat16 or x.dim() != 5:
             raise ValueError("x must be a bf16 [B, D, H, W, C] channels-last voxel grid")
-        x = x.contiguous()
         B, D, H, W, cin = x.shape
-        cout = wk.shape[0]
-        g = _geom(B, (D, H, W), cin, cout, k, s, p, transposed)
-        wb = _bf16_2d(wk, cout, wk.shape[1])
-        y = torch.empty(B, g.Do, g.Ho, g.Wo, cout, dtype=out_dtype, device=x.device)
-        L.call("pcs_conv3d", ct.byref(g), L.ptr(x), L.ptr(wb),
-               L.ptr(bias.float().contiguous()) if bias is not None else None, L.ptr(y),
+        cout, taps = wk.shape[0], k ** 3
+        if wk.shape[1] != taps * cin:
+            raise ValueError(f"weight has {wk.shape[1] // taps} input channels, x has {cin}")
+        cin_k, cout_k = _ceil(cin), _ceil(cout)
+        g = _geom(B, (D, H, W), cin_k, cout_k, k, s, p, transposed, op)
+        xk = _pad_channels(x, cin_k)
+        if (cin_k, cout_k) != (cin, cout):
+            wp = wk.new_zeros(cout_k, taps, cin_k)
+            wp[:cout, :, :cin] = wk.reshape(cout, taps, cin)
+            wk = wp.reshape(cout_k, taps * cin_k)
+        wb = _bf16_2d(wk, cout_k, taps * cin_k)
+        bk = None
+        if bias is not None:
+            bk = bias.float().contiguous() if cout_k == cout else _pad_channels(bias.float(), cout_k)
+        y = torch.empty(B, g.Do, g.Ho, g.Wo, cout_k, dtype=out_dtype, device=x.device)
+        L.call("pcs_conv3d", ct.byref(g), L.ptr(xk), L.ptr(wb), L.ptr(bk) if bk is not None else None, L.ptr(y),
                L.BF16 if out_dtype == torch.bfloat16 else L.F32, L.stream_ptr(x.device))
-        ctx.save_for_backward(x, wb)
-        ctx.cfg = (k, s, p, transposed, bias is not None)
-        return y
+        ctx.save_for_backward(xk, wb)
+        ctx.cfg = (k, s, p, transposed, bias is not None, op, cin, cout)
+        return y if cout_k == cout else y[..., :cout].contiguous()
 
     @staticmethod
     def backward(ctx, dy):
-        x, wb = ctx.saved_tensors
-        k, s, p, transposed, has_bias = ctx.cfg
-        B, D, H, W, cin = x.shape
-        cout = wb.shape[0]
+        xk, wb = ctx.saved_tensors
+        k, s, p, transposed, has_bias, op, cin, cout = ctx.cfg
+        B, D, H, W, cin_k = xk.shape
+        cout_k = wb.shape[0]
         taps = k ** 3
-        g = _geom(B, (D, H, W), cin, cout, k, s, p, transposed)
+        g = _geom(B, (D, H, W), cin_k, cout_k, k, s, p, transposed, op)
         M = B * g.Do * g.Ho * g.Wo
-        dyb = _bf16_2d(dy.reshape(M, cout), M, cout)
-        dev, st = x.device, L.stream_ptr(x.device)
+        dyb = _bf16_2d(_pad_channels(dy, cout_k).reshape(M, cout_k), M, cout_k)
+        dev, st = xk.device, L.stream_ptr(xk.device)
         dx = dwk = db = None
         if ctx.needs_input_grad[0]:
             # the input gradient of a convolution is the transposed convolution of dy with W_t^T
-            # (and vice versa): same k, s, p, grids swapped
-            wt = torch.empty(cin, taps * cout, dtype=torch.bfloat16, device=dev)
-            L.call("pcs_conv3d_weight_t", L.ptr(wb), cout, taps, cin, L.ptr(wt), st)
-            gb = _geom(B, (g.Do, g.Ho, g.Wo), cout, cin, k, s, p, not transposed)
+            # (and vice versa): same k, s, p, grids swapped.  A strided convolution whose floor
+            # division skipped trailing input planes gets them back as the transposed form's
+            # output_padding; a transposed one's own output_padding planes are read as rows of dy.
+            wt = torch.empty(cin_k, taps * cout_k, dtype=torch.bfloat16, device=dev)
+            L.call("pcs_conv3d_weight_t", L.ptr(wb), cout_k, taps, cin_k, L.ptr(wt), st)
+            back_op = (0, 0, 0)
+            if not transposed:
+                back_op = tuple(d - _out_size(o, k, s, p, True) for d, o in zip((D, H, W), (g.Do, g.Ho, g.Wo)))
+            gb = _geom(B, (g.Do, g.Ho, g.Wo), cout_k, cin_k, k, s, p, not transposed, back_op)
             if (gb.Do, gb.Ho, gb.Wo) != (D, H, W):
                 raise ValueError("input gradient: the strided output grid does not map back onto the input grid")
-            dx = torch.empty_like(x)
+            dx = torch.empty_like(xk)
             L.call("pcs_conv3d", ct.byref(gb), L.ptr(dyb), L.ptr(wt), None, L.ptr(dx), L.BF16, st)
+            if cin_k != cin:
+                dx = dx[..., :cin].contiguous()
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
             nbytes = L.load().pcs_conv3d_wgrad_workspace(ct.byref(g))
             if nbytes < 0:
                 raise L.PcsError(L.load().pcs_last_error().decode())
             ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-            dwk = torch.empty(cout, taps * cin, dtype=torch.float32, device=dev)
-            db = torch.empty(cout, dtype=torch.float32, device=dev) if has_bias else None
-            L.call("pcs_conv3d_wgrad", ct.byref(g), L.ptr(x), L.ptr(dyb), L.ptr(ws), nbytes, L.ptr(dwk), L.ptr(db), st)
-        return dx, dwk, db, None, None, None, None, None
+            dwk = torch.empty(cout_k, taps * cin_k, dtype=torch.float32, device=dev)
+            db = torch.empty(cout_k, dtype=torch.float32, device=dev) if has_bias else None
+            L.call("pcs_conv3d_wgrad", ct.byref(g), L.ptr(xk), L.ptr(dyb), L.ptr(ws), nbytes, L.ptr(dwk), L.ptr(db), st)
+            if (cin_k, cout_k) != (cin, cout):
+                dwk = dwk.reshape(cout_k, taps, cin_k)[:cout, :, :cin].reshape(cout, taps * cin)
+                db = db[:cout] if db is not None else None
+        return dx, dwk, db, None, None, None, None, None, None
 
 
 def conv3d(x, weight, bias=None, stride=1, padding=0, out_dtype=torch.bfloat16):
@@ -189,15 +235,17 @@ def conv3d(x, weight, bias=None, stride=1, padding=0, out_dtype=torch.bfloat16):
     weight [Cout, Cin, k, k, k] (torch layout, fp32), bias [Cout] or None."""
     cout, cin, k = weight.shape[0], weight.shape[1], weight.shape[2]
     wk = weight.permute(0, 2, 3, 4, 1).reshape(cout, k ** 3 * cin)
-    return _Conv3dFn.apply(x, wk, bias, k, int(stride), int(padding), False, out_dtype)
+    return _Conv3dFn.apply(x, wk, bias, k, int(stride), int(padding), False, out_dtype, 0)
 
 
-def conv_transpose3d(x, weight, bias=None, stride=2, padding=0, out_dtype=torch.bfloat16):
+def conv_transpose3d(x, weight, bias=None, stride=2, padding=0, out_dtype=torch.bfloat16, output_padding=0):
     """torch.nn.functional.conv_transpose3d on a channels-last bf16 grid x [B, D, H, W, Cin];
-    weight [Cin, Cout, k, k, k] (torch layout, fp32), bias [Cout] or None."""
+    weight [Cin, Cout, k, k, k] (torch layout, fp32), bias [Cout] or None; output_padding as
+    torch's (an int or 3 ints, each < stride)."""
     cin, cout, k = weight.shape[0], weight.shape[1], weight.shape[2]
     wk = weight.permute(1, 2, 3, 4, 0).reshape(cout, k ** 3 * cin)
-    return _Conv3dFn.apply(x, wk, bias, k, int(stride), int(padding), True, out_dtype)
+    op = (int(output_padding),) * 3 if isinstance(output_padding, int) else tuple(int(o) for o in output_padding)
+    return _Conv3dFn.apply(x, wk, bias, k, int(stride), int(padding), True, out_dtype, op)
 
 
 class Conv3d(torch.nn.Module):
@@ -218,11 +266,11 @@ class ConvTranspose3d(torch.nn.Module):
     """nn.ConvTranspose3d(cin, cout, k, stride, padding) with torch's parameter layout and init,
     on channels-last bf16 voxel grids (pcs_conv3d, transposed form)."""
 
-    def __init__(self, cin, cout, kernel_size=2, stride=2, padding=0, bias=True):
+    def __init__(self, cin, cout, kernel_size=2, stride=2, padding=0, output_padding=0, bias=True):
         super().__init__()
-        ref = torch.nn.ConvTranspose3d(cin, cout, kernel_size, stride, padding, bias=bias)
+        ref = torch.nn.ConvTranspose3d(cin, cout, kernel_size, stride, padding, output_padding, bias=bias)
         self.weight, self.bias = ref.weight, ref.bias
-        self.stride, self.padding = stride, padding
+        self.stride, self.padding, self.output_padding = stride, padding, output_padding
 
     def forward(self, x, out_dtype=torch.bfloat16):
-        return conv_transpose3d(x, self.weight, self.bias, self.stride, self.padding, out_dtype)
+        return conv_transpose3d(x, self.weight, self.bias, self.stride, self.padding, out_dtype, self.output_padding)

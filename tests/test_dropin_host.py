@@ -1,5 +1,5 @@
 """Host-side drop-in checks (no GPU): constructor limits fail at construction with a
-documented message (P:66-83 accepts any value; the kernels cover input_dim 1..8 and 1..64
+documented message (P:66-83 accepts any value; the kernels cover input_dim 1..8 and 1..256
 classes), the state-dict layout at non-default sizes, and per-replica dropout state under
 DataParallel's replication (torch/nn/parallel/replicate.py shallow-copies __dict__)."""
 import pytest
@@ -8,13 +8,13 @@ import pointnet_oracle as orc
 from pcs_amd.model import PointNetSegmentation
 
 
-@pytest.mark.parametrize("C,D", [(65, 4), (0, 4), (2, 9), (2, 0)])
+@pytest.mark.parametrize("C,D", [(257, 4), (0, 4), (2, 9), (2, 0)])
 def test_unsupported_sizes_raise_at_construction(C, D):
     with pytest.raises(ValueError, match="pcs_amd supports"):
         PointNetSegmentation(C, input_dim=D)
 
 
-@pytest.mark.parametrize("C,D", [(20, 4), (3, 3), (64, 8)])
+@pytest.mark.parametrize("C,D", [(20, 4), (3, 3), (64, 8), (65, 4), (256, 2)])
 def test_state_dict_layout_generic_sizes(C, D):
     m = PointNetSegmentation(C, input_dim=D)
     sd = m.state_dict()

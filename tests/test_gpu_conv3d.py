@@ -31,7 +31,18 @@ CASES = [
     (3, 1, 1, True, (4, 5, 3), 64, 64),       # transposed stencil (= flipped convolution)
     (3, 2, 1, True, (3, 4, 2), 64, 128),      # strided transposed stencil
     (3, 2, 1, True, (1, 4, 2), 64, 64),       # output depth 1: two parity classes are empty
+    (3, 2, 1, False, (6, 6, 8), 64, 64),      # strided stencil, even grid (input grad needs op = 1)
+    (2, 2, 0, False, (7, 5, 7), 64, 128),     # 2x2x2 down on an odd grid (skipped last plane)
+    (3, 2, 1, True, (3, 4, 2), 64, 64, 1),    # transposed with output_padding 1
+    (2, 2, 0, True, (3, 2, 4), 64, 64, (1, 0, 1)),   # 2x2x2 up with per-dimension output_padding
+    (3, 1, 1, False, (4, 3, 5), 32, 64),      # the U-Net's 32-channel level (padded to 64)
+    (3, 1, 1, False, (5, 4, 3), 4, 32),       # raw point features in, 32 channels out (padded)
+    (2, 2, 0, True, (2, 3, 2), 64, 32),       # transposed up to a 32-channel level
 ]
+
+
+def _case(c):
+    return c if len(c) == 8 else c + (0,)
 
 
 def _operands(k, transposed, grid, cin, cout, B=2, seed=0):
@@ -43,17 +54,28 @@ def _operands(k, transposed, grid, cin, cout, B=2, seed=0):
     return x, w, b
 
 
-def _ref(x, w, b, s, p, transposed):
-    f = F.conv_transpose3d if transposed else F.conv3d
-    return f(_ncdhw(x), w.double(), b.double(), stride=s, padding=p).permute(0, 2, 3, 4, 1)
+def _ref_fn(transposed, op):
+    if transposed:
+        return lambda *a, **kw: F.conv_transpose3d(*a, output_padding=op, **kw)
+    return F.conv3d
 
 
-@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout", CASES)
-def test_forward_matches_torch(k, s, p, transposed, grid, cin, cout):
+def _fn(V, transposed, op):
+    if transposed:
+        return lambda *a, **kw: V.conv_transpose3d(*a, output_padding=op, **kw)
+    return V.conv3d
+
+
+def _ref(x, w, b, s, p, transposed, op=0):
+    return _ref_fn(transposed, op)(_ncdhw(x), w.double(), b.double(), stride=s, padding=p).permute(0, 2, 3, 4, 1)
+
+
+@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout,op", [_case(c) for c in CASES])
+def test_forward_matches_torch(k, s, p, transposed, grid, cin, cout, op):
     import pcs_amd.voxel as V
     x, w, b = _operands(k, transposed, grid, cin, cout)
-    ref = _ref(x, w, b, s, p, transposed)
-    f = V.conv_transpose3d if transposed else V.conv3d
+    ref = _ref(x, w, b, s, p, transposed, op)
+    f = _fn(V, transposed, op)
     y = f(x.to(DEV), w.to(DEV), b.to(DEV), s, p, out_dtype=torch.float32)
     yb = f(x.to(DEV), w.to(DEV), b.to(DEV), s, p, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
@@ -77,23 +99,23 @@ def test_forward_large_tiles(k, s, p, transposed, grid, cin, cout):
     assert _rel(y, ref) < 2e-5
 
 
-@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout", CASES)
-def test_backward_matches_torch(k, s, p, transposed, grid, cin, cout):
+@pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout,op", [_case(c) for c in CASES])
+def test_backward_matches_torch(k, s, p, transposed, grid, cin, cout, op):
+    """Every case, including even grids under a stride (the input gradient's output_padding),
+    odd grids under the 2x2x2 down layer and channel counts off the 64 multiple (padded)."""
     import pcs_amd.voxel as V
-    if cin % 64:
-        pytest.skip("the weight gradient and the input gradient's GEMM need channels in multiples of 64")
     x, w, b = _operands(k, transposed, grid, cin, cout, seed=1)
     xr = _ncdhw(x).requires_grad_()
     wr, br = w.double().requires_grad_(), b.double().requires_grad_()
-    f_ref = F.conv_transpose3d if transposed else F.conv3d
-    yr = f_ref(xr, wr, br, stride=s, padding=p)
+    yr = _ref_fn(transposed, op)(xr, wr, br, stride=s, padding=p)
     g = torch.Generator().manual_seed(2)
     dy = torch.randn(yr.shape, generator=g, dtype=torch.float64).to(torch.bfloat16).double()   # bf16-exact
     yr.backward(dy)
     xd = x.to(DEV).requires_grad_()
     wd, bd = w.to(DEV).requires_grad_(), b.to(DEV).requires_grad_()
-    f = V.conv_transpose3d if transposed else V.conv3d
+    f = _fn(V, transposed, op)
     y = f(xd, wd, bd, s, p, out_dtype=torch.float32)
+    assert tuple(y.shape) == (yr.shape[0],) + tuple(yr.shape[2:]) + (yr.shape[1],)
     y.backward(dy.permute(0, 2, 3, 4, 1).float().to(DEV))
     torch.cuda.synchronize()
     assert _rel(wd.grad, wr.grad) < 1e-5

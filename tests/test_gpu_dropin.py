@@ -126,10 +126,11 @@ def test_replicas_in_threads_match_sequential():
     assert float(g1["global_feat.weight"].abs().sum()) > 0
 
 
-@pytest.mark.parametrize("C,D", [(20, 4), (3, 3), (64, 4)])
+@pytest.mark.parametrize("C,D", [(20, 4), (3, 3), (64, 4), (65, 4), (150, 4), (256, 2)])
 def test_classes_and_input_dim_fp32_parity(C, D):
     """Non-default num_classes / input_dim against the fp64 oracle (the oracle is generic in
-    both; parity unpinned by reference fixtures for these shapes)."""
+    both; parity unpinned by reference fixtures for these shapes).  C > 64 runs the wide head
+    (csrc/small.hip head_wide_kernel)."""
     from pcs_amd.data import synthetic_batch
     from pcs_amd.model import PointNetSegmentation
     sd = orc.init_params(C, 41 + C, input_dim=D, bn_affine_random=True)
