@@ -38,15 +38,14 @@ constexpr int MS = 32;    // rows per step
 
 template <int COUT> struct SegCfg {
   static constexpr int NST = COUT == 256 ? 3 : 4;          // ring stages
-  static constexpr int DZB = MS * COUT * 2;                 // raw dZ / Y slab bytes (rows unpadded)
-  static constexpr int YPB = MS * CB * 2;                   // raw Yp slab (XOR-swizzled slots)
+  static constexpr int DZB = MS * COUT * 2;                 // dZ (-> dy in place) / Y slab bytes
+  static constexpr int YPB = MS * CB * 2;                   // Yp slab
   static constexpr int MKB = MS * CB / 8;                   // dropout bits (512 B)
   static constexpr int STAGE = 2 * DZB + YPB + MKB;
-  static constexpr int DYR = COUT * 2 + 32;                 // dy row stride (32-B pad, prow rows)
-  static constexpr int XR = CB * 2 + 32;                    // x row stride
-  static constexpr int OFF_DY = NST * STAGE;                // dy [MS][DYR]
-  static constexpr int OFF_X = OFF_DY + MS * DYR;           // x [MS][XR]
-  static constexpr int OFF_CF = OFF_X + MS * XR;            // alpha | beta | gamma [COUT], es | et [CB]
+  static constexpr int XR = CB * 2 + 32;                    // x row stride (32-B pad, prow rows)
+  static constexpr int XB = MS * XR;                        // one x buffer
+  static constexpr int OFF_X = NST * STAGE;                 // x [2][MS][XR]
+  static constexpr int OFF_CF = OFF_X + 2 * XB;             // alpha | beta | gamma [COUT], es | et [CB]
   static constexpr int BYTES = OFF_CF + (3 * COUT + 2 * CB) * 4;
   static_assert(BYTES <= 160 * 1024, "LDS budget");
   static constexpr int KS = COUT / 32;                      // dgrad k-steps (32 deep)
@@ -58,6 +57,7 @@ template <int COUT> struct SegCfg {
   static_assert((2 * DZP + YPP) % 8 == 0, "uniform pieces per wave");
   static constexpr int VM_STEP = NPW + 1;                   // vector-memory loads per wave per step
   static constexpr int DY_RPT = MS * SPR / THREADS;         // dy slots per thread per step
+  static_assert(DY_RPT == 1 || DY_RPT == 2, "transform passes");
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -70,23 +70,25 @@ PCS_DEV int xcd_remap(int bid, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
-// LDS-DMA: 64 lanes x 16 B (or x 4 B) from sbase + voff (per lane) to lds_dst + lane * size
-PCS_DEV void glds16(const char *sbase, uint32_t voff, char *lds_dst) {
-  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t *)lds_dst;
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(m0v)
-               : "memory");
+// LDS-DMA: 64 lanes x 16 B (or x 4 B) from sbase + voff (per lane) to the LDS address in M0
+// (+ lane * size).  Inline asm so that the compiler's own wait insertion neither drains these
+// loads before unrelated LDS reads nor spills their addresses: the kernel counts them itself.
+// M0 is set from a per-step SGPR base plus an immediate (one SALU per piece); the caller
+// saves M0 before a group of pieces and restores it after (m0_save / m0_restore).
+template <int OFF> PCS_DEV void glds16o(const char *sbase, uint32_t voff, uint32_t m0base) {
+  asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0base), "n"(OFF) : "memory", "scc");
 }
-PCS_DEV void glds4(const char *sbase, uint32_t voff, char *lds_dst) {
-  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t *)lds_dst;
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(m0v)
-               : "memory");
+template <int OFF> PCS_DEV void glds4o(const char *sbase, uint32_t voff, uint32_t m0base) {
+  asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0base), "n"(OFF) : "memory", "scc");
 }
+PCS_DEV uint32_t m0_save() {
+  uint32_t k;
+  asm volatile("s_mov_b32 %0, m0" : "=s"(k));
+  return k;
+}
+PCS_DEV void m0_restore(uint32_t k) { asm volatile("s_mov_b32 m0, %0" ::"s"(k)); }
 template <int N> PCS_DEV void wait_vm() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -98,12 +100,18 @@ PCS_DEV void barrier_lds() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// LDS layouts.  The raw ring slabs are written by LDS-DMA (linear per piece): dZ / Y rows stay
-// unpadded (the transform reads them lane-linearly, conflict free); Yp's 16-B slots are
-// XOR-permuted by (row & 15) on the DMA source address, so the epilogue's 8-B reads of 16 rows
-// at one column hit 16 distinct slots.  dy and x are written by the transform, so they get the
-// layout of fused_bwd.hip: rows padded by 32 B and permuted (row bits 2 <-> 3), which makes the
-// ds_read_b128 fragment reads and the transposed ds_read_b64_tr_b16 reads conflict free.
+// LDS layouts.  The ring stages are written by LDS-DMA (linear per 1-KB piece), so the slot
+// permutations go on the DMA source addresses:
+// * dZ / Y rows (unpadded): 16-B chunk c of row r at chunk c ^ ftr(r), ftr an even value
+//   distinct over each row set a fragment read or a transposed read touches -- the dgrad's
+//   ds_read_b128 (16 rows, one chunk) and the wgrad's ds_read_b64_tr_b16 (rows {0-3, 8-11} or
+//   {4-7, 12-15}, two chunks) are both bank-conflict free (checked with the guide's bank model).
+//   The transform reads dZ and Y lane-linearly and writes dy back in place, so dy keeps it.
+// * Yp: chunk c of row r at c ^ (r & 15): the epilogue's 8-B reads of 16 rows at one column
+//   hit 16 distinct chunks.
+// * x (written by the transform): rows padded by 32 B and permuted (row bits 2 <-> 3), the
+//   layout of fused_bwd.hip, conflict free for the transposed reads.
+PCS_DEV int ftr(int row) { return ((row & 3) << 1) | (row & 8); }
 PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 PCS_DEV int fyp(int row) { return row & 15; }
 
@@ -135,6 +143,7 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
                                                           int64_t rows_per_split) {
   typedef SegCfg<COUT> F;
   constexpr int NBLK = CIN / CB;
+  constexpr int ROWB = COUT * 2;   // dZ / Y / dy row bytes
   __shared__ __attribute__((aligned(16))) char lds[F::BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -157,19 +166,21 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
   bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
   const float ks = MASK ? a.c_keep_scale : 1.f;
 
-  // ---- DMA of step s into ring stage s % NST.  Piece j = wid + 8 i of the step: dZ [0, DZP),
-  // Y [DZP, 2 DZP), Yp [2 DZP, 2 DZP + YPP), then one dword piece of the dropout bits (waves
-  // 0 / 1 take its two halves; the others repeat them, writing the same bytes, so that every
-  // wave issues the same count; without bits they read Yp's rows, never used).  Per-lane
-  // offsets relative to the step's first row; rows past the slice clamp to its last row.
+  // ---- DMA of step s into ring stage sidx.  Piece j = wid + 8 i of the step, 1 KB each, laid
+  // out contiguously in the stage: dZ [0, DZP), Y [DZP, 2 DZP), Yp [2 DZP, 2 DZP + YPP) (a
+  // round i has one kind for every wave: DZP is a multiple of 8), then one dword piece of the
+  // dropout bits (waves 0 / 1 take its two halves; the others repeat them, writing the same
+  // bytes, so that every wave issues the same count; without bits they read Yp's rows, never
+  // used).  Per-lane source offsets relative to the step's first row, carrying the slot
+  // swizzles; rows past the slice clamp to its last row (their LDS rows are never used).
+  static_assert(F::DZP % 8 == 0, "piece rounds of one kind");
   auto piece_off = [&](int i, int lastr) -> uint32_t {
-    const int j = wid + 8 * i;
-    if (j < 2 * F::DZP) {
-      const int pj = j < F::DZP ? j : j - F::DZP;
-      const int r = pj * (1024 / (COUT * 2)) + lane / F::SPR;
-      return (uint32_t)(min(r, lastr) * COUT * 2 + (lane % F::SPR) * 16);
+    if (8 * i < 2 * F::DZP) {
+      const int pj = (8 * i < F::DZP ? 8 * i : 8 * i - F::DZP) + wid;
+      const int r = pj * (1024 / ROWB) + lane / F::SPR;
+      return (uint32_t)(min(r, lastr) * ROWB + (((lane % F::SPR) ^ ftr(r)) << 4));
     }
-    const int r = (j - 2 * F::DZP) * 4 + (lane >> 4);
+    const int r = (8 * i - 2 * F::DZP + wid) * 4 + (lane >> 4);
     return (uint32_t)(min(r, lastr) * CIN * 2 + (((lane & 15) ^ fyp(r)) << 4));
   };
   auto mask_off = [&](int lastr) -> uint32_t {
@@ -180,40 +191,45 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
 #pragma unroll
   for (int i = 0; i < F::NPW; ++i) voff[i] = piece_off(i, MS - 1);
   voff[F::NPW] = mask_off(MS - 1);
-  auto dma_step = [&](int s) {
-    char *st = lds + (s % F::NST) * F::STAGE;
+  const uint32_t lds_m0 = (uint32_t)(uintptr_t)(lds_void_t *)lds;
+  auto dma_issue = [&](int sidx, int64_t m0, const uint32_t (&vo)[F::NPW + 1]) {
+    const uint32_t mb = lds_m0 + sidx * F::STAGE + wid * 1024;
+    const char *bdz = dZg + (sbase + m0) * ROWB;
+    const char *by = Yg + (sbase + m0) * ROWB;
+    const char *byp = Ypg + (sbase + m0) * (CIN * 2);
+    const char *bmk = MASK ? Mkg + (sbase + m0) * (CIN / 8) : byp;
+    const uint32_t keep = m0_save();
+    glds16o<0>(bdz, vo[0], mb);
+    if constexpr (F::NPW == 5) {   // COUT 256: dZ dZ Y Y Yp
+      glds16o<8192>(bdz, vo[1], mb);
+      glds16o<16384>(by, vo[2], mb);
+      glds16o<24576>(by, vo[3], mb);
+      glds16o<32768>(byp, vo[4], mb);
+    } else {                       // COUT 128: dZ Y Yp
+      static_assert(F::NPW == 3, "piece rounds");
+      glds16o<8192>(by, vo[1], mb);
+      glds16o<16384>(byp, vo[2], mb);
+    }
+    glds4o<2 * F::DZB + F::YPB>(bmk, vo[F::NPW], lds_m0 + sidx * F::STAGE + (wid & 1) * 256);
+    m0_restore(keep);
+  };
+  auto dma_step = [&](int s, int sidx) {
     const int64_t m0 = pcs_min64(lo + (int64_t)s * MS, hi - 1);
     const int lastr = (int)pcs_min64(hi - 1 - m0, MS - 1);
-    uint32_t vo[F::NPW + 1];
     if (lastr == MS - 1) {   // uniform: a full step
-#pragma unroll
-      for (int i = 0; i <= F::NPW; ++i) vo[i] = voff[i];
+      dma_issue(sidx, m0, voff);
     } else {
+      uint32_t vt[F::NPW + 1];
 #pragma unroll
-      for (int i = 0; i < F::NPW; ++i) vo[i] = piece_off(i, lastr);
-      vo[F::NPW] = mask_off(lastr);
+      for (int i = 0; i < F::NPW; ++i) vt[i] = piece_off(i, lastr);
+      vt[F::NPW] = mask_off(lastr);
+      dma_issue(sidx, m0, vt);
     }
-#pragma unroll
-    for (int i = 0; i < F::NPW; ++i) {
-      const int j = wid + 8 * i;
-      if (j < F::DZP)
-        glds16(dZg + (sbase + m0) * (COUT * 2), vo[i], st + j * 1024);
-      else if (j < 2 * F::DZP)
-        glds16(Yg + (sbase + m0) * (COUT * 2), vo[i], st + F::DZB + (j - F::DZP) * 1024);
-      else
-        glds16(Ypg + (sbase + m0) * (CIN * 2), vo[i], st + 2 * F::DZB + (j - 2 * F::DZP) * 1024);
-    }
-    if constexpr (MASK)
-      glds4(Mkg + (sbase + m0) * (CIN / 8), vo[F::NPW], st + 2 * F::DZB + F::YPB + (wid & 1) * 256);
-    else
-      glds4(Ypg + (sbase + m0) * (CIN * 2), vo[F::NPW], st + 2 * F::DZB + F::YPB + (wid & 1) * 256);
   };
 
-  // ---- per-thread constants: transform coefficients (registers), W^T fragments of this wave's
-  // dgrad column tile (ct = wave), epilogue coefficients of this lane's 4 columns
-  const int dlc = tid % F::SPR, drr = tid / F::SPR;   // dy slot: chunk, first row
-  const int xlc = tid & 15, xrr = tid >> 4;             // x slot: chunk, row
-  {   // transform coefficients in LDS (registers go to the MFMA operand pipelines)
+  // ---- transform coefficients in LDS (split layout), W^T fragments of this wave's dgrad
+  // column tile (ct = wave) in registers, epilogue coefficients of this lane's 4 columns
+  {
     float *cf = reinterpret_cast<float *>(lds + F::OFF_CF);
     for (int i = tid; i < COUT; i += THREADS) {
       const int j = split_idx(i, COUT);
@@ -227,7 +243,11 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       cf[3 * COUT + CB + j] = a.et[n0 + tid];
     }
   }
-  const char *cfd = lds + F::OFF_CF + dlc * 16;
+  const int dlc = tid % F::SPR, drr = tid / F::SPR;   // dy: physical slot, first row
+  const int xlc = tid & 15, xrr = tid >> 4;             // x: chunk, row
+  // the dy slot's logical chunk is the same for all its rows (they differ by 16 rows: ftr is
+  // periodic in 16), so one set of coefficients serves every pass
+  const char *cfd = lds + F::OFF_CF + (dlc ^ ftr(drr)) * 16;
   const char *cfx = lds + F::OFF_CF + 3 * COUT * 4 + xlc * 16;
   const int l16 = lane & 15, g = lane >> 4;
   const int ct = wid;
@@ -240,21 +260,30 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
   for (int kk = 0; kk < F::KS; ++kk)
     wfr[kk] = *reinterpret_cast<const u32x4 *>(Wt + (int64_t)(n0 + ct * 16 + l16) * COUT + (4 * kk + g) * 8);
 
-  // loop-invariant LDS offsets (the k-steps / tiles / passes then differ by immediates)
-  const int o_tr = tid * 16;                                           // raw dZ / Y, pass i: + i 8 KB
-  const int o_dyw = F::OFF_DY + prow(drr) * F::DYR + dlc * 16;         // dy write, pass i: + 16 i rows
+  // loop-invariant LDS offsets, relative to a stage (or an x buffer); the k-steps / tiles /
+  // passes then differ by immediates
+  const int o_tr = tid * 16;                        // dZ / Y / dy of the transform, pass i: + i 8 KB
   const int o_ypx = 2 * F::DZB + xrr * (CB * 2) + ((xlc ^ fyp(xrr)) << 4);
   const int o_mkx = 2 * F::DZB + F::YPB + xrr * 16 + xlc;
-  const int o_xw = F::OFF_X + prow(xrr) * F::XR + xlc * 16;
+  const int o_xw = prow(xrr) * F::XR + xlc * 16;
   const int o_ype = 2 * F::DZB + l16 * (CB * 2) + ((((cc >> 3) ^ l16) << 4) | ((cc & 7) << 1));   // + u 4 KB
   const int o_mke = 2 * F::DZB + F::YPB + l16 * 16 + (cc >> 3);                                     // + u 256
-  const int o_dg = F::OFF_DY + prow(l16) * F::DYR + g * 16;   // dgrad: + u 16 rows, + kk 64 B
-  const int q = (lane >> 2) & 3, p = lane & 3;                 // transposed-read lane roles
-  const int tr0 = prow(8 * g + q), tr1 = prow(8 * g + 4 + q);
-  const int o_ty0 = F::OFF_DY + tr0 * F::DYR + (16 * F::OBW * wid + 4 * p) * 2;   // + ob 32 B
-  const int o_ty1 = F::OFF_DY + tr1 * F::DYR + (16 * F::OBW * wid + 4 * p) * 2;
-  const int o_tx0 = F::OFF_X + tr0 * F::XR + 8 * p;   // + u 32 B
-  const int o_tx1 = F::OFF_X + tr1 * F::XR + 8 * p;
+  // dgrad fragment of k-step kk: logical chunk 4 kk + g of row 16 u + l16 sits at chunk
+  // (4 kk + g) ^ ftr(l16) = 16 (kk >> 2) + ((4 (kk & 3) + g) ^ ftr(l16))
+  int o_dg[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) o_dg[b] = l16 * ROWB + (((4 * b + g) ^ ftr(l16)) << 4);
+  const int q = (lane >> 2) & 3, p = lane & 3;      // transposed-read lane roles
+  const int tr0 = 8 * g + q, tr1 = 8 * g + 4 + q;   // dy rows (k) of the two 4-row halves
+  int o_ty[F::OBW][2];
+#pragma unroll
+  for (int ob = 0; ob < F::OBW; ++ob) {
+    const int s = 2 * (F::OBW * wid + ob) + (p >> 1);   // logical chunk of columns 16 (..) + 4 p
+    o_ty[ob][0] = tr0 * ROWB + ((s ^ ftr(tr0)) << 4) + 8 * (p & 1);
+    o_ty[ob][1] = tr1 * ROWB + ((s ^ ftr(tr1)) << 4) + 8 * (p & 1);
+  }
+  const int o_tx0 = prow(tr0) * F::XR + 8 * p;   // + u 32 B
+  const int o_tx1 = prow(tr1) * F::XR + 8 * p;
 
   f32x4 accw[F::OBW][8];
 #pragma unroll
@@ -265,26 +294,29 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
 #pragma unroll
   for (int r = 0; r < 4; ++r) { s1[r] = 0.f; s2[r] = 0.f; }
 
-  // ---- transform of step s (its DMA landed, barrier passed): dy and x (zeros past the slice)
-  auto transform = [&](int s) {
-    const char *st = lds + (s % F::NST) * F::STAGE;
-    const int64_t m0 = lo + (int64_t)s * MS;
-    float ca[8], cb[8], cg[8];
+  // ---- transform of step s (landed, barrier passed): dy in place over dZ, x into buffer s & 1;
+  // zeros past the slice.  Split in pieces so phase 2 can put the weight-gradient MFMAs of the
+  // previous step between them.
+  auto transform_dy = [&](int s, int sidx, int i) {
+    char *st = lds + sidx * F::STAGE;
+    const int rem = (int)pcs_min64(hi - (lo + (int64_t)s * MS), MS);   // rows of the step
+    float ca[8], cb[8], cg[8], v[8], y[8];
+    const u32x4 dz = *reinterpret_cast<const u32x4 *>(st + o_tr + i * THREADS * 16);
+    const u32x4 yy = *reinterpret_cast<const u32x4 *>(st + F::DZB + o_tr + i * THREADS * 16);
     lds_vec8(cfd, COUT * 2, ca);
     lds_vec8(cfd + COUT * 4, COUT * 2, cb);
     lds_vec8(cfd + 2 * COUT * 4, COUT * 2, cg);
+    unpack_chunk(dz, v);
+    unpack_chunk(yy, y);
 #pragma unroll
-    for (int i = 0; i < F::DY_RPT; ++i) {
-      const int r = drr + i * (THREADS / F::SPR);
-      float v[8], y[8];
-      unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o_tr + i * THREADS * 16), v);
-      unpack_chunk(*reinterpret_cast<const u32x4 *>(st + F::DZB + o_tr + i * THREADS * 16), y);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
-      const u32x4 out = pack_chunk(v);
-      *reinterpret_cast<u32x4 *>(lds + o_dyw + i * (THREADS / F::SPR) * F::DYR) =
-          m0 + r < hi ? out : mk_u32x4(0, 0, 0, 0);
-    }
+    for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
+    const u32x4 out = pack_chunk(v);
+    *reinterpret_cast<u32x4 *>(st + o_tr + i * THREADS * 16) =
+        drr + i * (THREADS / F::SPR) < rem ? out : mk_u32x4(0, 0, 0, 0);
+  };
+  auto transform_x = [&](int s, int sidx) {
+    const char *st = lds + sidx * F::STAGE;
+    const int rem = (int)pcs_min64(hi - (lo + (int64_t)s * MS), MS);
     float v[8], xs[8], xt[8];
     lds_vec8(cfx, CB * 2, xs);
     lds_vec8(cfx + CB * 4, CB * 2, xt);
@@ -296,39 +328,45 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       v[e] = ((mb >> e) & 1u) ? x * ks : 0.f;
     }
     const u32x4 out = pack_chunk(v);
-    *reinterpret_cast<u32x4 *>(lds + o_xw) = m0 + xrr < hi ? out : mk_u32x4(0, 0, 0, 0);
+    *reinterpret_cast<u32x4 *>(lds + F::OFF_X + (s & 1) * F::XB + o_xw) = xrr < rem ? out : mk_u32x4(0, 0, 0, 0);
   };
 
-  // ---- output rows of one step through a buffer descriptor (range: the slice's rows from m0)
-  auto store_rows = [&](int64_t m0, int vo, u32x4 v) {
-    const int64_t vr = pcs_max64(hi - m0, 0);
-    const uint32_t nbytes = vr > 0 ? (uint32_t)((vr - 1) * CIN * 2 + CB * 2) : 0u;
-    char *base = reinterpret_cast<char *>(Cg + (sbase + pcs_min64(m0, hi - 1)) * CIN + n0);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, vo, 0, 0);
-  };
-  const int o_st = (16 * (g & 1) + l16) * (CIN * 2) + (16 * ct + 8 * (g >> 1)) * 2;
+  // ---- output rows through one buffer descriptor for the slice (range: its rows): a store's
+  // rows past the slice are dropped by the hardware, so every wave issues exactly one store per
+  // step (the counted waits); the prologue's placeholder stores lie wholly out of range
+  const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<char *>(Cg + (sbase + lo) * CIN + n0), 0,
+      (int)(uint32_t)((hi - lo - 1) * CIN * 2 + CB * 2), 0x00020000);
+  const uint32_t o_st = (uint32_t)((16 * (g & 1) + l16) * (CIN * 2) + (16 * ct + 8 * (g >> 1)) * 2);
+  auto store_rows = [&](uint32_t vo, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, rs_out, (int)vo, 0, 0); };
 
   // ---- prologue: steps 0 .. NST-2 in flight (each followed by a store the range check drops,
   // as every loop step's DMA is followed by its epilogue store), step 0 landed and transformed
 #pragma unroll
   for (int s = 0; s < F::NST - 1; ++s) {
-    dma_step(s);
-    store_rows(hi, 0, mk_u32x4(0, 0, 0, 0));
+    dma_step(s, s);
+    store_rows(0xFFFFFF00u, mk_u32x4(0, 0, 0, 0));
   }
   wait_vm<1 + (F::NST - 2) * (F::VM_STEP + 1)>();
   barrier_lds();
-  transform(0);
+#pragma unroll
+  for (int i = 0; i < F::DY_RPT; ++i) transform_dy(0, 0, i);
+  transform_x(0, 0);
   barrier_lds();
 
+  // Per step t, two phases split by barriers:
+  //   phase 1: DMA of step t+NST-1; input gradient of step t (dy in stage t, W^T in registers)
+  //            and its epilogue (masks, S1 / S2, store);
+  //   phase 2: the weight gradient of step t (dy in stage t, x in buffer t & 1) interleaved
+  //            with the transform of step t+1 (stage t+1 in place, x into buffer (t+1) & 1):
+  //            MFMAs and VALU work of one wave with no dependence between them.
+  int sc = 0, sn = 1, sd = F::NST - 1;   // stages of steps t, t+1 and t+NST-1 (= t-1's)
+  uint32_t o_out = o_st;                 // this lane's store offset at step t
   for (int t = 0; t < nsteps; ++t) {
-    const int64_t m0 = lo + (int64_t)t * MS;
-    dma_step(t + F::NST - 1);   // into the stage step t-1 used (free since the last barrier)
-    const char *st = lds + (t % F::NST) * F::STAGE;
-    // input gradient out[m = 16 u + l16][c = 16 ct + 4 g + r] (both row tiles u), then the weight
-    // gradient dW[o = 16 (OBW wid + ob) + l16][c = 16 u + 4 g + r] over the step's 32 rows.  The
-    // LDS operand reads run PD k-steps ahead of the MFMAs (explicit ring; the scheduling
-    // barriers keep the compiler from collapsing it under register pressure).
+    const int rem = (int)pcs_min64(hi - (lo + (int64_t)t * MS), MS);
+    dma_step(t + F::NST - 1, sd);   // into the stage step t-1 used (free since the last barrier)
+    const char *st = lds + sc * F::STAGE;
+    const char *xb = lds + F::OFF_X + (t & 1) * F::XB;
     // (the epilogue's Yp values and dropout bits, read up front)
     uint2 ype[2];
     uint32_t kbe[2] = {0xFu, 0xFu};
@@ -337,41 +375,27 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       ype[u] = *reinterpret_cast<const uint2 *>(st + o_ype + u * 16 * (CB * 2));
       if constexpr (MASK) kbe[u] = (uint32_t)(uint8_t)st[o_mke + u * 256];
     }
+    // input gradient out[m = 16 u + l16][c = 16 ct + 4 g + r] (both row tiles u); the LDS
+    // operand reads run PD k-steps ahead of the MFMAs
     f32x4 accd[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     {
       constexpr int PD = 3;
       bf16x8 yf[PD + 1][2];
-      bf16x8 yt[F::OBW], xf[PD + 1];
       auto rd_dg = [&](int kk, bf16x8 (&d)[2]) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) d[u] = *reinterpret_cast<const bf16x8 *>(lds + o_dg + u * 16 * F::DYR + kk * 64);
+        for (int u = 0; u < 2; ++u)
+          d[u] = *reinterpret_cast<const bf16x8 *>(st + o_dg[kk & 3] + (kk >> 2) * 256 + u * 16 * ROWB);
       };
-      auto rd_x = [&](int u) { return tr_frag2(lds + o_tx0 + u * 32, lds + o_tx1 + u * 32); };
 #pragma unroll
       for (int kk = 0; kk < PD; ++kk) rd_dg(kk, yf[kk]);
 #pragma unroll
       for (int kk = 0; kk < F::KS; ++kk) {
         if (kk + PD < F::KS) rd_dg(kk + PD, yf[(kk + PD) % (PD + 1)]);
-        if (kk + PD == F::KS) {   // the weight gradient's first operands
-#pragma unroll
-          for (int ob = 0; ob < F::OBW; ++ob) yt[ob] = tr_frag2(lds + o_ty0 + ob * 32, lds + o_ty1 + ob * 32);
-        }
-        if (kk + PD > F::KS && kk + PD - F::KS - 1 < PD) xf[kk + PD - F::KS - 1] = rd_x(kk + PD - F::KS - 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
           accd[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wfr[kk]), yf[kk % (PD + 1)][u],
                                                            accd[u], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // (x fragments 0 .. PD-2 were issued above; keep PD-1 ahead)
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (u + PD - 1 < 8) xf[(u + PD - 1) % (PD + 1)] = rd_x(u + PD - 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ob = 0; ob < F::OBW; ++ob)
-          accw[ob][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u % (PD + 1)], yt[ob], accw[ob][u], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -380,15 +404,18 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       uint32_t pk[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const bool live = m0 + 16 * u + l16 < hi;
         const uint2 yp = ype[u];
         const float y[4] = {bf_lo(yp.x), bf_hi(yp.x), bf_lo(yp.y), bf_hi(yp.y)};
-        const uint32_t kb = MASK ? (kbe[u] >> (cc & 7)) & 0xFu : 0xFu;
+        // dropout bits of the lane's 4 columns, cleared for rows past the slice
+        const int kb = (int)((16 * u + l16 < rem ? 0xFu : 0u) & (MASK ? (kbe[u] >> (cc & 7)) : 0xFu));
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {   // (non-short-circuit: selects, no branches)
-          const bool keep = live & (((kb >> r) & 1u) != 0u) & (fmaf(y[r], es4[r], et4[r]) > 0.f);
-          v[r] = keep ? accd[u][r] * ks : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          // keep <=> bit set and z > 0: all-ones masks from the bit (sign-extended) and from the
+          // comparison, applied to the bits of the scaled gradient (VALU only, no SGPR masks)
+          const float z = fmaf(y[r], es4[r], et4[r]);
+          const int m = __builtin_amdgcn_sbfe(kb, r, 1) & (z > 0.f ? -1 : 0);
+          v[r] = __int_as_float(__float_as_int(accd[u][r] * ks) & m);
           s1[r] += v[r];
           s2[r] = fmaf(v[r], y[r], s2[r]);
         }
@@ -405,14 +432,39 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       }
       // a buffer store whose range ends at the slice's last row: rows past it are dropped by
       // the hardware, so every wave issues exactly one store per step (the counted waits)
-      store_rows(m0, o_st, mk_u32x4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]));
+      store_rows(o_out, mk_u32x4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]));
+      o_out += MS * CIN * 2;
     }
     // step t+1 landed: every older DMA done (the newer: the store above, step t+NST-1's
     // pieces, and the NST-2 steps' loads + stores in between)
     wait_vm<1 + (F::NST - 2) * (F::VM_STEP + 1)>();
     barrier_lds();
-    if (t + 1 < nsteps) transform(t + 1);
+    // phase 2: weight gradient dW[o = 16 (OBW wid + ob) + l16][c = 16 u + 4 g + r] over the 32
+    // rows of step t, with the transform of step t+1 between its MFMA groups
+    {
+      const bool more = t + 1 < nsteps;
+      bf16x8 yt[F::OBW], xf[2];
+#pragma unroll
+      for (int ob = 0; ob < F::OBW; ++ob) yt[ob] = tr_frag2(st + o_ty[ob][0], st + o_ty[ob][1]);
+      xf[0] = tr_frag2(xb + o_tx0, xb + o_tx1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u + 1 < 8) xf[(u + 1) & 1] = tr_frag2(xb + o_tx0 + (u + 1) * 32, xb + o_tx1 + (u + 1) * 32);
+#pragma unroll
+        for (int ob = 0; ob < F::OBW; ++ob)
+          accw[ob][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u & 1], yt[ob], accw[ob][u], 0, 0, 0);
+        // transform pieces after the MFMA groups 1, 3 (dy passes) and 5 (x)
+        if (more) {
+          if (u == 1) transform_dy(t + 1, sn, 0);
+          if (F::DY_RPT > 1 && u == 3) transform_dy(t + 1, sn, F::DY_RPT - 1);
+          if (u == 5) transform_x(t + 1, sn);
+        }
+      }
+    }
     barrier_lds();
+    sd = sc;
+    sc = sn;
+    sn = sn + 1 == F::NST ? 0 : sn + 1;
   }
   wait_vm<0>();   // the clamped DMAs past the end
 
