@@ -602,6 +602,44 @@ int pcs_conv3d_wgrad(const pcs_conv3d_geom *g, const void *X, const void *dY, vo
 /* W [Cout][taps][Cin] -> Wt [Cin][taps][Cout] (bf16) */
 int pcs_conv3d_weight_t(const void *W, int32_t Cout, int32_t taps, int32_t Cin, void *Wt, pcs_stream_t stream);
 
+/*
+ * Occupied-voxel (sparse) path: the north star's "hash-indexed gather" (BASELINE configs[2],
+ * SURVEY §8 f4; build-defined, the reference has no voxel grid: parity is against the numpy
+ * restatement oracle/sparse_oracle.py and against torch's dense conv3d on the occupied sites).
+ *   key = scene * G^3 + (ix * G + iy) * G + iz (the voxel key of pcs_voxelize: keys are in voxel
+ *         order, ascending).
+ * pcs_voxel_keys: keys[voxel_of_point[p]] = key of point p (the box / grid of pcs_voxelize).
+ * pcs_voxel_hash_*: open-addressing table, capacity a power of two >= 2 n
+ *   (pcs_voxel_hash_capacity); table_keys u64 [cap], table_vals i32 [cap] (row of the key);
+ *   find: out[i] = row of queries[i] or -1.
+ * pcs_sparse_neighbors: nbr [n][27] i32, nbr[v][t] = row of the voxel at (ix + a - 1, iy + b - 1,
+ *   iz + c - 1), t = (a * 3 + b) * 3 + c, same scene, or -1 (the tap order of a torch Conv3d
+ *   weight [Cout, Cin, 3, 3, 3] on a dense [B, C, G(x), G(y), G(z)] grid).
+ * pcs_sparse_conv: submanifold convolution Y[m] = b + sum_t W[tw(t)] X[nbr[m][t]] over the M rows
+ *   (X rows addressed by nbr), tw(t) = flip ? taps - 1 - t : t; X bf16 [*, Cin], W bf16
+ *   [Cout][taps][Cin], Y [M, Cout] in ydtype; Cin % 32 == 0, Cout % 64 == 0.  The input gradient
+ *   is the same call on dY with pcs_conv3d_weight_t(W) and flip = 1.  A 64-row tile runs only the
+ *   taps one of its rows has a neighbour at.
+ * pcs_sparse_conv_wgrad: dW [Cout][taps][Cin] f32 = sum_m dY[m] (x) X[nbr[m][t]], db [Cout] (may be
+ *   NULL); Cin, Cout % 64 == 0; fixed-order partial sums (deterministic).
+ */
+int pcs_voxel_keys(const float *points, const int64_t *offsets, int64_t num_scenes, int64_t T, int32_t grid,
+                   float lo_x, float lo_y, float lo_z, float hi_x, float hi_y, float hi_z,
+                   const int64_t *voxel_of_point, uint64_t *keys, pcs_stream_t stream);
+int64_t pcs_voxel_hash_capacity(int64_t n);
+int pcs_voxel_hash_build(const uint64_t *keys, int64_t n, uint64_t *table_keys, int32_t *table_vals,
+                         int64_t capacity, pcs_stream_t stream);
+int pcs_voxel_hash_find(const uint64_t *table_keys, const int32_t *table_vals, int64_t capacity,
+                        const uint64_t *queries, int64_t nq, int32_t *out, pcs_stream_t stream);
+int pcs_sparse_neighbors(const uint64_t *table_keys, const int32_t *table_vals, int64_t capacity,
+                         const uint64_t *keys, int64_t n, int32_t grid, int32_t *nbr, pcs_stream_t stream);
+int pcs_sparse_conv(const int32_t *nbr, int64_t M, int32_t taps, const void *X, int32_t Cin, const void *W,
+                    int32_t Cout, const float *bias, void *Y, int32_t ydtype, int32_t flip, pcs_stream_t stream);
+int64_t pcs_sparse_conv_wgrad_workspace(int64_t M, int32_t taps, int32_t Cin, int32_t Cout);   /* bytes */
+int pcs_sparse_conv_wgrad(const int32_t *nbr, int64_t M, int32_t taps, const void *X, int32_t Cin, const void *dY,
+                          int32_t Cout, void *workspace, int64_t workspace_bytes, float *dW, float *db,
+                          pcs_stream_t stream);
+
 /* Build-time identification and error string. */
 int pcs_abi_version(void);
 const char *pcs_last_error(void);

@@ -130,6 +130,14 @@ SIGNATURES = [
     ("pcs_conv3d_wgrad_workspace", _i64, [ct.POINTER(Conv3dGeom)]),
     ("pcs_conv3d_wgrad", ct.c_int, [ct.POINTER(Conv3dGeom), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     ("pcs_conv3d_weight_t", ct.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
+    ("pcs_sparse_conv", ct.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _i32, _vp]),
+    ("pcs_sparse_conv_wgrad_workspace", _i64, [_i64, _i32, _i32, _i32]),
+    ("pcs_sparse_conv_wgrad", ct.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _i64, _vp, _vp, _vp]),
+    ("pcs_voxel_keys", ct.c_int, [_vp, _vp, _i64, _i64, _i32, _f, _f, _f, _f, _f, _f, _vp, _vp, _vp]),
+    ("pcs_voxel_hash_capacity", _i64, [_i64]),
+    ("pcs_voxel_hash_build", ct.c_int, [_vp, _i64, _vp, _vp, _i64, _vp]),
+    ("pcs_voxel_hash_find", ct.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+    ("pcs_sparse_neighbors", ct.c_int, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp]),
     ("pcs_gram_workspace", _i64, [_i64, _i64, _i32, _i32, ct.POINTER(_i32)]),
     ("pcs_gram", ct.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     ("pcs_pool_rows_add", ct.c_int, [_vp, _i32, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i32,

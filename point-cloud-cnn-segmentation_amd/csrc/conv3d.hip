@@ -25,7 +25,6 @@ namespace {
 
 constexpr int THREADS = 256;
 constexpr int BN = 64, KS = 32;   // output channels per tile, k-step (bf16 elements)
-constexpr int ROWB = KS * 2;               // 64 B per LDS operand row
 
 // 16-B slot swizzle of a 64-B LDS row: conflict-free ds_read_b128 fragment reads (rows 4 apart
 // land on different slots of a 256-B bank row)
@@ -684,6 +683,246 @@ __global__ __launch_bounds__(256) void conv3d_weight_t_kernel(const bf16_t *__re
   Wt[i] = W[((int64_t)co * taps + t) * Cin + ci];
 }
 
+// ---- submanifold sparse convolution on occupied voxels (the north star's hash-indexed gather,
+// BASELINE configs[2]): the rows are the occupied voxels, the input row of (row m, tap t) comes
+// from the neighbour map nbr[m][t] (-1: an empty site, zeros) built by pcs_sparse_neighbors.  The
+// same gather GEMM as conv3d_kernel; a tile runs only the taps some of its rows have a neighbour
+// at (a bit mask collected in LDS first), which is where the sparsity saves MFMA work.
+//   Y[m] = b + sum_t W[tw(t)] X[nbr[m][t]],  tw(t) = flip ? taps - 1 - t : t
+// With flip and W^T (pcs_conv3d_weight_t) this is the input gradient: offset(taps-1-t) =
+// -offset(t) for the centred 3x3x3 taps, so dX[n] = sum_t W_t^T dY[nbr[n][taps-1-t]].
+template <int BMT, int KST, bool OUT_BF16>
+__global__ __launch_bounds__(THREADS) void sparse_conv_kernel(const int32_t *__restrict__ nbr, int64_t M, int taps,
+                                                              const bf16_t *__restrict__ X, int Cin,
+                                                              const bf16_t *__restrict__ W, int Cout,
+                                                              const float *__restrict__ bias, void *__restrict__ Y,
+                                                              int flip) {
+  constexpr int RB = KST * 2;
+  constexpr int CPR = KST / 8;
+  constexpr int RPP = THREADS / CPR;
+  constexpr int HA = BMT / RPP, HB = BN / RPP;
+  constexpr int TI = BMT / 32;
+  constexpr int KK = KST / 32;
+  __shared__ __attribute__((aligned(16))) char lds[2][(BMT + BN) * RB];
+  __shared__ uint32_t tmask;
+  __shared__ int tlist[32];
+  __shared__ int ntl;
+  auto swzf = [](int row, int slot) { return KST == 32 ? cswz(row, slot) : (slot ^ ((row >> 1) & 7)); };
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * BMT;
+  const int n0 = blockIdx.y * BN;
+  const int srow = tid / CPR, q = tid % CPR;
+
+  // the taps this tile meets
+  if (tid == 0) tmask = 0u;
+  __syncthreads();
+  uint32_t mym = 0u;
+  for (int i = tid; i < BMT * taps; i += THREADS) {
+    const int r = i / taps, t = i - r * taps;
+    if (m0 + r < M && nbr[(m0 + r) * taps + t] >= 0) mym |= 1u << t;
+  }
+  if (mym) atomicOr(&tmask, mym);
+  __syncthreads();
+  if (tid == 0) {
+    int c = 0;
+    const uint32_t m = tmask;
+    for (int t = 0; t < taps; ++t)
+      if ((m >> t) & 1u) tlist[c++] = t;
+    ntl = c;
+  }
+  __syncthreads();
+  const int cps = Cin / KST;
+  const int nks = ntl * cps;
+  const bf16_t *wrow = W + (int64_t)(n0 + srow) * taps * Cin + q * 8;
+  const int64_t wstep = (int64_t)RPP * taps * Cin;
+
+  u32x4 ra[HA], rb[HB];
+  auto load = [&](int ks) {
+    const int j = ks / cps, c0 = (ks - j * cps) * KST;
+    const int t = tlist[j], tw = flip ? taps - 1 - t : t;
+#pragma unroll
+    for (int h = 0; h < HA; ++h) {
+      const int64_t u = m0 + srow + RPP * h;
+      const int iv = u < M ? nbr[u * taps + t] : -1;
+      ra[h] = iv >= 0 ? *reinterpret_cast<const u32x4 *>(X + (int64_t)iv * Cin + c0 + q * 8) : mk_u32x4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) rb[h] = *reinterpret_cast<const u32x4 *>(wrow + h * wstep + (int64_t)tw * Cin + c0);
+  };
+  auto stage = [&](int buf) {
+    char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
+#pragma unroll
+    for (int h = 0; h < HA; ++h) {
+      const int r = srow + RPP * h;
+      *reinterpret_cast<u32x4 *>(tA + r * RB + swzf(r, q) * 16) = ra[h];
+    }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) {
+      const int r = srow + RPP * h;
+      *reinterpret_cast<u32x4 *>(tB + r * RB + swzf(r, q) * 16) = rb[h];
+    }
+  };
+
+  f32x4 acc[TI][2];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nks > 0) {
+    load(0);
+    stage(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nks) load(ks + 1);
+    const char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 af[TI], bw[2];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wr * (BMT / 2) + i * 16 + lr;
+        af[i] = *reinterpret_cast<const bf16x8 *>(tA + r * RB + swzf(r, kk * 4 + lg) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 32 + j * 16 + lr;
+        bw[j] = *reinterpret_cast<const bf16x8 *>(tB + r * RB + swzf(r, kk * 4 + lg) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (ks + 1 < nks) stage(buf ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int64_t uo = m0 + wr * (BMT / 2) + i * 16 + lr;
+    if (uo >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = n0 + wc * 32 + j * 16 + 4 * lg;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        const float4 bb = *reinterpret_cast<const float4 *>(bias + co);
+        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      }
+      if constexpr (OUT_BF16) {
+        *reinterpret_cast<uint2 *>(reinterpret_cast<bf16_t *>(Y) + uo * Cout + co) =
+            make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      } else {
+        *reinterpret_cast<float4 *>(reinterpret_cast<float *>(Y) + uo * Cout + co) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+// weight gradient of the sparse convolution: dW[co][t][ci] = sum_m dY[m][co] X[nbr[m][t]][ci];
+// a workgroup owns a (64 co x 64 ci) tile, TG consecutive taps and a slice of rows (the
+// structure of conv3d_wgrad_kernel with the neighbour map as the index), partials per slice
+__global__ __launch_bounds__(THREADS) void sparse_wgrad_kernel(const int32_t *__restrict__ nbr, int64_t M, int taps,
+                                                               const bf16_t *__restrict__ X, int Cin,
+                                                               const bf16_t *__restrict__ dY, int Cout,
+                                                               float *__restrict__ ws, int64_t vps) {
+  __shared__ __attribute__((aligned(16))) char lds[2][(1 + TG) * WIMG];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int nco = Cout / 64;
+  const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
+  const int t0 = blockIdx.y * TG, ntg = min(TG, taps - t0);
+  const int64_t lo = (int64_t)blockIdx.z * vps, hi = pcs_min64(lo + vps, M);
+  const int sv = tid >> 3, q8 = tid & 7;
+
+  f32x4 acc[TG][2][2];
+#pragma unroll
+  for (int a = 0; a < TG; ++a)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 rd, rx[TG];
+  auto load = [&](int64_t v0) {
+    const int64_t u = v0 + sv;
+    rd = mk_u32x4(0, 0, 0, 0);
+#pragma unroll
+    for (int a = 0; a < TG; ++a) rx[a] = mk_u32x4(0, 0, 0, 0);
+    if (u < hi) {
+      rd = *reinterpret_cast<const u32x4 *>(dY + u * Cout + co0 + q8 * 8);
+#pragma unroll
+      for (int a = 0; a < TG; ++a) {
+        if (a < ntg) {
+          const int iv = nbr[u * taps + t0 + a];
+          if (iv >= 0) rx[a] = *reinterpret_cast<const u32x4 *>(X + (int64_t)iv * Cin + ci0 + q8 * 8);
+        }
+      }
+    }
+  };
+  auto stage = [&](int buf) {
+    *reinterpret_cast<u32x4 *>(lds[buf] + woff(sv, q8 * 16)) = rd;
+#pragma unroll
+    for (int a = 0; a < TG; ++a)
+      if (a < ntg) *reinterpret_cast<u32x4 *>(lds[buf] + (1 + a) * WIMG + woff(sv, q8 * 16)) = rx[a];
+  };
+  const int nks = (int)((hi - lo + WV - 1) / WV);
+  if (nks > 0) {
+    load(lo);
+    stage(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nks) load(lo + (int64_t)(ks + 1) * WV);
+    bf16x8 fd[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fd[i] = wfrag(lds[buf], wr * 32 + i * 16, lane);
+#pragma unroll
+    for (int a = 0; a < TG; ++a) {
+      if (a < ntg) {
+        bf16x8 fx[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fx[j] = wfrag(lds[buf] + (1 + a) * WIMG, wc * 32 + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[a][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[a][i][j], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < nks) stage(buf ^ 1);
+    __syncthreads();
+  }
+  float *out = ws + (int64_t)blockIdx.z * Cout * taps * Cin;
+#pragma unroll
+  for (int a = 0; a < TG; ++a) {
+    if (a >= ntg) continue;
+    const int t = t0 + a;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + wc * 32 + j * 16 + lr;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+          out[((int64_t)co * taps + t) * Cin + ci] = acc[a][i][j][v];
+        }
+      }
+  }
+}
+
+int64_t sparse_wgrad_splits(int64_t M, int taps, int Cin, int Cout) {
+  const int64_t tiles = (int64_t)(Cout / 64) * (Cin / 64) * ((taps + TG - 1) / TG);
+  int64_t sp = (2048 + tiles - 1) / tiles;
+  const int64_t maxsp = (M + 4 * WV - 1) / (4 * WV);
+  if (sp > maxsp) sp = maxsp;
+  return sp < 1 ? 1 : sp;
+}
+
 bool geom_ok(const pcs_conv3d_geom *g, const char **why) {
   if (!g) { *why = "null geometry"; return false; }
   if (g->B <= 0 || g->Di <= 0 || g->Hi <= 0 || g->Wi <= 0 || g->Do <= 0 || g->Ho <= 0 || g->Wo <= 0) {
@@ -837,5 +1076,77 @@ extern "C" int pcs_conv3d_weight_t(const void *W, int32_t Cout, int32_t taps, in
                      reinterpret_cast<hipStream_t>(stream), static_cast<const bf16_t *>(W), Cout, taps, Cin,
                      static_cast<bf16_t *>(Wt));
   PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- submanifold sparse convolution (hash-indexed gather; see sparse_conv_kernel)
+extern "C" int pcs_sparse_conv(const int32_t *nbr, int64_t M, int32_t taps, const void *X, int32_t Cin, const void *W,
+                               int32_t Cout, const float *bias, void *Y, int32_t ydtype, int32_t flip,
+                               pcs_stream_t stream) {
+  if (!nbr || !X || !W || !Y || M < 0 || taps < 1 || taps > 27 || Cin <= 0 || Cout <= 0 || Cin % KS != 0 ||
+      Cout % BN != 0 || (ydtype != PCS_F32 && ydtype != PCS_BF16))
+    return pcs_set_einval("pcs_sparse_conv", "bad arguments (1 <= taps <= 27, Cin % 32 == 0, Cout % 64 == 0, Y f32 | bf16)");
+  if (M == 0) return 0;
+  const int64_t tiles = (M + 63) / 64;
+  if (tiles > 0x7fffffff) return pcs_set_einval("pcs_sparse_conv", "too many rows");
+  const dim3 grid((unsigned)tiles, (unsigned)(Cout / BN));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bf16_t *Xb = static_cast<const bf16_t *>(X), *Wb = static_cast<const bf16_t *>(W);
+#define PCS_SC(KST, OB) \
+  hipLaunchKernelGGL((sparse_conv_kernel<64, KST, OB>), grid, dim3(THREADS), 0, s, nbr, M, (int)taps, Xb, (int)Cin, Wb, \
+                     (int)Cout, bias, Y, (int)flip)
+  if (Cin % 64 == 0) {
+    if (ydtype == PCS_BF16) PCS_SC(64, true); else PCS_SC(64, false);
+  } else {
+    if (ydtype == PCS_BF16) PCS_SC(32, true); else PCS_SC(32, false);
+  }
+#undef PCS_SC
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t pcs_sparse_conv_wgrad_workspace(int64_t M, int32_t taps, int32_t Cin, int32_t Cout) {
+  if (M < 0 || taps < 1 || taps > 27 || Cin <= 0 || Cout <= 0 || Cin % 64 != 0 || Cout % 64 != 0)
+    return pcs_set_einval("pcs_sparse_conv_wgrad_workspace", "bad arguments (Cin, Cout multiples of 64)");
+  const int64_t sp = sparse_wgrad_splits(M, taps, Cin, Cout);
+  return sp * ((int64_t)Cout * taps * Cin + Cout) * 4;
+}
+
+extern "C" int pcs_sparse_conv_wgrad(const int32_t *nbr, int64_t M, int32_t taps, const void *X, int32_t Cin,
+                                     const void *dY, int32_t Cout, void *workspace, int64_t workspace_bytes, float *dW,
+                                     float *db, pcs_stream_t stream) {
+  const int64_t need = pcs_sparse_conv_wgrad_workspace(M, taps, Cin, Cout);
+  if (need < 0) return (int)need;
+  if (!nbr || !X || !dY || !dW || !workspace || workspace_bytes < need)
+    return pcs_set_einval("pcs_sparse_conv_wgrad", "nbr, X, dY, dW and a workspace of pcs_sparse_conv_wgrad_workspace bytes");
+  const int64_t sp = sparse_wgrad_splits(M, taps, Cin, Cout);
+  const int64_t vps = ((M + sp - 1) / sp + WV - 1) / WV * WV;
+  const int64_t wlen = (int64_t)Cout * taps * Cin;
+  float *ws = static_cast<float *>(workspace), *wsb = ws + sp * wlen;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (M > 0) {
+    hipLaunchKernelGGL(sparse_wgrad_kernel, dim3((unsigned)((Cout / 64) * (Cin / 64)), (unsigned)((taps + TG - 1) / TG), (unsigned)sp),
+                       dim3(THREADS), 0, s, nbr, M, (int)taps, static_cast<const bf16_t *>(X), (int)Cin,
+                       static_cast<const bf16_t *>(dY), (int)Cout, ws, vps);
+  } else {
+    const hipError_t e = hipMemsetAsync(ws, 0, sp * wlen * 4, s);
+    if (e != hipSuccess) return pcs_set_error(e, "pcs_sparse_conv_wgrad");
+  }
+  PCS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((wlen + 255) / 256)), dim3(256), 0, s, ws, sp, wlen, dW);
+  PCS_CHECK_LAUNCH();
+  if (db) {
+    if (M > 0) {
+      hipLaunchKernelGGL(conv3d_bgrad_kernel, dim3((unsigned)(Cout / 64), (unsigned)sp), dim3(THREADS), 0, s,
+                         static_cast<const bf16_t *>(dY), (int)Cout, M, vps, wsb);
+    } else {
+      const hipError_t e = hipMemsetAsync(wsb, 0, sp * Cout * 4, s);
+      if (e != hipSuccess) return pcs_set_error(e, "pcs_sparse_conv_wgrad");
+    }
+    PCS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, wsb, sp,
+                       (int64_t)Cout, db);
+    PCS_CHECK_LAUNCH();
+  }
   return 0;
 }
