@@ -46,7 +46,8 @@ template <int COUT> struct SegCfg {
   static constexpr int XB = MS * XR;                        // one x buffer
   static constexpr int OFF_X = NST * STAGE;                 // x [2][MS][XR]
   static constexpr int OFF_CF = OFF_X + 2 * XB;             // alpha | beta | gamma [COUT], es | et [CB]
-  static constexpr int BYTES = OFF_CF + (3 * COUT + 2 * CB) * 4;
+  static constexpr int OFF_LUT = OFF_CF + (3 * COUT + 2 * CB) * 4;   // dropout-bit masks, [256][4] u32
+  static constexpr int BYTES = OFF_LUT + 256 * 16;
   static_assert(BYTES <= 160 * 1024, "LDS budget");
   static constexpr int KS = COUT / 32;                      // dgrad k-steps (32 deep)
   static constexpr int OBW = COUT / 128;                    // wgrad 16-row output tiles per wave
@@ -237,10 +238,17 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       cf[COUT + j] = a.pb[i];
       cf[2 * COUT + j] = a.pc[i];
     }
-    if (tid < CB) {
+    if (tid < CB) {   // x = relu(es y + et) ks = relu((es ks) y + et ks): the keep scale folded in (ks > 0)
       const int j = split_idx(tid, CB);
-      cf[3 * COUT + j] = a.es[n0 + tid];
-      cf[3 * COUT + CB + j] = a.et[n0 + tid];
+      cf[3 * COUT + j] = a.es[n0 + tid] * ks;
+      cf[3 * COUT + CB + j] = a.et[n0 + tid] * ks;
+    }
+    // dropout byte -> the AND masks of 8 packed bf16 values (dword d: bits 2d, 2d+1 as halves)
+    if (tid < 256) {
+      uint32_t *lut = reinterpret_cast<uint32_t *>(lds + F::OFF_LUT) + tid * 4;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        lut[d] = (((tid >> (2 * d)) & 1) ? 0x0000FFFFu : 0u) | (((tid >> (2 * d + 1)) & 1) ? 0xFFFF0000u : 0u);
     }
   }
   const int dlc = tid % F::SPR, drr = tid / F::SPR;   // dy: physical slot, first row
@@ -310,9 +318,9 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
     unpack_chunk(yy, y);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
-    const u32x4 out = pack_chunk(v);
-    *reinterpret_cast<u32x4 *>(st + o_tr + i * THREADS * 16) =
-        drr + i * (THREADS / F::SPR) < rem ? out : mk_u32x4(0, 0, 0, 0);
+    u32x4 out = pack_chunk(v);
+    if (rem < MS && drr + i * (THREADS / F::SPR) >= rem) out = mk_u32x4(0, 0, 0, 0);   // (uniform test first)
+    *reinterpret_cast<u32x4 *>(st + o_tr + i * THREADS * 16) = out;
   };
   auto transform_x = [&](int s, int sidx) {
     const char *st = lds + sidx * F::STAGE;
@@ -321,14 +329,15 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
     lds_vec8(cfx, CB * 2, xs);
     lds_vec8(cfx + CB * 4, CB * 2, xt);
     unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o_ypx), v);
-    const uint32_t mb = MASK ? (uint32_t)(uint8_t)st[o_mkx] : 0xffu;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float x = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
-      v[e] = ((mb >> e) & 1u) ? x * ks : 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+    u32x4 out = pack_chunk(v);
+    if constexpr (MASK) {   // dropout: AND with the byte's masks (one LDS read for 8 values)
+      const u32x4 m = *reinterpret_cast<const u32x4 *>(lds + F::OFF_LUT + (uint32_t)(uint8_t)st[o_mkx] * 16);
+      out = mk_u32x4(out[0] & m[0], out[1] & m[1], out[2] & m[2], out[3] & m[3]);
     }
-    const u32x4 out = pack_chunk(v);
-    *reinterpret_cast<u32x4 *>(lds + F::OFF_X + (s & 1) * F::XB + o_xw) = xrr < rem ? out : mk_u32x4(0, 0, 0, 0);
+    if (rem < MS && xrr >= rem) out = mk_u32x4(0, 0, 0, 0);
+    *reinterpret_cast<u32x4 *>(lds + F::OFF_X + (s & 1) * F::XB + o_xw) = out;
   };
 
   // ---- output rows through one buffer descriptor for the slice (range: its rows): a store's
