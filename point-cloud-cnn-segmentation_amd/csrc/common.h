@@ -175,6 +175,10 @@ int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_
 bool pcs_seg_bwd_applicable(const pcs_gemm_args &a);
 int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a);
 int pcs_seg_bwd_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);
+// conv5's folded input gradient as one LDS-DMA stream (fused_c5.hip)
+bool pcs_c5_dgrad_class(const pcs_gemm_args &a);
+bool pcs_c5_dgrad_applicable(const pcs_gemm_args &a);
+int pcs_c5_dgrad_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
 // wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)
 bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a);
 int pcs_wgrad_big_splits(const pcs_wgrad_args &a);

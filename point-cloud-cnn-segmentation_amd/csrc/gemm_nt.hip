@@ -597,6 +597,8 @@ extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
     return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
   if (wide_class(*a))
     return pcs_fill_geometry(a, PCS_BIG_BM, 256, a->Ncols / 256);   // one 512-thread WG per CU
+  if (pcs_c5_dgrad_class(*a))   // conv5's folded input gradient: one 512-thread WG per CU
+    return pcs_fill_geometry(a, GEMM_BM, 256, 1);
   const int64_t ncb = a->Ncols >= 128 ? a->Ncols / 128 : 1;
   return pcs_fill_geometry(a, GEMM_BM, 2048, ncb);                 // ~8 WGs per CU
 }
@@ -663,6 +665,7 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_big_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
   }
+  if (pcs_c5_dgrad_applicable(a)) return pcs_c5_dgrad_launch(a, rpc, s);
   const int tps = (int)((a.scene_rows + GEMM_BM - 1) / GEMM_BM);
   const int tpc = (int)(rpc / GEMM_BM);
   const bool bn128 = a.Ncols % 128 == 0;
