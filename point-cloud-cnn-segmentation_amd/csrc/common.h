@@ -179,6 +179,11 @@ int pcs_seg_bwd_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);
 bool pcs_c5_dgrad_class(const pcs_gemm_args &a);
 bool pcs_c5_dgrad_applicable(const pcs_gemm_args &a);
 int pcs_c5_dgrad_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
+// streaming forward of the narrow-K BN+ReLU layers (fwd_stream.hip): output columns per
+// workgroup (0 = not this kernel's class; shapes only, the chunk geometry), applicability, launch
+int pcs_fwd_stream_nb(const pcs_gemm_args &a);
+bool pcs_fwd_stream_applicable(const pcs_gemm_args &a);
+int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
 // wide-layer bf16 weight-gradient kernel (gemm_big_tn.hip)
 bool pcs_wgrad_big_applicable(const pcs_wgrad_args &a);
 int pcs_wgrad_big_splits(const pcs_wgrad_args &a);

@@ -595,6 +595,8 @@ static bool wide_class(const pcs_gemm_args &a) {
 extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Ncols <= 0)
     return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
+  if (const int nbc = pcs_fwd_stream_nb(*a))   // streaming forward: one 512-thread WG per CU
+    return pcs_fill_geometry(a, 256, 256, a->Ncols / nbc);
   if (wide_class(*a))
     return pcs_fill_geometry(a, PCS_BIG_BM, 256, a->Ncols / 256);   // one 512-thread WG per CU
   if (pcs_c5_dgrad_class(*a))   // conv5's folded input gradient: one 512-thread WG per CU
@@ -657,6 +659,7 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (wide_class(a) && pcs_gemm_wres_applicable(a)) return pcs_gemm_wres_launch(a, rpc, s);
+  if (pcs_fwd_stream_applicable(a)) return pcs_fwd_stream_launch(a, rpc, s);
   if (wide_class(a) && pcs_gemm_glds_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_glds_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
