@@ -81,11 +81,23 @@ template <> struct FsCfg<128, 1024> {  // conv5 (BN5 + ReLU on the way out: a5)
   static constexpr int NB = 512, WCN = 8, MS = 64, NST = 4;
 };
 
+#ifndef FS_STG
+#define FS_STG 1
+#endif
+#ifndef FS_CPOL
+#define FS_CPOL 2   // cache policy bits of the staged (STG) output stores: 2 = nt
+#endif
+
 template <int K, int NCOLS, bool MASK> struct FsGeo {
   typedef FsCfg<K, NCOLS> C;
   static constexpr int NB = C::NB, WCN = C::WCN, MS = C::MS, NST = C::NST;
   static constexpr int WRN = 8 / WCN;          // wave rows
   static constexpr int WC = NB / WCN;          // columns per wave
+  // 128-B wave rows (WC = 64): the output goes through a per-wave LDS tile and leaves as 8 rows x
+  // 128 B per store instruction (16 rows x 64 B straight from the MFMA layout otherwise)
+  // FS_STG 2: the whole step's [MS][NB] tile is staged and each store instruction writes one
+  // NB * 2 = 1 KB row, after the step's first barrier (all waves' parts of the tile written)
+  static constexpr int STG = (FS_STG && WC == 64) ? ((FS_STG == 2 && NB == 512 && WRN == 1) ? 2 : 1) : 0;
   static constexpr int CT = WC / 16;           // 16-column MFMA tiles per wave
   static constexpr int RW = MS / WRN;          // rows per wave per step
   static constexpr int RT = RW / 16;           // 16-row MFMA tiles per wave
@@ -99,9 +111,13 @@ template <int K, int NCOLS, bool MASK> struct FsGeo {
   static constexpr int MPW = MKB / 256 / 8;    // 256-B (dword) DMA pieces per wave per step
   static constexpr int OFF_LUT = NST * STAGE;  // dropout byte -> 4 AND masks of packed bf16
   static constexpr int OFF_RED = OFF_LUT + (MASK ? 256 * 16 : 0);   // chunk-end merge [WRN][NB] float4
-  static constexpr int BYTES = OFF_RED + WRN * NB * 16;
+  static constexpr int OFF_STG = OFF_RED + WRN * NB * 16;             // [8 waves][RW][WC] bf16 (STG)
+  static constexpr int BYTES = OFF_STG + (STG ? 8 * RW * WC * 2 : 0);   // (STG 2: MS * NB * 2, the same)
   static constexpr int LPS = PPW + MPW;        // vector-memory loads per wave per step
-  static constexpr int SPS = (CT / 2) * RT;    // stores per wave per step
+  static constexpr int SPS = STG == 2 ? MS / 8 : STG ? RW / 8 : (CT / 2) * RT;   // stores per wave per step
+  // vector-memory operations newer than step t+1's DMA at the loop's wait (STG 2 stores step t
+  // only after it)
+  static constexpr int WAIT_N = (NST - 2) * (LPS + SPS) + (STG == 2 ? 0 : SPS);
   static constexpr int TPASS = MS * SPR / THREADS;   // transform passes (slots per thread)
   static_assert(NCOLS % NB == 0 && NB % WCN == 0 && WC % 32 == 0, "column tiling (CT even)");
   static_assert(MS % (16 * WRN) == 0 && XB % 8192 == 0 && PPW >= 1, "row tiling / DMA pieces");
@@ -285,7 +301,15 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
   const int rbase = wr * F::RW;   // this wave's first row of a step
   // lane (l16, g) after the swaps: row l16 of a row tile, columns 16 (2 q + (g & 1)) + 8 (g >> 1)
   const uint32_t o_st = (uint32_t)((rbase + l16) * (NCOLS * 2) + (wc * F::WC + 16 * (g & 1) + 8 * (g >> 1)) * 2);
-  auto store16 = [&](uint32_t vo, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, rs_out, (int)vo, 0, 0); };
+  // (nt measured faster for the staged 128-B row stores -- conv5 3.74 -> 3.65 ms, seg_conv1 2.02 ->
+  // 1.98 -- and slower for the 16 x 64 B ones of seg_conv2 / seg_conv3, 3.06 -> 3.12 ms)
+  auto store16 = [&](uint32_t vo, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs_out, (int)vo, 0, F::STG ? FS_CPOL : 0);
+  };
+  // STG 1: lane = row rbase + lane / 8 (+ 8 i), columns wc WC + 8 (lane % 8) .. + 8;
+  // STG 2: lane = row wid (+ 8 i), columns 64 (lane / 8) + 8 (lane % 8) .. + 8
+  uint32_t o_stg = F::STG == 2 ? (uint32_t)(wid * (NCOLS * 2) + (64 * (lane >> 3) + 8 * (lane & 7)) * 2)
+                               : (uint32_t)((rbase + (lane >> 3)) * (NCOLS * 2) + (wc * F::WC + 8 * (lane & 7)) * 2);
 
   // B-fragment LDS offsets: row rbase + 16 rt + l16 (f(row) = f(l16) for both swizzles, as
   // rbase + 16 rt is a multiple of 16), logical slot 4 kk + g
@@ -377,6 +401,16 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
         }
       }
       nrow += live ? 1.f : 0.f;
+      if constexpr (F::STG) {
+        // 8-B granule 4 ct + g of the wave's row 16 rt + l16, at granule (4 ct + g) ^ (row & 15):
+        // the 16 rows a lane group writes at one granule hit 16 distinct granules of the bank row
+        char *sw = F::STG == 2 ? lds + F::OFF_STG + (16 * rt + l16) * (NB * 2) + wc * 128
+                               : lds + F::OFF_STG + wid * (F::RW * 128) + (16 * rt + l16) * 128;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          *reinterpret_cast<uint2 *>(sw + (((4 * ct + g) ^ l16) << 3)) = make_uint2(pk[ct][0], pk[ct][1]);
+        continue;
+      }
 #pragma unroll
       for (int q = 0; q < CT / 2; ++q) {
 #pragma unroll
@@ -389,11 +423,38 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
                                                                          pk[2 * q + 1][1]));
       }
     }
+    if constexpr (F::STG == 1) {
+      // rows back from the wave's tile: lane = row 8 i + lane / 8, 16-B chunk lane % 8 (logical
+      // granules 2c, 2c+1 share physical chunk c ^ ((row >> 1) & 7), swapped on odd rows)
+      const int c = lane & 7;
+#pragma unroll
+      for (int i = 0; i < F::RW / 8; ++i) {
+        const int row = 8 * i + (lane >> 3);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + F::OFF_STG + wid * (F::RW * 128) + row * 128 +
+                                                         ((c ^ ((row >> 1) & 7)) << 4));
+        const u32x4 w = (row & 1) ? mk_u32x4(v[2], v[3], v[0], v[1]) : v;
+        store16(o_stg + (uint32_t)(i * 8 * NCOLS * 2), w);
+      }
+      o_stg += MS * NCOLS * 2;
+    }
     o_out += MS * NCOLS * 2;
-    // step t+1 landed: newer are this step's stores after its own group, and NST-2 (DMA,
-    // stores) groups
-    wait_vm<F::SPS + (NST - 2) * (F::LPS + F::SPS)>();
+    // step t+1 landed: newer are NST-2 (DMA, stores) groups and (unless STG 2) this step's stores
+    wait_vm<F::WAIT_N>();
     barrier_lds();
+    if constexpr (F::STG == 2) {
+      // whole rows of the step's tile: wave w stores rows w + 8 i, lane = 16-B chunk lane % 8 of
+      // the 128-B column block lane / 8 (granule swizzle as written, halves swapped on odd rows)
+      const int c = lane & 7, b = lane >> 3;
+#pragma unroll
+      for (int i = 0; i < MS / 8; ++i) {
+        const int row = wid + 8 * i;
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + F::OFF_STG + row * (NB * 2) + b * 128 +
+                                                         ((c ^ ((row >> 1) & 7)) << 4));
+        const u32x4 w = (row & 1) ? mk_u32x4(v[2], v[3], v[0], v[1]) : v;
+        store16(o_stg + (uint32_t)(i * 8 * NCOLS * 2), w);
+      }
+      o_stg += MS * NCOLS * 2;
+    }
     if (t + 1 < nsteps) transform(sc + 1 == NST ? 0 : sc + 1);
     barrier_lds();
     sc = sc + 1 == NST ? 0 : sc + 1;
