@@ -88,7 +88,7 @@ template <> struct FsCfg<128, 1024> {  // conv5 (BN5 + ReLU on the way out: a5)
 #define FS_CPOL 2   // cache policy bits of the staged (STG) output stores: 2 = nt
 #endif
 
-template <int K, int NCOLS, bool MASK> struct FsGeo {
+template <int K, int NCOLS, bool MASK, bool C8 = false> struct FsGeo {
   typedef FsCfg<K, NCOLS> C;
   static constexpr int NB = C::NB, WCN = C::WCN, MS = C::MS, NST = C::NST;
   static constexpr int WRN = 8 / WCN;          // wave rows
@@ -97,7 +97,10 @@ template <int K, int NCOLS, bool MASK> struct FsGeo {
   // 128 B per store instruction (16 rows x 64 B straight from the MFMA layout otherwise)
   // FS_STG 2: the whole step's [MS][NB] tile is staged and each store instruction writes one
   // NB * 2 = 1 KB row, after the step's first barrier (all waves' parts of the tile written)
-  static constexpr int STG = (FS_STG && WC == 64) ? ((FS_STG == 2 && NB == 512 && WRN == 1) ? 2 : 1) : 0;
+  // C8 (the fp8 e4m3 a5 of cfg5): 64-B wave rows, staged, 16 rows x 64 B per store
+  static constexpr int STG = C8 ? 1 : (FS_STG && WC == 64) ? ((FS_STG == 2 && NB == 512 && WRN == 1) ? 2 : 1) : 0;
+  static constexpr int ESZ = C8 ? 1 : 2;                  // output element bytes
+  static constexpr int SROW = WC * ESZ;                   // staged wave-row bytes (128 or 64)
   static constexpr int CT = WC / 16;           // 16-column MFMA tiles per wave
   static constexpr int RW = MS / WRN;          // rows per wave per step
   static constexpr int RT = RW / 16;           // 16-row MFMA tiles per wave
@@ -112,9 +115,9 @@ template <int K, int NCOLS, bool MASK> struct FsGeo {
   static constexpr int OFF_LUT = NST * STAGE;  // dropout byte -> 4 AND masks of packed bf16
   static constexpr int OFF_RED = OFF_LUT + (MASK ? 256 * 16 : 0);   // chunk-end merge [WRN][NB] float4
   static constexpr int OFF_STG = OFF_RED + WRN * NB * 16;             // [8 waves][RW][WC] bf16 (STG)
-  static constexpr int BYTES = OFF_STG + (STG ? 8 * RW * WC * 2 : 0);   // (STG 2: MS * NB * 2, the same)
+  static constexpr int BYTES = OFF_STG + (STG ? 8 * RW * SROW : 0);   // (STG 2: MS * NB * 2, the same)
   static constexpr int LPS = PPW + MPW;        // vector-memory loads per wave per step
-  static constexpr int SPS = STG == 2 ? MS / 8 : STG ? RW / 8 : (CT / 2) * RT;   // stores per wave per step
+  static constexpr int SPS = STG == 2 ? MS / 8 : STG ? RW * SROW / 1024 : (CT / 2) * RT;   // stores per wave per step
   // vector-memory operations newer than step t+1's DMA at the loop's wait (STG 2 stores step t
   // only after it)
   static constexpr int WAIT_N = (NST - 2) * (LPS + SPS) + (STG == 2 ? 0 : SPS);
@@ -124,15 +127,17 @@ template <int K, int NCOLS, bool MASK> struct FsGeo {
   static_assert(!MASK || (MKB % 2048 == 0 && MPW >= 1), "dropout-bit pieces");
   static_assert(K % 32 == 0 && ROWB <= 1024 && (MS * SPR) % THREADS == 0, "K");
   static_assert(BYTES <= 160 * 1024, "LDS budget");
+  static_assert(!C8 || (WC == 64 && RW % 16 == 0), "fp8 output staging");
 };
 
 // physical 16-B slot of logical slot c in LDS row r: c ^ f(r), f distinct over the 16 rows a
 // ds_read_b128 lane group touches at one logical slot (128-B rows hold two rows per bank row)
 template <int K> PCS_DEV int fsw(int r) { return K == 64 ? ((r >> 1) & 7) : (r & 15); }
 
-template <int K, int NCOLS, int EPI, bool MASK, bool SBIAS>
+template <int K, int NCOLS, int EPI, bool MASK, bool SBIAS, bool C8 = false>
 __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, int64_t rows_per_chunk) {
-  typedef FsGeo<K, NCOLS, MASK> F;
+  typedef FsGeo<K, NCOLS, MASK, C8> F;
+  static_assert(!C8 || EPI == PCS_EPI_BNRELU, "fp8 output: the BN+ReLU epilogue (a5)");
   constexpr int NB = F::NB, MS = F::MS, NST = F::NST, CT = F::CT, RT = F::RT, KS = F::KS;
   constexpr int ROWB = F::ROWB, SPR = F::SPR;
   constexpr int NCB = NCOLS / NB;
@@ -295,9 +300,10 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
   // ---- output through one buffer descriptor for the slice's rows (columns n0 .. of the block):
   // rows past the slice fall outside its range and are dropped by the hardware, so every wave
   // issues the same stores each step; the prologue's placeholder stores lie wholly out of range
+  constexpr int ESZ = F::ESZ;
   const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<char *>(reinterpret_cast<bf16_t *>(a.C) + (sbase + lo) * NCOLS + n0), 0,
-      (int)(uint32_t)((hi - lo - 1) * NCOLS * 2 + NB * 2), 0x00020000);
+      reinterpret_cast<char *>(a.C) + ((sbase + lo) * NCOLS + n0) * ESZ, 0,
+      (int)(uint32_t)((hi - lo - 1) * NCOLS * ESZ + NB * ESZ), 0x00020000);
   const int rbase = wr * F::RW;   // this wave's first row of a step
   // lane (l16, g) after the swaps: row l16 of a row tile, columns 16 (2 q + (g & 1)) + 8 (g >> 1)
   const uint32_t o_st = (uint32_t)((rbase + l16) * (NCOLS * 2) + (wc * F::WC + 16 * (g & 1) + 8 * (g >> 1)) * 2);
@@ -308,7 +314,9 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
   };
   // STG 1: lane = row rbase + lane / 8 (+ 8 i), columns wc WC + 8 (lane % 8) .. + 8;
   // STG 2: lane = row wid (+ 8 i), columns 64 (lane / 8) + 8 (lane % 8) .. + 8
-  uint32_t o_stg = F::STG == 2 ? (uint32_t)(wid * (NCOLS * 2) + (64 * (lane >> 3) + 8 * (lane & 7)) * 2)
+  // C8: lane = row rbase + lane / 4 (+ 16 i), columns wc WC + 16 (lane % 4) .. + 16
+  uint32_t o_stg = C8 ? (uint32_t)((rbase + (lane >> 2)) * NCOLS + wc * F::WC + 16 * (lane & 3))
+                 : F::STG == 2 ? (uint32_t)(wid * (NCOLS * 2) + (64 * (lane >> 3) + 8 * (lane & 7)) * 2)
                                : (uint32_t)((rbase + (lane >> 3)) * (NCOLS * 2) + (wc * F::WC + 8 * (lane & 7)) * 2);
 
   // B-fragment LDS offsets: row rbase + 16 rt + l16 (f(row) = f(l16) for both swizzles, as
@@ -380,10 +388,19 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
           if constexpr (EPI == PCS_EPI_BNRELU) v[r] = fmaxf(fmaf(acc[ct][rt][r], es[ct][r], eb[ct][r]), 0.f);
           else v[r] = acc[ct][rt][r] + eb[ct][r];
         }
-        pk[ct][0] = pack2bf(v[0], v[1]);
-        pk[ct][1] = pack2bf(v[2], v[3]);
-        const float d[4] = {bf2f(pk[ct][0] & 0xffffu), bf2f(pk[ct][0] >> 16), bf2f(pk[ct][1] & 0xffffu),
-                            bf2f(pk[ct][1] >> 16)};   // the stored values
+        float d[4];   // the stored values
+        if constexpr (C8) {
+          pk[ct][0] = pack4fp8(v[0], v[1], v[2], v[3]);
+          pk[ct][1] = 0u;
+          const f32x2 d0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)pk[ct][0], false);
+          const f32x2 d1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)pk[ct][0], true);
+          d[0] = d0[0]; d[1] = d0[1]; d[2] = d1[0]; d[3] = d1[1];
+        } else {
+          pk[ct][0] = pack2bf(v[0], v[1]);
+          pk[ct][1] = pack2bf(v[2], v[3]);
+          d[0] = bf2f(pk[ct][0] & 0xffffu); d[1] = bf2f(pk[ct][0] >> 16);
+          d[2] = bf2f(pk[ct][1] & 0xffffu); d[3] = bf2f(pk[ct][1] >> 16);
+        }
         if constexpr (EPI == PCS_EPI_BNRELU) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) s1[ct][r] += live ? d[r] : 0.f;
@@ -404,6 +421,12 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       if constexpr (F::STG) {
         // 8-B granule 4 ct + g of the wave's row 16 rt + l16, at granule (4 ct + g) ^ (row & 15):
         // the 16 rows a lane group writes at one granule hit 16 distinct granules of the bank row
+        if constexpr (C8) {   // 4-B granules of 64-B rows, the same (row & 15) permutation
+          char *sw = lds + F::OFF_STG + wid * (F::RW * 64) + (16 * rt + l16) * 64;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) *reinterpret_cast<uint32_t *>(sw + (((4 * ct + g) ^ l16) << 2)) = pk[ct][0];
+          continue;
+        }
         char *sw = F::STG == 2 ? lds + F::OFF_STG + (16 * rt + l16) * (NB * 2) + wc * 128
                                : lds + F::OFF_STG + wid * (F::RW * 128) + (16 * rt + l16) * 128;
 #pragma unroll
@@ -423,7 +446,27 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
                                                                          pk[2 * q + 1][1]));
       }
     }
-    if constexpr (F::STG == 1) {
+    if constexpr (C8) {
+      // rows back: lane = row 16 i + lane / 4, 16-B chunk c = lane % 4 (logical granules 4c .. 4c+3
+      // sit in physical chunk c ^ ((row >> 2) & 3), granule e at e ^ (row & 3))
+      const int c = lane & 3;
+#pragma unroll
+      for (int i = 0; i < F::RW / 16; ++i) {
+        const int row = 16 * i + (lane >> 2);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + F::OFF_STG + wid * (F::RW * 64) + row * 64 +
+                                                         ((c ^ ((row >> 2) & 3)) << 4));
+        const int x = row & 3;
+        u32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t a01 = (x & 1) ? v[e ^ 1] : v[e];
+          const uint32_t a23 = (x & 1) ? v[e ^ 3] : v[e ^ 2];
+          w[e] = (x & 2) ? a23 : a01;
+        }
+        store16(o_stg + (uint32_t)(i * 16 * NCOLS), w);
+      }
+      o_stg += MS * NCOLS;
+    } else if constexpr (F::STG == 1) {
       // rows back from the wave's tile: lane = row 8 i + lane / 8, 16-B chunk lane % 8 (logical
       // granules 2c, 2c+1 share physical chunk c ^ ((row >> 1) & 7), swapped on odd rows)
       const int c = lane & 7;
@@ -527,7 +570,8 @@ int pcs_fwd_stream_nb(const pcs_gemm_args &a) {
 }
 
 bool pcs_fwd_stream_applicable(const pcs_gemm_args &a) {
-  if (!pcs_fwd_stream_nb(a) || !a.C || !a.pa || !a.pb || a.pool || (a.flags & PCS_FLAG_C_FP8)) return false;
+  if (!pcs_fwd_stream_nb(a) || !a.C || !a.pa || !a.pb || a.pool) return false;
+  if ((a.flags & PCS_FLAG_C_FP8) && a.epilogue != PCS_EPI_BNRELU) return false;
   if (a.scene_rows * a.num_scenes >= ((int64_t)1 << 31)) return false;
   if (a.epilogue == PCS_EPI_BNRELU) return a.es && a.et && !a.a_mask && !a.scene_bias;
   // dropout bits only where the layer has them (seg_conv2 / seg_conv3 inputs)
@@ -543,7 +587,11 @@ int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStr
   hipLaunchKernelGGL((fwd_stream_kernel<K, NC, EPI, MK, SB>), dim3(nb), dim3(THREADS), 0, s, a, rows_per_chunk)
   const bool mk = a.a_mask != nullptr;
   if (a.epilogue == PCS_EPI_BNRELU) {
-    PCS_FS(128, 1024, PCS_EPI_BNRELU, false, false);
+    if (a.flags & PCS_FLAG_C_FP8)
+      hipLaunchKernelGGL((fwd_stream_kernel<128, 1024, PCS_EPI_BNRELU, false, false, true>), dim3(nb), dim3(THREADS), 0,
+                         s, a, rows_per_chunk);
+    else
+      PCS_FS(128, 1024, PCS_EPI_BNRELU, false, false);
   } else if (FsShape<64, 512>::is(a)) {
     if (a.scene_bias) PCS_FS(64, 512, PCS_EPI_FWD, false, true); else PCS_FS(64, 512, PCS_EPI_FWD, false, false);
   } else if (FsShape<512, 256>::is(a)) {

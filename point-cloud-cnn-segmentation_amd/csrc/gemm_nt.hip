@@ -658,8 +658,8 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (wide_class(a) && pcs_gemm_wres_applicable(a)) return pcs_gemm_wres_launch(a, rpc, s);
   if (pcs_fwd_stream_applicable(a)) return pcs_fwd_stream_launch(a, rpc, s);
+  if (wide_class(a) && pcs_gemm_wres_applicable(a)) return pcs_gemm_wres_launch(a, rpc, s);
   if (wide_class(a) && pcs_gemm_glds_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_glds_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);

@@ -121,3 +121,35 @@ def test_fwd_stream_agrees_with_generic_kernel(K, C, kind):
 def test_fwd_stream_seg_conv2_without_dropout():
     out, st, ref, counts = _run(2, 9000 + 7, 512, 256, "mask", 3, nomask=True)
     assert float((out - ref).abs().max() / ref.abs().max()) < 8e-3
+
+
+@pytest.mark.parametrize("B,N", [(2, 70000 + 5), (1, 31)])
+def test_fwd_stream_conv5_fp8_store(B, N):
+    """cfg5's a5 (PCS_FLAG_C_FP8): e4m3 bytes staged through LDS as 64-B wave rows; every stored
+    byte within one e4m3 rounding of the fp64 value, column sums equal to the stored bytes' sums."""
+    import pcs_amd._lib as L
+    K, C = 128, 1024
+    g = torch.Generator(device="cpu").manual_seed(17 + N)
+    M = B * N
+    yp = (torch.randn(M, K, generator=g) * 2.0).to(torch.bfloat16)
+    W = (torch.randn(C, K, generator=g) * 0.1).to(torch.bfloat16)
+    pa, pb = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.2
+    es, et = torch.randn(C, generator=g), torch.randn(C, generator=g) * 0.3
+    T = {k: t.to(DEV).contiguous() for k, t in dict(yp=yp, W=W, pa=pa, pb=pb, es=es, et=et).items()}
+    out = torch.empty(M, C, dtype=torch.uint8, device=DEV)
+    a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=C, dtype=L.BF16, prologue=L.PRO_BNRELU,
+                   epilogue=L.EPI_BNRELU, chunks_per_scene=0, A=T["yp"].data_ptr(), W=T["W"].data_ptr(),
+                   C=out.data_ptr(), a_keep_scale=1.0, c_keep_scale=1.0, flags=L.FLAG_C_FP8)
+    a.pa, a.pb, a.es, a.et = (T[k].data_ptr() for k in ("pa", "pb", "es", "et"))
+    L.load().pcs_gemm_geometry(ct.byref(a))
+    st = torch.empty(B * a.chunks_per_scene, C, 2, device=DEV)
+    a.stats = st.data_ptr()
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    torch.cuda.synchronize()
+    x = torch.relu(yp.double() * pa.double() + pb.double()).to(torch.bfloat16).double()
+    ref = torch.relu((x @ W.double().T) * es.double() + et.double())
+    got = out.cpu().view(torch.float8_e4m3fn).double()
+    err = (got - ref).abs() - (ref.abs() * 2.0 ** -4 + 2.0 ** -10)
+    assert float(err.max()) < 1e-4 * float(ref.abs().max())
+    cs = st[..., 0].double().cpu().sum(0)
+    assert float((cs - got.sum(0)).abs().max()) < 1e-5 * float(got.sum(0).abs().max())
