@@ -84,6 +84,12 @@ template <> struct FsCfg<128, 1024> {  // conv5 (BN5 + ReLU on the way out: a5)
 #ifndef FS_STG
 #define FS_STG 1
 #endif
+#ifndef FS_ABL
+#define FS_ABL 0   // timing ablations (wrong outputs): 1 no MFMAs, 2 no epilogue math, 3 no transform
+#endif
+#ifndef FS_ILV
+#define FS_ILV 1
+#endif
 #ifndef FS_CPOL
 #define FS_CPOL 2   // cache policy bits of the staged (STG) output stores: 2 = nt
 #endif
@@ -100,6 +106,11 @@ template <int K, int NCOLS, bool MASK, bool C8 = false> struct FsGeo {
   // C8 (the fp8 e4m3 a5 of cfg5): 64-B wave rows, staged, 16 rows x 64 B per store
   static constexpr int STG = C8 ? 1 : (FS_STG && WC == 64) ? ((FS_STG == 2 && NB == 512 && WRN == 1) ? 2 : 1) : 0;
   static constexpr int ESZ = C8 ? 1 : 2;                  // output element bytes
+  // the transform of step t+1 between the MFMA k-step groups of step t (its DMA waited for
+  // before them) instead of after the epilogue; not with STG 2 (stores after the first barrier).
+  // Measured (profiles/ab_r03_fwd_stream.md): seg_conv1 1.98 -> 1.89 ms, but seg_conv2 2.96 ->
+  // 3.03, seg_conv3 1.33 -> 1.35, conv5 3.68 -> 3.71 (the earlier wait costs them prefetch depth)
+  static constexpr bool ILV = FS_ILV && STG != 2 && K == 64;
   static constexpr int SROW = WC * ESZ;                   // staged wave-row bytes (128 or 64)
   static constexpr int CT = WC / 16;           // 16-column MFMA tiles per wave
   static constexpr int RW = MS / WRN;          // rows per wave per step
@@ -192,11 +203,13 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
     const float4 s1 = *reinterpret_cast<const float4 *>(a.pa + 8 * tc + 4);
     const float4 t0 = *reinterpret_cast<const float4 *>(a.pb + 8 * tc);
     const float4 t1 = *reinterpret_cast<const float4 *>(a.pb + 8 * tc + 4);
+    // with dropout the kept values are relu(y s + t) ks = relu(y (s ks) + t ks) (ks = 1 / (1 - p) > 0),
+    // then ANDed with the keep masks: the keep scale is folded into the coefficients
     const float ks = MASK ? a.a_keep_scale : 1.f;
-    // with dropout the kept values are relu(y s + t) * ks (then ANDed with the keep masks)
     ts[0] = s0.x; ts[1] = s0.y; ts[2] = s0.z; ts[3] = s0.w; ts[4] = s1.x; ts[5] = s1.y; ts[6] = s1.z; ts[7] = s1.w;
     tt[0] = t0.x; tt[1] = t0.y; tt[2] = t0.z; tt[3] = t0.w; tt[4] = t1.x; tt[5] = t1.y; tt[6] = t1.z; tt[7] = t1.w;
-    (void)ks;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { ts[e] *= ks; tt[e] *= ks; }
   }
   if constexpr (MASK) {   // dropout byte -> the AND masks of 8 packed bf16 values
     if (tid < 256) {
@@ -273,20 +286,16 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
   };
 
   // ---- in-place BN + ReLU (+ dropout) of a landed stage: each element once
-  const float kscale = MASK ? a.a_keep_scale : 1.f;
-  auto transform = [&](int sidx) {
+  auto transform_pass = [&](int sidx, int p) {
+    if constexpr (FS_ABL == 3) return;
     char *st = lds + sidx * F::STAGE;
-#pragma unroll
-    for (int p = 0; p < F::TPASS; ++p) {
+    {
       const int r = trow + p * (THREADS / SPR);
       u32x4 *q = reinterpret_cast<u32x4 *>(st + r * ROWB + ((tc ^ fsw<K>(r)) << 4));
       float v[8];
       unpack_chunk(*q, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[e] = fmaxf(fmaf(v[e], ts[e], tt[e]), 0.f);
-        if constexpr (MASK) v[e] *= kscale;
-      }
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], ts[e], tt[e]), 0.f);
       u32x4 out = pack_chunk(v);
       if constexpr (MASK) {
         const uint32_t byte = (uint8_t)st[F::XB + r * (K / 8) + tc];
@@ -295,6 +304,10 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       }
       *q = out;
     }
+  };
+  auto transform = [&](int sidx) {
+#pragma unroll
+    for (int p = 0; p < F::TPASS; ++p) transform_pass(sidx, p);
   };
 
   // ---- output through one buffer descriptor for the slice's rows (columns n0 .. of the block):
@@ -356,6 +369,14 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
     // barrier of every wave)
     dma_step(t + NST - 1, sc == 0 ? NST - 1 : sc - 1);
     const char *st = lds + sc * F::STAGE;
+    const int sn = sc + 1 == NST ? 0 : sc + 1;   // stage of step t+1
+    const bool more = t + 1 < nsteps;
+    if constexpr (F::ILV) {
+      // step t+1 landed (newer: NST-2 (DMA, stores) groups), so its transform can run between
+      // this step's MFMA groups
+      wait_vm<(NST - 2) * (F::LPS + F::SPS)>();
+      barrier_lds();
+    }
     f32x4 acc[CT][RT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
@@ -369,9 +390,23 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-          acc[ct][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wfr[ct][kk]), xf[rt],
-                                                               acc[ct][rt], 0, 0, 0);
+        for (int rt = 0; rt < RT; ++rt) {
+          if constexpr (FS_ABL == 1) {
+            asm volatile("" ::"v"(wfr[ct][kk]), "v"(xf[rt]));
+            acc[ct][rt][0] += 1.f;
+          } else {
+            acc[ct][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wfr[ct][kk]), xf[rt],
+                                                                 acc[ct][rt], 0, 0, 0);
+          }
+        }
+      if constexpr (F::ILV) {
+        constexpr int PER = KS / F::TPASS;   // MFMA k-steps per transform pass
+        if ((kk + 1) % PER == 0 && more) {
+          __builtin_amdgcn_sched_barrier(0);
+          transform_pass(sn, kk / PER);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
     // ---- epilogue of step t: lane holds y[row rbase + 16 rt + l16][col0 + 16 ct + 4 g + r]
     const int rem = (int)pcs_min64(hi - (lo + (int64_t)t * MS), MS);
@@ -380,6 +415,13 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
     for (int rt = 0; rt < RT; ++rt) {
       const bool live = full || rbase + 16 * rt + l16 < rem;
       uint32_t pk[CT][2];
+      if constexpr (FS_ABL == 2) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          pk[ct][0] = __float_as_uint(acc[ct][rt][0]) ^ __float_as_uint(acc[ct][rt][1]);
+          pk[ct][1] = __float_as_uint(acc[ct][rt][2]) ^ __float_as_uint(acc[ct][rt][3]);
+        }
+      } else
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         float v[4];
@@ -482,8 +524,10 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
     }
     o_out += MS * NCOLS * 2;
     // step t+1 landed: newer are NST-2 (DMA, stores) groups and (unless STG 2) this step's stores
-    wait_vm<F::WAIT_N>();
-    barrier_lds();
+    if constexpr (!F::ILV) {
+      wait_vm<F::WAIT_N>();
+      barrier_lds();
+    }
     if constexpr (F::STG == 2) {
       // whole rows of the step's tile: wave w stores rows w + 8 i, lane = 16-B chunk lane % 8 of
       // the 128-B column block lane / 8 (granule swizzle as written, halves swapped on odd rows)
@@ -498,7 +542,9 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       }
       o_stg += MS * NCOLS * 2;
     }
-    if (t + 1 < nsteps) transform(sc + 1 == NST ? 0 : sc + 1);
+    if constexpr (!F::ILV) {
+      if (more) transform(sn);
+    }
     barrier_lds();
     sc = sc + 1 == NST ? 0 : sc + 1;
   }
