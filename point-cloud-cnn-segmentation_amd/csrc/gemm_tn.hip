@@ -334,6 +334,7 @@ extern "C" int64_t pcs_wgrad_workspace(pcs_wgrad_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Cout <= 0 || a->Cin <= 0)
     return pcs_set_einval("pcs_wgrad_workspace", "bad geometry");
   const int ms = a->dtype == PCS_BF16 ? TnCfg<bf16_t>::MS : TnCfg<float>::MS;
+  if (a->splits_per_scene <= 0 && pcs_wgrad_c5_class(*a)) a->splits_per_scene = pcs_wgrad_c5_splits(*a);
   if (a->splits_per_scene <= 0 && pcs_wgrad_big_applicable(*a)) a->splits_per_scene = pcs_wgrad_big_splits(*a);
   if (a->splits_per_scene <= 0) {
     const int tm = a->Cout % 128 == 0 ? 128 : 64, tn = a->Cin % 128 == 0 ? 128 : 64;
@@ -364,7 +365,8 @@ extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   const int64_t rps = rows_per_split_of(a, ms);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int rc;
-  if (pcs_wgrad_big_applicable(a)) rc = pcs_wgrad_big_launch(a, s);
+  if (pcs_wgrad_c5_applicable(a)) rc = pcs_wgrad_c5_launch(a, rps, s);
+  else if (pcs_wgrad_big_applicable(a)) rc = pcs_wgrad_big_launch(a, s);
   else if (a.dtype == PCS_BF16) rc = dispatch_tiles<bf16_t>(a, rps, s);
   else if (a.dtype == PCS_F32) rc = dispatch_tiles<float>(a, rps, s);
   else return pcs_set_einval("pcs_wgrad", "bad dtype");
