@@ -256,6 +256,12 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
   // the dy slot's logical chunk is the same for all its rows (they differ by 16 rows: ftr is
   // periodic in 16), so one set of coefficients serves every pass
   const char *cfd = lds + F::OFF_CF + (dlc ^ ftr(drr)) * 16;
+#ifndef SEG_CREG
+#define SEG_CREG 1
+#endif
+  // SEG_CREG: the thread's 24 dy-transform coefficients held in registers (read from LDS once,
+  // after the barrier below) instead of 6 ds_read_b128 per transform pass
+  float rca[8], rcb[8], rcg[8];
   const char *cfx = lds + F::OFF_CF + 3 * COUT * 4 + xlc * 16;
   const int l16 = lane & 15, g = lane >> 4;
   const int ct = wid;
@@ -311,9 +317,14 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
     float ca[8], cb[8], cg[8], v[8], y[8];
     const u32x4 dz = *reinterpret_cast<const u32x4 *>(st + o_tr + i * THREADS * 16);
     const u32x4 yy = *reinterpret_cast<const u32x4 *>(st + F::DZB + o_tr + i * THREADS * 16);
-    lds_vec8(cfd, COUT * 2, ca);
-    lds_vec8(cfd + COUT * 4, COUT * 2, cb);
-    lds_vec8(cfd + 2 * COUT * 4, COUT * 2, cg);
+    if constexpr (SEG_CREG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { ca[e] = rca[e]; cb[e] = rcb[e]; cg[e] = rcg[e]; }
+    } else {
+      lds_vec8(cfd, COUT * 2, ca);
+      lds_vec8(cfd + COUT * 4, COUT * 2, cb);
+      lds_vec8(cfd + 2 * COUT * 4, COUT * 2, cg);
+    }
     unpack_chunk(dz, v);
     unpack_chunk(yy, y);
 #pragma unroll
@@ -358,6 +369,11 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
   }
   wait_vm<1 + (F::NST - 2) * (F::VM_STEP + 1)>();
   barrier_lds();
+  if constexpr (SEG_CREG) {   // (the coefficients were written to LDS before this barrier)
+    lds_vec8(cfd, COUT * 2, rca);
+    lds_vec8(cfd + COUT * 4, COUT * 2, rcb);
+    lds_vec8(cfd + 2 * COUT * 4, COUT * 2, rcg);
+  }
 #pragma unroll
   for (int i = 0; i < F::DY_RPT; ++i) transform_dy(0, 0, i);
   transform_x(0, 0);
@@ -388,7 +404,10 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
     // operand reads run PD k-steps ahead of the MFMAs
     f32x4 accd[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     {
-      constexpr int PD = 3;
+#ifndef SEG_PD
+#define SEG_PD 3
+#endif
+      constexpr int PD = SEG_PD;
       bf16x8 yf[PD + 1][2];
       auto rd_dg = [&](int kk, bf16x8 (&d)[2]) {
 #pragma unroll
