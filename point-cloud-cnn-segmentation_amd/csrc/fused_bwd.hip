@@ -770,7 +770,10 @@ extern "C" int64_t pcs_dgrad_wgrad_bn_workspace(pcs_gemm_args *a) {
     return pcs_set_einval("pcs_dgrad_wgrad_bn_workspace",
                           "bf16 with (Cout, Cin) = K x Ncols in {64x64, 128x64} only");
   const int nblk = sh->cin / sh->cb;
-  int64_t sps = (256 + a->num_scenes * nblk - 1) / (a->num_scenes * nblk);
+  // 64 x 64 (conv2, conv3: <= 128 VGPRs) fits two 512-thread workgroups per CU: twice the
+  // workgroups, 0.91 -> 0.85 ms at cfg2; 128 x 64 (conv4, 158-164 VGPRs) stays at one
+  const int64_t target = sh->cout == 64 ? 512 : 256;
+  int64_t sps = (target + a->num_scenes * nblk - 1) / (a->num_scenes * nblk);
   const int64_t max_sps = (a->scene_rows + 4 * sh->ms - 1) / (4 * sh->ms);
   if (sps > max_sps) sps = max_sps;
   if (sps < 1) sps = 1;
