@@ -7,7 +7,7 @@
 // * a workgroup (8 waves) owns NB = 256 dz5 columns and all 128 a4 channels of a scene-aligned
 //   row slice: the [256 x 128] fp32 partial of R stays in registers (64 per lane), the slice's
 //   partial goes out once, summed over the slices by pcs_reduce_partials (fixed order);
-// * 32-row steps of dz5 (16 KB) and y4 (8 KB) through a 4-stage LDS ring by LDS-DMA, counted
+// * 32-row steps of dz5 (16 KB) and y4 (8 KB) through a 2-stage LDS ring by LDS-DMA, counted
 //   waits; relu(bn4(y4)) formed once per element into a double-buffered x tile (the 4 column
 //   blocks of a slice repeat this 128-wide transform, on one XCD, through L2);
 // * MFMA operands by ds_read_b64_tr_b16 of the row-major dz5 and x tiles (k = rows), the
@@ -20,7 +20,15 @@ constexpr int THREADS = 512;
 constexpr int MS = 32;           // rows per step
 constexpr int NB = 256;          // dz5 columns per workgroup
 constexpr int CIN = 128;         // a4 channels
-constexpr int NST = 4;           // ring stages
+// two stages (66 KB of LDS) so that two workgroups share a CU (512 in the grid): 3.85 -> 3.64 ms
+// in tools/bench_wc5.py against four stages at one workgroup per CU (three: 3.85)
+#ifndef WC5_NST
+#define WC5_NST 2
+#endif
+#ifndef WC5_TARGET
+#define WC5_TARGET 512
+#endif
+constexpr int NST = WC5_NST;     // ring stages
 constexpr int ROWB = NB * 2;     // 512-B dz5 rows in LDS
 constexpr int SPR = ROWB / 16;   // 32 slots
 constexpr int DZB = MS * ROWB;   // 16 KB
@@ -236,10 +244,10 @@ bool pcs_wgrad_c5_applicable(const pcs_wgrad_args &a) {
   return pcs_wgrad_c5_class(a) && !a.x_mask && a.dZ && a.X && a.s && a.t;
 }
 
-// one 512-thread workgroup per CU: splits per scene so that (Cout / 256) x B x splits ~ 256
+// two 512-thread workgroups per CU: splits per scene so that (Cout / 256) x B x splits ~ 512
 int pcs_wgrad_c5_splits(const pcs_wgrad_args &a) {
   const int64_t ncb = a.Cout / NB;
-  int64_t sps = (256 + a.num_scenes * ncb - 1) / (a.num_scenes * ncb);
+  int64_t sps = (WC5_TARGET + a.num_scenes * ncb - 1) / (a.num_scenes * ncb);
   const int64_t max_sps = (a.scene_rows + 4 * MS - 1) / (4 * MS);   // >= 4 steps per split
   if (sps > max_sps) sps = max_sps;
   if (sps < 1) sps = 1;
