@@ -181,7 +181,7 @@ bool pcs_c5_dgrad_applicable(const pcs_gemm_args &a);
 int pcs_c5_dgrad_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
 // streaming forward of the narrow-K BN+ReLU layers (fwd_stream.hip): output columns per
 // workgroup (0 = not this kernel's class; shapes only, the chunk geometry), applicability, launch
-int pcs_fwd_stream_nb(const pcs_gemm_args &a);
+int pcs_fwd_stream_nb(const pcs_gemm_args &a, int *target_workgroups);
 bool pcs_fwd_stream_applicable(const pcs_gemm_args &a);
 int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
 // conv5's R = dz5^T relu(bn4(y4)) as an LDS-DMA stream (wgrad_c5.hip)

@@ -68,17 +68,28 @@ PCS_DEV void barrier_lds() {
 //   NB output columns per workgroup, WCN wave columns (8 / WCN wave rows), MS rows per step,
 //   NST ring stages.
 template <int K, int NCOLS> struct FsCfg;
+// TARGET: workgroups in the grid (256 = one per CU; the small 64-wide layers, whose workgroups
+// fit several to a CU, take more)
 template <> struct FsCfg<64, 512> {   // seg_conv1 (local half)
-  static constexpr int NB = 512, WCN = 8, MS = 64, NST = 4;
+  static constexpr int NB = 512, WCN = 8, MS = 64, NST = 4, TARGET = 256;
 };
 template <> struct FsCfg<512, 256> {   // seg_conv2
-  static constexpr int NB = 256, WCN = 8, MS = 32, NST = 4;
+  static constexpr int NB = 256, WCN = 8, MS = 32, NST = 4, TARGET = 256;
 };
 template <> struct FsCfg<256, 128> {   // seg_conv3
-  static constexpr int NB = 128, WCN = 4, MS = 64, NST = 4;
+  static constexpr int NB = 128, WCN = 4, MS = 64, NST = 4, TARGET = 256;
 };
 template <> struct FsCfg<128, 1024> {  // conv5 (BN5 + ReLU on the way out: a5)
-  static constexpr int NB = 512, WCN = 8, MS = 64, NST = 4;
+  static constexpr int NB = 512, WCN = 8, MS = 64, NST = 4, TARGET = 256;
+};
+#ifndef FS_SMALL_TARGET
+#define FS_SMALL_TARGET 1024
+#endif
+template <> struct FsCfg<64, 128> {    // conv4
+  static constexpr int NB = 128, WCN = 4, MS = 64, NST = 4, TARGET = FS_SMALL_TARGET;
+};
+template <> struct FsCfg<64, 64> {     // conv2, conv3
+  static constexpr int NB = 64, WCN = 2, MS = 64, NST = 4, TARGET = FS_SMALL_TARGET;
 };
 
 #ifndef FS_STG
@@ -601,22 +612,28 @@ template <int K, int NC> struct FsShape {
 
 // Class (geometry, shapes only) and applicability (operands) of the streaming forward kernel.
 // bf16, PRO_BNRELU; EPI_FWD on (K, Ncols) = (64, 512) seg_conv1, (512, 256) seg_conv2, (256, 128)
-// seg_conv3; EPI_BNRELU with a bf16 store on (128, 1024) conv5.
-int pcs_fwd_stream_nb(const pcs_gemm_args &a) {
+// seg_conv3, (64, 128) conv4, (64, 64) conv2 / conv3; EPI_BNRELU with a bf16 store on (128, 1024) conv5.
+template <int K, int NC> int fs_nb(int *target) {
+  if (target) *target = FsCfg<K, NC>::TARGET;
+  return FsCfg<K, NC>::NB;
+}
+int pcs_fwd_stream_nb(const pcs_gemm_args &a, int *target) {
   if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_AW_FP8)) || a.prologue != PCS_PRO_BNRELU)
     return 0;
   if (a.epilogue == PCS_EPI_FWD) {
-    if (FsShape<64, 512>::is(a)) return FsCfg<64, 512>::NB;
-    if (FsShape<512, 256>::is(a)) return FsCfg<512, 256>::NB;
-    if (FsShape<256, 128>::is(a)) return FsCfg<256, 128>::NB;
+    if (FsShape<64, 512>::is(a)) return fs_nb<64, 512>(target);
+    if (FsShape<512, 256>::is(a)) return fs_nb<512, 256>(target);
+    if (FsShape<256, 128>::is(a)) return fs_nb<256, 128>(target);
+    if (FsShape<64, 128>::is(a)) return fs_nb<64, 128>(target);
+    if (FsShape<64, 64>::is(a)) return fs_nb<64, 64>(target);
   } else if (a.epilogue == PCS_EPI_BNRELU) {
-    if (FsShape<128, 1024>::is(a)) return FsCfg<128, 1024>::NB;
+    if (FsShape<128, 1024>::is(a)) return fs_nb<128, 1024>(target);
   }
   return 0;
 }
 
 bool pcs_fwd_stream_applicable(const pcs_gemm_args &a) {
-  if (!pcs_fwd_stream_nb(a) || !a.C || !a.pa || !a.pb || a.pool) return false;
+  if (!pcs_fwd_stream_nb(a, nullptr) || !a.C || !a.pa || !a.pb || a.pool) return false;
   if ((a.flags & PCS_FLAG_C_FP8) && a.epilogue != PCS_EPI_BNRELU) return false;
   if (a.scene_rows * a.num_scenes >= ((int64_t)1 << 31)) return false;
   if (a.epilogue == PCS_EPI_BNRELU) return a.es && a.et && !a.a_mask && !a.scene_bias;
@@ -627,7 +644,7 @@ bool pcs_fwd_stream_applicable(const pcs_gemm_args &a) {
 }
 
 int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s) {
-  const int nb_cols = pcs_fwd_stream_nb(a);
+  const int nb_cols = pcs_fwd_stream_nb(a, nullptr);
   const int nb = (int)(a.num_scenes * a.chunks_per_scene) * (a.Ncols / nb_cols);
 #define PCS_FS(K, NC, EPI, MK, SB) \
   hipLaunchKernelGGL((fwd_stream_kernel<K, NC, EPI, MK, SB>), dim3(nb), dim3(THREADS), 0, s, a, rows_per_chunk)
@@ -644,6 +661,10 @@ int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStr
     if (mk) PCS_FS(512, 256, PCS_EPI_FWD, true, false); else PCS_FS(512, 256, PCS_EPI_FWD, false, false);
   } else if (FsShape<256, 128>::is(a)) {
     if (mk) PCS_FS(256, 128, PCS_EPI_FWD, true, false); else PCS_FS(256, 128, PCS_EPI_FWD, false, false);
+  } else if (FsShape<64, 128>::is(a)) {
+    PCS_FS(64, 128, PCS_EPI_FWD, false, false);
+  } else if (FsShape<64, 64>::is(a)) {
+    PCS_FS(64, 64, PCS_EPI_FWD, false, false);
   } else {
     return pcs_set_einval("pcs_gemm", "streaming forward: unsupported shape");
   }

@@ -595,8 +595,9 @@ static bool wide_class(const pcs_gemm_args &a) {
 extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0 || a->Ncols <= 0)
     return pcs_set_einval("pcs_gemm_geometry", "empty geometry");
-  if (const int nbc = pcs_fwd_stream_nb(*a))   // streaming forward: one 512-thread WG per CU
-    return pcs_fill_geometry(a, 256, 256, a->Ncols / nbc);
+  int fs_target = 256;
+  if (const int nbc = pcs_fwd_stream_nb(*a, &fs_target))   // streaming forward
+    return pcs_fill_geometry(a, 256, fs_target, a->Ncols / nbc);
   if (wide_class(*a))
     return pcs_fill_geometry(a, PCS_BIG_BM, 256, a->Ncols / 256);   // one 512-thread WG per CU
   if (pcs_c5_dgrad_class(*a))   // conv5's folded input gradient: one 512-thread WG per CU

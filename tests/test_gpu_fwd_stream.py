@@ -1,5 +1,5 @@
 """The streaming forward kernel (csrc/fwd_stream.hip: pcs_gemm PRO_BNRELU with EPI_FWD on the
-narrow-K layers seg_conv1 / seg_conv2 / seg_conv3, EPI_BNRELU on conv5) against torch
+narrow-K layers seg_conv1 / seg_conv2 / seg_conv3 / conv4 / conv2-3, EPI_BNRELU on conv5) against torch
 fp64 on the same bf16 operands and against the generic kernel (PCS_FLAG_GENERIC), on ragged
 scenes (rows not a multiple of the step, several chunks, a slice shorter than one step).
 
@@ -15,7 +15,8 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
-SHAPES = [(64, 512, "scene"), (512, 256, "mask"), (256, 128, "mask"), (128, 1024, "bnrelu")]
+SHAPES = [(64, 512, "scene"), (512, 256, "mask"), (256, 128, "mask"), (64, 128, "bias"), (64, 64, "bias"),
+          (128, 1024, "bnrelu")]
 
 
 def _run(B, N, K, C, kind, seed, generic=False, nomask=False):

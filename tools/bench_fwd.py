@@ -27,6 +27,8 @@ def run(B, N, K, C, kind, reps):
     a.pa, a.pb = keep[0].data_ptr(), keep[1].data_ptr()
     if kind == "bnrelu":
         a.es, a.et = keep[2].data_ptr(), keep[3].data_ptr()
+    if kind == "bias":
+        a.bias = keep[2].data_ptr()
     if kind == "scene":
         a.scene_bias = keep[4].data_ptr()
     bits = torch.randint(0, 256, (M, K // 8), device=dev, dtype=torch.uint8)
@@ -52,7 +54,10 @@ def run(B, N, K, C, kind, reps):
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     B, N = 4, 128 ** 3
-    for K, C, kind in [(64, 512, "scene"), (512, 256, "mask"), (256, 128, "mask"), (128, 1024, "bnrelu")]:
+    shapes = [(64, 512, "scene"), (512, 256, "mask"), (256, 128, "mask"), (128, 1024, "bnrelu")]
+    if os.environ.get("FS_SHAPES") == "small":   # conv4, conv2 / conv3
+        shapes = [(64, 128, "bias"), (64, 64, "bias")]
+    for K, C, kind in shapes:
         run(B, N, K, C, kind, reps)
 
 
