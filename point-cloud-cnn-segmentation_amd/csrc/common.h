@@ -184,6 +184,11 @@ int pcs_c5_dgrad_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStrea
 int pcs_fwd_stream_nb(const pcs_gemm_args &a, int *target_workgroups);
 bool pcs_fwd_stream_applicable(const pcs_gemm_args &a);
 int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
+// the Gram of relu(bn(Y)) at C = 128 in one pass over Y (wgrad_c5.hip; pcs_gram)
+bool pcs_gram128_class(const pcs_wgrad_args &a);
+bool pcs_gram128_applicable(const pcs_wgrad_args &a);
+int pcs_gram128_splits(const pcs_wgrad_args &a);
+int pcs_gram128_launch(const pcs_wgrad_args &a, hipStream_t s);
 // conv5's R = dz5^T relu(bn4(y4)) as an LDS-DMA stream (wgrad_c5.hip)
 bool pcs_wgrad_c5_class(const pcs_wgrad_args &a);
 bool pcs_wgrad_c5_applicable(const pcs_wgrad_args &a);

@@ -411,6 +411,7 @@ extern "C" int64_t pcs_gram_workspace(int64_t num_scenes, int64_t scene_rows, in
   if (num_scenes <= 0 || scene_rows <= 0 || C <= 0 || C % 64 || !splits_per_scene)
     return pcs_set_einval("pcs_gram_workspace", "bad geometry");
   pcs_wgrad_args a = gram_args(nullptr, nullptr, nullptr, num_scenes, scene_rows, C, dtype, 0);
+  if (pcs_gram128_class(a)) a.splits_per_scene = pcs_gram128_splits(a);
   const int64_t g = pcs_wgrad_workspace(&a);
   if (g < 0) return g;
   *splits_per_scene = a.splits_per_scene;
@@ -429,7 +430,9 @@ extern "C" int pcs_gram(const void *Y, const float *s, const float *t, int64_t n
   int rc;
   if (!s && !pcs_wgrad_big_applicable(a))   // s = t = NULL: Y is already the activation
     return pcs_set_einval("pcs_gram", "s = t = NULL needs the 256x256 kernel (bf16, C % 256 == 0)");
-  if (pcs_wgrad_big_applicable(a)) {
+  if (pcs_gram128_applicable(a)) {
+    rc = pcs_gram128_launch(a, st);
+  } else if (pcs_wgrad_big_applicable(a)) {
     rc = pcs_wgrad_big_launch(a, st);
   } else {
     const int ms = dtype == PCS_BF16 ? TnCfg<bf16_t>::MS : TnCfg<float>::MS;

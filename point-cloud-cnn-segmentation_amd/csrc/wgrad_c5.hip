@@ -231,7 +231,218 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
           make_float4(acc[ob][u][0], acc[ob][u][1], acc[ob][u][2], acc[ob][u][3]);
 }
 
+// ---------------------------------------------------------------------------------------
+// The Gram of a4 = relu(bn4(y4)) (pcs_gram at C = 128: bn5's statistics from G = a4^T a4 and the
+// column sums of a4, fwd_stats:conv5).  The generic tiled kernel reads y4 once per 64-wide tile
+// column (3.2 TB/s, 0.66 ms at cfg2); here one workgroup owns all 128 x 128 of a row slice:
+// * 64-row steps of y4 (16 KB) through an NST-stage LDS ring by LDS-DMA, rows in the transposed-
+//   read layout (chunk c at c ^ ftr(r)); relu(bn4(.)) applied in place, rows past the slice zeroed;
+// * both MFMA operands are transposed reads of that tile: wave w accumulates G[16 w + l16][all]
+//   (8 blocks, 32 fp32 per lane); the fp32 column sums ride the transform.
+constexpr int G_MS = 64;                  // rows per step
+#ifndef GRAM_NST
+#define GRAM_NST 4
+#endif
+#ifndef GRAM_SYM
+#define GRAM_SYM 1
+#endif
+#ifndef GRAM_TARGET
+#define GRAM_TARGET 512
+#endif
+constexpr int G_NST = GRAM_NST;
+constexpr int G_YB = G_MS * YROW;         // 16 KB
+constexpr int G_LPS = G_YB / 1024 / 8;    // 1-KB DMA pieces per wave per step (2)
+constexpr int G_BYTES = G_NST * G_YB;
+static_assert(G_BYTES + 8 * CIN * 4 <= 160 * 1024, "LDS budget");
+
+__global__ __launch_bounds__(THREADS) void gram128_kernel(pcs_wgrad_args a, int64_t rows_per_split) {
+  __shared__ __attribute__((aligned(16))) char lds[G_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int split = xcd_remap(blockIdx.x, gridDim.x);
+  const int sps = a.splits_per_scene;
+  const int scene = __builtin_amdgcn_readfirstlane(split / sps), sis = __builtin_amdgcn_readfirstlane(split % sps);
+  const int64_t N = a.scene_rows;
+  const int64_t lo = (int64_t)sis * rows_per_split;
+  const int64_t hi = pcs_min64(lo + rows_per_split, N);
+  const int64_t sbase = (int64_t)scene * N;
+  // an empty trailing slice (splits x rounded rows past the scene) runs no step and writes zeros
+  const int nsteps = hi > lo ? (int)((hi - lo + G_MS - 1) / G_MS) : 0;
+  const char *Yg = reinterpret_cast<const char *>(a.Y);
+
+  // transform: thread -> rows tid / 16 and 32 + tid / 16, logical chunk tid % 16 (8 channels)
+  const int xlc = tid & 15, xrr = tid >> 4;
+  float xs[8], xt[8], cs[8];
+  load_vec<8>(a.s, 8 * xlc, xs);
+  load_vec<8>(a.t, 8 * xlc, xt);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    asm volatile("" ::"v"(xs[e]), "v"(xt[e]));   // retired before the DMA
+    cs[e] = 0.f;
+  }
+  __syncthreads();
+
+  // DMA pieces j = wid + 8 i: 4 rows of 256 B each; rows past the slice clamp to its last row
+  auto y_off = [&](int i, int lastr) -> uint32_t {
+    const int r = (wid + 8 * i) * 4 + (lane >> 4), ps = lane & 15;
+    return (uint32_t)(min(r, lastr) * YROW + ((ps ^ ftr(r)) << 4));
+  };
+  uint32_t voff[G_LPS];
+#pragma unroll
+  for (int i = 0; i < G_LPS; ++i) voff[i] = y_off(i, G_MS - 1);
+  const uint32_t lds_m0 = (uint32_t)(uintptr_t)(lds_void_t *)lds;
+  static_assert(G_LPS == 2, "two y4 pieces per wave per step");
+  auto dma_issue = [&](int sidx, int64_t m0, const uint32_t (&vo)[G_LPS]) {
+    const uint32_t mb = lds_m0 + sidx * G_YB + wid * 1024;
+    const char *by = Yg + (sbase + m0) * YROW;
+    const uint32_t keep = m0_save();
+    glds16o<0>(by, vo[0], mb);
+    glds16o<8192>(by, vo[1], mb);
+    m0_restore(keep);
+  };
+  auto dma_step = [&](int s) {
+    const int64_t m0 = pcs_min64(lo + (int64_t)s * G_MS, hi - 1);
+    const int lastr = (int)pcs_min64(hi - 1 - m0, G_MS - 1);
+    const int sidx = s % G_NST;
+    if (lastr == G_MS - 1) {   // uniform: a full step
+      dma_issue(sidx, m0, voff);
+    } else {
+      uint32_t vt[G_LPS];
+#pragma unroll
+      for (int i = 0; i < G_LPS; ++i) vt[i] = y_off(i, lastr);
+      dma_issue(sidx, m0, vt);
+    }
+  };
+  // in place: a4 over y4 in the stage, rows past the slice -> 0
+  auto transform = [&](int s) {
+    const int rem = (int)pcs_min64(hi - (lo + (int64_t)s * G_MS), G_MS);
+    char *st = lds + (s % G_NST) * G_YB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = xrr + 32 * h;
+      u32x4 *pc = reinterpret_cast<u32x4 *>(st + r * YROW + ((xlc ^ ftr(r)) << 4));
+      float v[8];
+      unpack_chunk(*pc, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = r < rem ? fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += v[e];   // column sums in fp32 (as the tiled kernel)
+      *pc = pack_chunk(v);
+    }
+  };
+
+  // transposed reads: columns 16 u + 4 p of rows 32 kk + 8 g + q and 32 kk + 8 g + 4 + q
+  const int g = lane >> 4, l16 = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
+  const int tr0 = 8 * g + q, tr1 = 8 * g + 4 + q;
+  auto o_frag = [&](int u, int row) { return row * YROW + (((2 * u + (p >> 1)) ^ ftr(row)) << 4) + 8 * (p & 1); };
+#if GRAM_SYM
+  // symmetric: wave w forms the 16-wide blocks (w, w + d mod 8), d = 0 .. 3 (and d = 4 for w < 4):
+  // the 36 blocks of one triangle; the partial gets each block and its transpose
+  constexpr int NU = 5;
+  const int nu = wid < 4 ? 5 : 4;
+#else
+  constexpr int NU = 8;
+  const int nu = 8;
+#endif
+  int o_u[NU][2];
+#pragma unroll
+  for (int d = 0; d < NU; ++d) {
+    const int u = GRAM_SYM ? (wid + d) & 7 : d;
+    o_u[d][0] = o_frag(u, tr0);
+    o_u[d][1] = o_frag(u, tr1);
+  }
+  const int o_w0 = o_frag(wid, tr0), o_w1 = o_frag(wid, tr1);
+
+  f32x4 acc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < G_NST - 1; ++s) dma_step(s);
+  for (int t = 0; t < nsteps; ++t) {
+    wait_vm<(G_NST - 2) * G_LPS>();   // step t landed (t+1 .. t+NST-2 in flight)
+    barrier_lds();                     // ... for every wave; all done with step t-1's stage
+    dma_step(t + G_NST - 1);           // into step t-1's stage
+    transform(t);
+    barrier_lds();
+    const char *st = lds + (t % G_NST) * G_YB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kb = kk * 32 * YROW;
+      const bf16x8 w = tr_frag2(st + kb + o_w0, st + kb + o_w1);
+      bf16x8 xf[2];
+      xf[0] = tr_frag2(st + kb + o_u[0][0], st + kb + o_u[0][1]);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        if (u + 1 < NU) xf[(u + 1) & 1] = tr_frag2(st + kb + o_u[u + 1][0], st + kb + o_u[u + 1][1]);
+        if (u < 4 || u < nu) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u & 1], w, acc[u], 0, 0, 0);
+      }
+    }
+  }
+  wait_vm<0>();   // the clamped DMAs past the end
+
+  // G partial: [16 wid + l16][16 u + 4 g .. + 4]
+  float *out = a.partial + (int64_t)split * CIN * CIN;
+#pragma unroll
+  for (int d = 0; d < NU; ++d) {
+    if (d >= nu) continue;
+    const int u = GRAM_SYM ? (wid + d) & 7 : d;
+    *reinterpret_cast<float4 *>(out + (int64_t)(16 * wid + l16) * CIN + 16 * u + 4 * g) =
+        make_float4(acc[d][0], acc[d][1], acc[d][2], acc[d][3]);
+    if (GRAM_SYM && d > 0) {   // the transposed block
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(int64_t)(16 * u + 4 * g + r) * CIN + 16 * wid + l16] = acc[d][r];
+    }
+  }
+  // column sums: lanes l, l + 16, l + 32, l + 48 of a wave, then the 8 waves through LDS
+  __syncthreads();
+  float *red = reinterpret_cast<float *>(lds);   // [8 waves][128]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = cs[e];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    cs[e] = v;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wid * CIN + 8 * lane + e] = cs[e];
+  }
+  __syncthreads();
+  if (tid < CIN) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[w * CIN + tid];
+    const int64_t nsplit = a.num_scenes * (int64_t)sps;
+    a.partial[nsplit * CIN * CIN + (int64_t)split * CIN + tid] = v;
+  }
+}
+
 }  // namespace
+
+bool pcs_gram128_class(const pcs_wgrad_args &a) {   // shapes / modes only (the split geometry)
+  return a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && a.dy_mode == PCS_PRO_BNRELU &&
+         a.x_mode == PCS_PRO_BNRELU && a.Cin == CIN && a.Cout == CIN &&
+         a.num_scenes * a.scene_rows < ((int64_t)1 << 31);
+}
+bool pcs_gram128_applicable(const pcs_wgrad_args &a) {
+  return pcs_gram128_class(a) && a.Y && a.Y == a.X && a.s && a.t && !a.x_mask;
+}
+int pcs_gram128_splits(const pcs_wgrad_args &a) {
+  int64_t sps = (GRAM_TARGET + a.num_scenes - 1) / a.num_scenes;
+  const int64_t max_sps = (a.scene_rows + 4 * G_MS - 1) / (4 * G_MS);   // >= 4 steps per split
+  if (sps > max_sps) sps = max_sps;
+  if (sps < 1) sps = 1;
+  return (int)sps;
+}
+int pcs_gram128_launch(const pcs_wgrad_args &a, hipStream_t s) {
+  int64_t rps = (a.scene_rows + a.splits_per_scene - 1) / a.splits_per_scene;
+  rps = (rps + G_MS - 1) / G_MS * G_MS;
+  const int nb = (int)(a.num_scenes * a.splits_per_scene);
+  hipLaunchKernelGGL(gram128_kernel, dim3(nb), dim3(THREADS), 0, s, a, rps);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
 
 // conv5's R: bf16, dy_mode RAW (dZ = dz5), x_mode BNRELU without dropout bits, Cin 128,
 // Cout a multiple of 256

@@ -33,7 +33,10 @@ def _case(B, N, C, dtype, seed=0):
 
 
 @pytest.mark.parametrize("B,N,C,dtype", [(2, 700, 256, "bf16"),   # 256x256 kernel (upper tiles)
-                                         (3, 333, 128, "bf16"),   # generic bf16 kernel
+                                         (3, 333, 128, "bf16"),   # one-pass 128 kernel (wgrad_c5.hip)
+                                         (2, 70005, 128, "bf16"),  # ... several slices, ragged tail
+                                         (51, 3000, 128, "bf16"),  # ... an empty trailing slice
+                                         (2, 300, 192, "bf16"),   # generic bf16 kernel
                                          (2, 257, 128, "fp32")])
 def test_gram_matches_torch(B, N, C, dtype):
     L, dt, Y, s, t, a, G, S = _case(B, N, C, dtype)
