@@ -184,6 +184,10 @@ int pcs_c5_dgrad_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStrea
 int pcs_fwd_stream_nb(const pcs_gemm_args &a, int *target_workgroups);
 bool pcs_fwd_stream_applicable(const pcs_gemm_args &a);
 int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStream_t s);
+// the streamed CE head (head_stream.hip; pcs_head): class (shapes / modes), grid target, launch
+bool pcs_head_stream_class(const pcs_head_args &a);
+int pcs_head_stream_target();
+int pcs_head_stream_launch(const pcs_head_args &a, int64_t rows_per_chunk, hipStream_t s);
 // the Gram of relu(bn(Y)) at C = 128 in one pass over Y (wgrad_c5.hip; pcs_gram)
 bool pcs_gram128_class(const pcs_wgrad_args &a);
 bool pcs_gram128_applicable(const pcs_wgrad_args &a);

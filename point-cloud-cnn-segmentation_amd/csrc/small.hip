@@ -798,6 +798,12 @@ __global__ __launch_bounds__(THREADS) void head_wide_kernel(pcs_head_args a, int
   }
 }
 
+#ifndef HEAD_BATCH
+#define HEAD_BATCH 4
+#endif
+#ifndef HEAD_SB
+#define HEAD_SB 0
+#endif
 // Register-resident head for C <= 4 classes: 16 threads per point (one 8-channel bf16 /
 // 4-channel fp32 chunk each; 2 chunks per thread for fp32), logits all-reduced across
 // those 16 lanes by shuffles, seg_conv4 weights, dW/db partials and bn_seg3 S1/S2 kept
@@ -808,7 +814,7 @@ __global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, in
   constexpr int CPT = 8 / EPC;            // chunks per thread (8 channels per thread)
   constexpr int TPR = HEAD_CIN / 8;       // 16 threads per row
   constexpr int RPP = THREADS / TPR;      // 16 rows per pass
-  constexpr int BATCH = 4;
+  constexpr int BATCH = HEAD_BATCH;
   __shared__ float red[THREADS];
   const int tid = threadIdx.x, sub = tid % TPR, r0 = tid / TPR, ch0 = sub * 8;
   const int cps = a.chunks_per_scene;
@@ -852,6 +858,9 @@ __global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, in
     }
 #pragma unroll
     for (int q = 0; q < BATCH; ++q) {
+#if HEAD_SB
+      __builtin_amdgcn_sched_barrier(0);   // one row at a time (no interleaved live ranges)
+#endif
       const int64_t r = rb + r0 + RPP * q;
       const bool ok = r < hi;
       const int64_t row = scene * N + (ok ? r : hi - 1);
@@ -1263,6 +1272,11 @@ extern "C" int pcs_pool_bwd(const pcs_pool_bwd_args *ap, pcs_stream_t stream) {
 
 extern "C" int64_t pcs_head_geometry(pcs_head_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_head_geometry", "bad geometry");
+  if (pcs_head_stream_class(*a)) {   // the streamed CE head (head_stream.hip): 64-row steps
+    const int64_t tpc = chunk_geo(a->scene_rows, a->num_scenes, 64, &a->chunks_per_scene,
+                                  pcs_head_stream_target());
+    return tpc * 64;
+  }
   if (a->num_classes <= 4) {   // register-resident kernel: 64-row granules, ~8 WGs per CU
     const int64_t tpc = chunk_geo(a->scene_rows, a->num_scenes, 64, &a->chunks_per_scene, 2048);
     return tpc * 64;
@@ -1288,6 +1302,7 @@ extern "C" int pcs_head(const pcs_head_args *ap, pcs_stream_t stream) {
   const int tpc = (int)(rpc / HEAD_R);
   const int nb = (int)(a.num_scenes * a.chunks_per_scene);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (pcs_head_stream_class(a)) return pcs_head_stream_launch(a, rpc, s);
   if (a.num_classes <= 4) {
 #define PCS_HS(T, CC, MODE) \
   hipLaunchKernelGGL((head_small_kernel<T, CC, MODE>), dim3(nb), dim3(THREADS), 0, s, a, rpc)
