@@ -348,6 +348,11 @@ int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weigh
  * keep = u >= p, 8 bits per byte along the channel dimension; bits[M, C/8]. */
 int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
                      uint8_t *bits, pcs_stream_t stream);
+/* The same bits from at most max_workgroups 256-thread workgroups (<= 0: as many as the words
+ * need), striding over the words: a draw that shares the GPU with a register-heavy kernel
+ * (the training step draws beside the Gram of a5) occupies few wave slots for longer. */
+int pcs_dropout_bits_bounded(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                             uint8_t *bits, int32_t max_workgroups, pcs_stream_t stream);
 
 /*
  * Gram of the BN+ReLU activations a = relu(Y * s + t) (Y [M, C] scene-major rows), or of Y

@@ -1016,9 +1016,10 @@ PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
 __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbytes, uint32_t thr,
                                     uint8_t *bits) {
   // byte j covers elements 8j..8j+7; one Philox call gives 8 16-bit uniforms.  A thread makes
-  // 4 consecutive bytes and stores them as one word (byte stores are issue-bound).
-  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (j0 >= nbytes) return;
+  // 4 consecutive bytes and stores them as one word (byte stores are issue-bound); a grid smaller
+  // than the words (pcs_dropout_bits_bounded) strides over them: the bits depend on j only
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; j0 < nbytes; j0 += stride) {
   uint32_t word = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -1038,6 +1039,7 @@ __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbyt
     *reinterpret_cast<uint32_t *>(bits + j0) = word;
   } else {
     for (int q = 0; q < 4 && j0 + q < nbytes; ++q) bits[j0 + q] = (uint8_t)(word >> (8 * q));
+  }
   }
 }
 
@@ -1370,15 +1372,23 @@ extern "C" int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *
   return 0;
 }
 
-extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
-                                uint8_t *bits, pcs_stream_t stream) {
+extern "C" int pcs_dropout_bits_bounded(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                                        uint8_t *bits, int32_t max_workgroups, pcs_stream_t stream) {
   if (!bits || C % 8 != 0 || p < 0.f || p >= 1.f) return pcs_set_einval("pcs_dropout_bits", "bad arguments");
   const int64_t nbytes = M * (C / 8);
+  if (nbytes <= 0) return 0;
   const uint32_t thr = (uint32_t)(p * 65536.0f + 0.5f);
-  hipLaunchKernelGGL(dropout_bits_kernel, dim3(blocks_for((nbytes + 3) / 4, 256)), dim3(256), 0,
+  int64_t nb = blocks_for((nbytes + 3) / 4, 256);
+  if (max_workgroups > 0 && nb > max_workgroups) nb = max_workgroups;
+  hipLaunchKernelGGL(dropout_bits_kernel, dim3((unsigned)nb), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), seed, offset, nbytes, thr, bits);
   PCS_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                                uint8_t *bits, pcs_stream_t stream) {
+  return pcs_dropout_bits_bounded(seed, offset, M, C, p, bits, 0, stream);
 }
 
 namespace {

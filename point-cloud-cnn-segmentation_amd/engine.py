@@ -347,23 +347,29 @@ class Engine:
         sv = Saved(B=B, N=N, train=train) if saved is None else saved
         sv.B, sv.N, sv.train, sv.x = B, N, train, x
         sv.gram4 = None   # (a reused Saved must not carry the previous pass's Gram)
-        if train and masks is None:
-            # Philox keep bits (ALU-bound, no data dependence) drawn on a side stream while the
-            # trunk's kernels run; the stream waits for everything enqueued before (the buffers
-            # may reuse memory the previous kernels still read) and seg_conv2 waits for it
+        def draw_masks(max_wg=0):
+            # Philox keep bits (ALU-bound, no data dependence) drawn on a side stream beside the
+            # trunk's kernels; the stream waits for everything enqueued before (the buffers may
+            # reuse memory the previous kernels still read) and seg_conv2 waits for it
             m1 = torch.empty(M, 64, dtype=torch.uint8, device=dev)
             m2 = torch.empty(M, 32, dtype=torch.uint8, device=dev)
             side = self._side_stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 ss = L.stream_ptr()
-                L.call("pcs_dropout_bits", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), ss)
-                L.call("pcs_dropout_bits", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), ss)
+                L.call("pcs_dropout_bits_bounded", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), max_wg, ss)
+                L.call("pcs_dropout_bits_bounded", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), max_wg, ss)
                 sv.mask_ready = torch.cuda.Event()
                 sv.mask_ready.record(side)
             m1.record_stream(side)
             m2.record_stream(side)
             sv.mask_bufs = (m1, m2)
+        # bf16 (stored-a5 Gram): draw beside the Gram of a5, MFMA-bound at 214 VGPRs x 2 waves per
+        # SIMD, with two 256-thread workgroups per CU (24 VGPRs a wave: they fit beside it and use
+        # its idle VALU issue); otherwise at the start of the forward with a full grid
+        draw_beside_gram = train and masks is None and self._raw_gram() and not self.fp8
+        if train and masks is None and not draw_beside_gram:
+            draw_masks()
         sv.wc = wc = self.cast_weights(P)
         T = self.tdt
 
@@ -453,6 +459,8 @@ class Engine:
             if nbytes < 0:
                 raise L.PcsError(L.load().pcs_last_error().decode())
             gws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            if draw_beside_gram:
+                draw_masks(2 * torch.cuda.get_device_properties(dev).multi_processor_count)
             self._launch("wgrad:global_feat", "pcs_gram_raw", L.ptr(a5), M, 1024, self.a5_dt, L.ptr(gws), nbytes,
                          L.ptr(G5), s)
             # per-scene column sums of a5 from conv5's per-chunk partials (chunks are scene-aligned)

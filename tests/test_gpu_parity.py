@@ -198,6 +198,11 @@ def test_dropout_bits_statistics_and_determinism():
     assert torch.equal(a, b) and not torch.equal(a, c)
     # channels are independent: per-channel keep rates all near 0.7
     assert np.abs(bits.mean(0) - 0.7).max() < 0.02
+    # a bounded grid (words strided over few workgroups) draws the same bits, ragged tail included
+    for wg in (1, 7, 512):
+        d = torch.zeros(M - 3, C // 8, dtype=torch.uint8, device=DEV)
+        L.call("pcs_dropout_bits_bounded", 123, 0, M - 3, C, 0.3, L.ptr(d), wg, L.stream_ptr())
+        assert torch.equal(d, a[:M - 3])
 
 
 def test_train_mode_random_dropout_runs_and_differs():
