@@ -32,7 +32,8 @@ constexpr int WAVEB = YW + WR * 8;     // + 64 B of labels
 #define HS_SB 0
 #endif
 #ifndef HS_WPS
-#define HS_WPS 4   // waves per SIMD requested: two workgroups per CU, at most 128 VGPRs (no spills)
+#define HS_WPS 4   // waves per SIMD requested for C <= 2: two workgroups per CU, at most 128 VGPRs
+                   // (no spills; C = 3, 4 would spill 60-70 registers there and keep one per CU)
 #endif
 constexpr int NST = HS_NST;
 constexpr int BYTES = 8 * NST * WAVEB;
@@ -64,7 +65,7 @@ template <int N> PCS_DEV void wait_vm() {
 }
 
 template <int C>
-__global__ __launch_bounds__(THREADS, HS_WPS) void head_stream_kernel(pcs_head_args a, int64_t rows_per_chunk) {
+__global__ __launch_bounds__(THREADS, (C <= 2 ? HS_WPS : 1)) void head_stream_kernel(pcs_head_args a, int64_t rows_per_chunk) {
   __shared__ __attribute__((aligned(16))) char lds[BYTES];
   __shared__ float red[THREADS];
   const int tid = threadIdx.x, lane = tid & 63;
