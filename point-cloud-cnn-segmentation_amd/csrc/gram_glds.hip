@@ -31,6 +31,10 @@
 //   the Gram of the stored activation, as in bf16.
 #include "common.h"
 
+#ifndef GG_PRIO
+#define GG_PRIO 1   // base wave priority: above the dropout draw that shares its CUs (step -0.36 ms)
+#endif
+
 namespace {
 
 constexpr int THREADS = 512;
@@ -264,9 +268,9 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const void *__restri
     if (qs + 1 < total) wait_vm<10>(); else wait_vm<2>();      // retires B-hi(qs)
     wait_lgkm0();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1 + GG_PRIO);
     mfma_quad(0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(GG_PRIO);
     barrier_raw();
     // phase 2: (lo, hi); restage A-lo of step qs+2
     read_b(buf, 1, 2);
@@ -274,26 +278,26 @@ __global__ __launch_bounds__(THREADS) void gram_glds_kernel(const void *__restri
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<8>(); else wait_vm<0>();   // A-hi(qs)
     wait_lgkm0();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1 + GG_PRIO);
     mfma_quad(0, 2);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(GG_PRIO);
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of step qs+2
     read_a(buf, 1);
     issue(qs + 2, 2);
     wait_lgkm0();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1 + GG_PRIO);
     mfma_quad(4, 0);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(GG_PRIO);
     barrier_raw();
     // phase 4: (hi, hi); restage B-hi of step qs+2
     issue(qs + 2, 3);
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();   // A-lo, B-lo(qs+1)
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1 + GG_PRIO);
     mfma_quad(4, 2);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(GG_PRIO);
     barrier_raw();
 
   }
