@@ -33,7 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import pcs_amd  # noqa: E402
-from pcs_amd.data import class_weights, synthetic_batch  # noqa: E402
+from pcs_amd.data import class_weights_from_counts, label_counts, synthetic_batch  # noqa: E402
 from pcs_amd.model import PointNetSegmentation  # noqa: E402
 from pcs_amd.optim import FusedAdam  # noqa: E402
 from pcs_amd.train import FusedTrainStep  # noqa: E402
@@ -231,8 +231,11 @@ def cpu_baseline(max_seconds=10.0):
         torch.set_num_threads(prev)
     masks = orc.dropout_masks(3, B * N)
     nsteps, nel = timed(lambda: orc.train_step(sd, pts, lab, w, masks=masks, dtype=np.float32))
+    note = ("torch threads = the affinity count" if threads == aff else
+            f"torch threads capped at OMP_NUM_THREADS={threads}: the GPU box sets it to its CPU share "
+            f"per GPU; the affinity mask lists all {aff} host cores, which the other GPUs' jobs share")
     return {"value": B * N * steps / el / 1e6, "unit": "M points/s", "cores": int(threads),
-            "kind": "port", "affinity_cores": int(aff), "torch_threads": int(threads),
+            "kind": "port", "affinity_cores": int(aff), "torch_threads": int(threads), "threads_note": note,
             "sample": f"pure-PyTorch CPU restatement of the reference step (oracle/torch_cpu.py: "
                       f"ATen conv1d / batch_norm / dropout / cross_entropy + autograd, fp32, train "
                       f"mode, dropout on), B=4 x N=4096 (32^3 lattice), C=2, {steps} steps in "
@@ -240,6 +243,21 @@ def cpu_baseline(max_seconds=10.0):
             "numpy": {"value": B * N * nsteps / nel / 1e6, "unit": "M points/s",
                       "blas_threads": blas,
                       "sample": f"numpy fp32 oracle fwd+CE+bwd, same batch, {nsteps} steps in {nel:.1f}s"}}
+
+
+def shared_class_weights(label_arrays, num_classes, world):
+    """One class-weight vector for every rank (P:168-189, P:216: the reference builds a single
+    weight tensor from the labels it scans): the per-class counts of this rank's scenes are
+    summed over the process group, so every rank derives the weights of the global batch (the
+    concatenation of all ranks' scenes), not of its own shard."""
+    counts = label_counts(label_arrays, num_classes)
+    if world > 1:
+        t = torch.from_numpy(counts)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t)
+        counts = t.cpu().numpy()
+    return class_weights_from_counts(counts, num_classes)
 
 
 def launch_ranks(n):
@@ -318,7 +336,7 @@ def main():
         from pcs_amd.loader import global_max_points, pad_on_device
         G = 256 if args.grid == 128 else args.grid
         clouds = occupied_clouds(1234 + rank, B, grid=G, occupancy=args.occupancy, num_classes=C)
-        w = class_weights([l for _, l in clouds], num_classes=C)
+        w = shared_class_weights([l for _, l in clouds], C, world)
         rb = ragged_collate([(torch.from_numpy(p), torch.from_numpy(l)) for p, l in clouds], torch.int32)
         N = global_max_points(rb.max_points, None, dev)
         real_points = int(rb.offsets[-1])
@@ -327,7 +345,7 @@ def main():
     else:
         N = G ** 3
         pts, lab, _ = synthetic_batch(1234 + rank, [N] * B, C, grid=G, dense=True)
-        w = class_weights([lab[b] for b in range(B)], num_classes=C)
+        w = shared_class_weights([lab[b] for b in range(B)], C, world)
         x = torch.from_numpy(pts).to(dev)
         y = torch.from_numpy(lab).to(dev)
         real_points = B * N

@@ -41,10 +41,13 @@ enum {
                            kernel runs v_mfma_scale_f32_16x16x128_f8f6f4 (K % 256 == 0; RAW
                            prologue; FWD statistics / pool or DGRAD)                         */
   PCS_FLAG_C_FP8 = 8,   /* EPI_BNRELU of the bf16 256-wide kernel stores C as fp8 e4m3      */
-  PCS_FLAG_POOL_SIGNED_W = 16 /* FWD max-pool on the LDS-DMA kernel: the caller has multiplied
+  PCS_FLAG_POOL_SIGNED_W = 16, /* FWD max-pool on the LDS-DMA kernel: the caller has multiplied
                            W's rows (pcs_sign_rows) and bias by sign(es), so the pool keeps the
                            plain column max of acc (no multiply); es still names the sign.
                            Needs pool and es, no statistics (they would be of the signed y)  */
+  PCS_FLAG_GLDS8 = 32   /* bf16 global_feat GEMMs: the 8-wave 16x16x32 LDS-DMA kernel
+                           (gemm_glds.hip) instead of the 4-wave 32x32x16 one (gemm_w4.hip),
+                           for A/B timing and cross-checks                                   */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
@@ -130,6 +133,10 @@ typedef struct {
  * kernel (and so the row tile: 256 for the bf16 wide-layer kernel, 128 otherwise) is chosen
  * from dtype, K, Ncols and flags, so call it with the same values as pcs_gemm. */
 int64_t pcs_gemm_geometry(pcs_gemm_args *args);
+/* 1 when pcs_gemm would run these arguments on the four-wave 32x32x16 LDS-DMA kernel
+ * (csrc/gemm_w4.hip: bf16 global_feat forward max-pool on sign-folded W rows, or the folded
+ * input gradient without statistics), 0 otherwise.  No GPU work. */
+int pcs_gemm_w4_selected(const pcs_gemm_args *args);
 /* Launch the GEMM. */
 int pcs_gemm(const pcs_gemm_args *args, pcs_stream_t stream);
 /* conv1 (Cin = K = input_dim, 1..8; the reference's points carry 4, P:70, P:106) forward:
@@ -161,6 +168,10 @@ typedef struct {
   float *dW;            /* [Cout, Cin] f32 output, row stride ldw */
   int64_t ldw;          /* 0 = Cin */
   int32_t flags;        /* PCS_FLAG_GENERIC: never use the 256x256 wide-layer kernel */
+  float *dy_colsum;     /* [Cout] f32 or NULL: sum_m dy[m, n] (RAW dy, conv5's R pass only:
+                           bn5's S1 = the column sums of dz5 as stored, one ones-fragment MFMA
+                           per dz5 fragment beside R's; the workspace grows by one Cout row per
+                           slice).  Other kernels refuse it. */
 } pcs_wgrad_args;
 
 int64_t pcs_wgrad_workspace(pcs_wgrad_args *args); /* bytes; fills splits_per_scene */
@@ -617,13 +628,16 @@ int pcs_conv3d_weight_t(const void *W, int32_t Cout, int32_t taps, int32_t Cin, 
  * pcs_voxel_hash_*: open-addressing table, capacity a power of two >= 2 n
  *   (pcs_voxel_hash_capacity); table_keys u64 [cap], table_vals i32 [cap] (row of the key);
  *   find: out[i] = row of queries[i] or -1.
+ *   Keys must be unique and below 2^64 - 1 (the EMPTY sentinel): a duplicate key keeps
+ *   whichever row its insert wins, so pcs_amd.sparse.sparse_from_keys checks uniqueness.
  * pcs_sparse_neighbors: nbr [n][27] i32, nbr[v][t] = row of the voxel at (ix + a - 1, iy + b - 1,
  *   iz + c - 1), t = (a * 3 + b) * 3 + c, same scene, or -1 (the tap order of a torch Conv3d
  *   weight [Cout, Cin, 3, 3, 3] on a dense [B, C, G(x), G(y), G(z)] grid).
  * pcs_sparse_conv: submanifold convolution Y[m] = b + sum_t W[tw(t)] X[nbr[m][t]] over the M rows
  *   (X rows addressed by nbr), tw(t) = flip ? taps - 1 - t : t; X bf16 [*, Cin], W bf16
  *   [Cout][taps][Cin], Y [M, Cout] in ydtype; Cin % 32 == 0, Cout % 64 == 0.  The input gradient
- *   is the same call on dY with pcs_conv3d_weight_t(W) and flip = 1.  A 64-row tile runs only the
+ *   is the same call on dY with pcs_conv3d_weight_t(W) and flip = 1 (flip needs taps == 27, the
+ *   centred neighbour map, or taps == 1).  A 64-row tile runs only the
  *   taps one of its rows has a neighbour at.
  * pcs_sparse_conv_wgrad: dW [Cout][taps][Cin] f32 = sum_m dY[m] (x) X[nbr[m][t]], db [Cout] (may be
  *   NULL); Cin, Cout % 64 == 0; fixed-order partial sums (deterministic).

@@ -47,6 +47,7 @@ FLAG_NO_GLDS = 2
 FLAG_AW_FP8 = 4
 FLAG_C_FP8 = 8
 FLAG_POOL_SIGNED_W = 16
+FLAG_GLDS8 = 32
 
 
 class WgradArgs(ct.Structure):
@@ -58,7 +59,7 @@ class WgradArgs(ct.Structure):
         ("pool_idx", _vp), ("pool_coef", _vp),
         ("x_mode", _i32),
         ("X", _vp), ("s", _vp), ("t", _vp), ("x_mask", _vp), ("x_keep_scale", _f),
-        ("partial", _vp), ("dW", _vp), ("ldw", _i64), ("flags", _i32),
+        ("partial", _vp), ("dW", _vp), ("ldw", _i64), ("flags", _i32), ("dy_colsum", _vp),
     ]
 
 
@@ -100,6 +101,7 @@ class HeadArgs(ct.Structure):
 # (name, restype, argtypes) of every exported symbol declared in include/pcs.h
 SIGNATURES = [
     ("pcs_gemm_geometry", _i64, [ct.POINTER(GemmArgs)]),
+    ("pcs_gemm_w4_selected", ct.c_int, [ct.POINTER(GemmArgs)]),
     ("pcs_gemm", ct.c_int, [ct.POINTER(GemmArgs), _vp]),
     ("pcs_conv1_fwd", ct.c_int, [ct.POINTER(GemmArgs), _vp]),
     ("pcs_wgrad_workspace", _i64, [ct.POINTER(WgradArgs)]),

@@ -1086,6 +1086,10 @@ extern "C" int pcs_sparse_conv(const int32_t *nbr, int64_t M, int32_t taps, cons
   if (!nbr || !X || !W || !Y || M < 0 || taps < 1 || taps > 27 || Cin <= 0 || Cout <= 0 || Cin % KS != 0 ||
       Cout % BN != 0 || (ydtype != PCS_F32 && ydtype != PCS_BF16))
     return pcs_set_einval("pcs_sparse_conv", "bad arguments (1 <= taps <= 27, Cin % 32 == 0, Cout % 64 == 0, Y f32 | bf16)");
+  // flip = 1 reads tap taps - 1 - t for tap t: the input gradient's offset(taps - 1 - t) = -offset(t)
+  // holds only for the full centred 27-tap map (or the single centre tap)
+  if (flip != 0 && taps != 27 && taps != 1)
+    return pcs_set_einval("pcs_sparse_conv", "flip needs the centred 27-tap neighbour map (or taps == 1)");
   if (M == 0) return 0;
   const int64_t tiles = (M + 63) / 64;
   if (tiles > 0x7fffffff) return pcs_set_einval("pcs_sparse_conv", "too many rows");

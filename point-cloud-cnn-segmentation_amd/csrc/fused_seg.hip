@@ -25,16 +25,13 @@
 //   buffer) by all 512 threads, each element once; the input gradient of step t from the
 //   registers' W^T block (loaded once) and dy fragments; the weight gradient of step t from
 //   transposed reads (ds_read_b64_tr_b16) of dy and x; then the epilogue in registers (mask,
-//   S1 / S2, 16-B stores widened with v_permlane16_swap).  One barrier per step (SEG_1B: the
-//   wait for step t+1 and the barrier at the top of step t, the DMA after it; the two-barrier
-//   form, with the wait between the phases, is kept behind SEG_1B=0).
+//   S1 / S2, 16-B stores widened with v_permlane16_swap).  One barrier per step: the wait for
+//   step t+1 and the barrier at the top of step t, the DMA after it (a two-barrier form, with
+//   the wait between the phases, measured 0.05-0.1 ms slower and was removed).
 // * dW partial per workgroup (fp32, the slice's slab) and per-slice S1 / S2, reduced by the
 //   caller's pcs_reduce_partials as pcs_dgrad_wgrad_bn's other shapes.
 #include "common.h"
 
-#ifndef SEG_1B
-#define SEG_1B 1   // one barrier per step (the wait for step t+1 at the top): 8.48 -> 8.38 ms, 3.15 -> 3.10 ms
-#endif
 
 namespace {
 
@@ -395,12 +392,10 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
   uint32_t o_out = o_st;                 // this lane's store offset at step t
   for (int t = 0; t < nsteps; ++t) {
     const int rem = (int)pcs_min64(hi - (lo + (int64_t)t * MS), MS);
-#if SEG_1B
     // one barrier per step: step t+1 landed (newer: the stores and DMAs of the NST-3 steps in
     // between, and step t-1's store), visible to every wave; every wave done with step t-1
     wait_vm<1 + (F::NST - 3) * (F::VM_STEP + 1)>();
     barrier_lds();
-#endif
     dma_step(t + F::NST - 1, sd);   // into the stage step t-1 used (free since the last barrier)
     const char *st = lds + sc * F::STAGE;
     const char *xb = lds + F::OFF_X + (t & 1) * F::XB;
@@ -475,12 +470,6 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
       store_rows(o_out, mk_u32x4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]));
       o_out += MS * CIN * 2;
     }
-#if !SEG_1B
-    // step t+1 landed: every older DMA done (the newer: the store above, step t+NST-1's
-    // pieces, and the NST-2 steps' loads + stores in between)
-    wait_vm<1 + (F::NST - 2) * (F::VM_STEP + 1)>();
-    barrier_lds();
-#endif
     // phase 2: weight gradient dW[o = 16 (OBW wid + ob) + l16][c = 16 u + 4 g + r] over the 32
     // rows of step t, with the transform of step t+1 between its MFMA groups
     {
@@ -503,9 +492,6 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
         }
       }
     }
-#if !SEG_1B
-    barrier_lds();
-#endif
     sd = sc;
     sc = sn;
     sn = sn + 1 == F::NST ? 0 : sn + 1;
@@ -543,9 +529,16 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
 
 // Shapes served: (Cout, Cin) = K x Ncols in {256 x 512 (seg_conv2), 128 x 256 (seg_conv3)}, bf16,
 // PRO_BWD / EPI_DGRAD with dropout bits and no addend.
+int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a);
 bool pcs_seg_bwd_applicable(const pcs_gemm_args &a) {
-  return a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && !a.addend &&
-         ((a.K == 256 && a.Ncols == 512) || (a.K == 128 && a.Ncols == 256));
+  if (!(a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && !a.addend &&
+        ((a.K == 256 && a.Ncols == 512) || (a.K == 128 && a.Ncols == 256))))
+    return false;
+  // the buffer-store ranges and per-lane row offsets are 32-bit: a slice of the widest rows
+  // (Ncols bf16) must stay below 2 GB, else the generic kernels run it
+  pcs_gemm_args g = a;
+  const int64_t rps = pcs_seg_bwd_geometry(&g);
+  return rps * (int64_t)a.Ncols * 2 < ((int64_t)1 << 31);
 }
 
 int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a) {

@@ -636,6 +636,10 @@ bool pcs_fwd_stream_applicable(const pcs_gemm_args &a) {
   if (!pcs_fwd_stream_nb(a, nullptr) || !a.C || !a.pa || !a.pb || a.pool) return false;
   if ((a.flags & PCS_FLAG_C_FP8) && a.epilogue != PCS_EPI_BNRELU) return false;
   if (a.scene_rows * a.num_scenes >= ((int64_t)1 << 31)) return false;
+  // 32-bit store ranges / row offsets: a chunk of the widest rows must stay below 2 GB
+  const int64_t rpc = a.chunks_per_scene > 0 ? (a.scene_rows + a.chunks_per_scene - 1) / a.chunks_per_scene
+                                             : a.scene_rows;
+  if (rpc * (int64_t)(a.K > a.Ncols ? a.K : a.Ncols) * 2 >= ((int64_t)1 << 31)) return false;
   if (a.epilogue == PCS_EPI_BNRELU) return a.es && a.et && !a.a_mask && !a.scene_bias;
   // dropout bits only where the layer has them (seg_conv2 / seg_conv3 inputs)
   if (a.a_mask && !(FsShape<512, 256>::is(a) || FsShape<256, 128>::is(a))) return false;

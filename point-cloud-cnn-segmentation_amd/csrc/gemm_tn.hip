@@ -346,7 +346,8 @@ extern "C" int64_t pcs_wgrad_workspace(pcs_wgrad_args *a) {
     if (sps < 1) sps = 1;
     a->splits_per_scene = (int32_t)sps;
   }
-  return (int64_t)a->num_scenes * a->splits_per_scene * a->Cout * a->Cin * 4;
+  const int64_t nslabs = (int64_t)a->num_scenes * a->splits_per_scene;
+  return nslabs * a->Cout * a->Cin * 4 + (a->dy_colsum ? nslabs * a->Cout * 4 : 0);
 }
 
 extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
@@ -360,6 +361,8 @@ extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   if (a.dy_mode == PCS_PRO_BWD_POOL && (!a.pool_idx || !a.pool_coef))
     return pcs_set_einval("pcs_wgrad", "PRO_BWD_POOL needs pool_idx, pool_coef");
   if (a.x_mode == PCS_PRO_BNRELU && (!a.s || !a.t)) return pcs_set_einval("pcs_wgrad", "x BNRELU needs s, t");
+  if (a.dy_colsum && !pcs_wgrad_c5_applicable(a))
+    return pcs_set_einval("pcs_wgrad", "dy_colsum: conv5's R pass only (bf16, RAW dZ, BNRELU x, Cin 128)");
   if (pcs_wgrad_workspace(&a) < 0) return PCS_EINVAL;
   const int ms = a.dtype == PCS_BF16 ? TnCfg<bf16_t>::MS : TnCfg<float>::MS;
   const int64_t rps = rows_per_split_of(a, ms);
@@ -372,6 +375,11 @@ extern "C" int pcs_wgrad(const pcs_wgrad_args *ap, pcs_stream_t stream) {
   else return pcs_set_einval("pcs_wgrad", "bad dtype");
   if (rc) return rc;
   const int64_t nslabs = a.num_scenes * a.splits_per_scene;
+  if (a.dy_colsum) {
+    rc = pcs_reduce_partials(a.partial + nslabs * a.Cout * a.Cin, nslabs, a.Cout, 1.0f, a.dy_colsum, a.Cout, a.Cout,
+                             stream);
+    if (rc) return rc;
+  }
   return pcs_reduce_partials(a.partial, nslabs, (int64_t)a.Cout * a.Cin, 1.0f, a.dW,
                              a.ldw ? a.ldw : a.Cin, a.Cin, stream);
 }

@@ -28,9 +28,6 @@ constexpr int WAVEB = YW + WR * 8;     // + 64 B of labels
 #ifndef HS_NST
 #define HS_NST 4
 #endif
-#ifndef HS_SB
-#define HS_SB 0
-#endif
 #ifndef HS_WPS
 #define HS_WPS 4   // waves per SIMD requested for C <= 2: two workgroups per CU, at most 128 VGPRs
                    // (no spills; C = 3, 4 would spill 60-70 registers there and keep one per CU)
@@ -153,9 +150,6 @@ __global__ __launch_bounds__(THREADS, (C <= 2 ? HS_WPS : 1)) void head_stream_ke
     const int64_t rbase = (int64_t)it * MS + WR * wid;   // chunk-relative row of the wave's first
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-#if HS_SB
-      __builtin_amdgcn_sched_barrier(0);   // one row pass at a time (live ranges)
-#endif
       const int rr = 4 * h + rq;
       const int64_t rrel = rbase + rr;
       const bool ok = lo + rrel < hi;
@@ -263,9 +257,6 @@ __global__ __launch_bounds__(THREADS, (C <= 2 ? HS_WPS : 1)) void head_stream_ke
 
 // bf16, CE mode, C <= 4, no logits out (the fused train step); shapes / modes only
 bool pcs_head_stream_class(const pcs_head_args &a) {
-#ifdef HS_OFF
-  return false;
-#endif
   return a.dtype == PCS_BF16 && a.mode == PCS_HEAD_CE && a.num_classes >= 1 && a.num_classes <= 4 &&
          !a.logits && a.Cin == CIN && a.num_scenes * a.scene_rows < ((int64_t)1 << 31);
 }

@@ -801,9 +801,6 @@ __global__ __launch_bounds__(THREADS) void head_wide_kernel(pcs_head_args a, int
 #ifndef HEAD_BATCH
 #define HEAD_BATCH 4
 #endif
-#ifndef HEAD_SB
-#define HEAD_SB 0
-#endif
 // Register-resident head for C <= 4 classes: 16 threads per point (one 8-channel bf16 /
 // 4-channel fp32 chunk each; 2 chunks per thread for fp32), logits all-reduced across
 // those 16 lanes by shuffles, seg_conv4 weights, dW/db partials and bn_seg3 S1/S2 kept
@@ -858,9 +855,6 @@ __global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, in
     }
 #pragma unroll
     for (int q = 0; q < BATCH; ++q) {
-#if HEAD_SB
-      __builtin_amdgcn_sched_barrier(0);   // one row at a time (no interleaved live ranges)
-#endif
       const int64_t r = rb + r0 + RPP * q;
       const bool ok = r < hi;
       const int64_t row = scene * N + (ok ? r : hi - 1);

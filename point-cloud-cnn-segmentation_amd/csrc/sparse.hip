@@ -135,6 +135,9 @@ extern "C" int pcs_voxel_keys(const float *points, const int64_t *offsets, int64
   if (!points || !offsets || !voxel_of_point || !keys || num_scenes < 1 || T < 0 || grid < 1 || grid > (1 << 20) ||
       !(hi_x > lo_x && hi_y > lo_y && hi_z > lo_z))
     return pcs_set_einval("pcs_voxel_keys", "bad arguments");
+  // keys are scene * G^3 + voxel: they must stay below the hash table's EMPTY sentinel (2^64 - 1)
+  if ((double)grid * grid * grid * (double)num_scenes >= 18446744073709551615.0)
+    return pcs_set_einval("pcs_voxel_keys", "key overflow (num_scenes * grid^3 >= 2^64 - 1)");
   if (T == 0) return 0;
   const Box b = {{lo_x, lo_y, lo_z}, {hi_x, hi_y, hi_z}};
   hipLaunchKernelGGL(voxel_keys_kernel, dim3(blocks_for_n(T)), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),

@@ -154,6 +154,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
     }
   };
 
+  const bool do_s1 = a.dy_colsum != nullptr;
   // x = relu(bn4(y4)) of step s into x buffer s & 1; rows past the slice -> 0
   const int o_yx = DZB + xrr * YROW + ((xlc ^ (xrr & 15)) << 4);
   const int o_xw = prow(xrr) * XR + xlc * 16;
@@ -166,6 +167,13 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
     u32x4 out = pack_chunk(v);
     if (xrr >= rem) out = mk_u32x4(0, 0, 0, 0);
     *reinterpret_cast<u32x4 *>(lds + OFF_X + (s & 1) * XB + o_xw) = out;
+    // S1 (dy_colsum): a 17th 16-channel block of ones in the row's pad, zero past the slice,
+    // so that the same transposed read gives the ones fragment with R's row (k) order
+    if (do_s1 && xlc < 2) {
+      const uint32_t one = xrr < rem ? 0x3f803f80u : 0u;
+      *reinterpret_cast<u32x4 *>(lds + OFF_X + (s & 1) * XB + prow(xrr) * XR + CIN * 2 + xlc * 16) =
+          mk_u32x4(one, one, one, one);
+    }
   };
 
   // transposed-read offsets (fused_seg.hip's weight-gradient half): dz5 columns 16 (2 wid + ob) +
@@ -181,11 +189,13 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
   }
   const int o_tx0 = prow(tr0) * XR + 8 * p, o_tx1 = prow(tr1) * XR + 8 * p;   // + u 32 B
 
-  f32x4 acc[OBW][8];
+  f32x4 acc[OBW][8], acc1[OBW];   // acc1: S1 (every row of the 16 x 16 block is the column sum)
 #pragma unroll
-  for (int ob = 0; ob < OBW; ++ob)
+  for (int ob = 0; ob < OBW; ++ob) {
+    acc1[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc[ob][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   // ---- prologue: steps 0 .. NST-2 in flight, step 0 landed and transformed
 #pragma unroll
@@ -212,6 +222,11 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
       for (int ob = 0; ob < OBW; ++ob)
         acc[ob][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u & 1], dt[ob], acc[ob][u], 0, 0, 0);
     }
+    if (do_s1) {   // uniform
+      const bf16x8 of = tr_frag2(xb + o_tx0 + 8 * 32, xb + o_tx1 + 8 * 32);
+#pragma unroll
+      for (int ob = 0; ob < OBW; ++ob) acc1[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, dt[ob], acc1[ob], 0, 0, 0);
+    }
     // step t+1 landed (newer: NST-2 steps' pieces)
     wait_vm<(NST - 2) * LPS>();
     barrier_lds();
@@ -221,6 +236,13 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
   }
   wait_vm<0>();   // the clamped DMAs past the end
 
+  // ---- this slice's S1 partial (after all slices' R partials): lanes of row group g = 0
+  if (do_s1 && g == 0) {
+    const int64_t nsl = (int64_t)gridDim.x / ncb;
+    float *o1 = a.partial + nsl * Cout * CIN + (int64_t)split * Cout + n0;
+#pragma unroll
+    for (int ob = 0; ob < OBW; ++ob) o1[16 * (OBW * wid + ob) + l16] = acc1[ob][0];
+  }
   // ---- this slice's partial: R[n0 + 16 (OBW wid + ob) + l16][16 u + 4 g .. + 4]
   float *out = a.partial + ((int64_t)split * Cout + n0) * CIN;
 #pragma unroll
@@ -242,9 +264,6 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
 constexpr int G_MS = 64;                  // rows per step
 #ifndef GRAM_NST
 #define GRAM_NST 4
-#endif
-#ifndef GRAM_SYM
-#define GRAM_SYM 1
 #endif
 #ifndef GRAM_TARGET
 #define GRAM_TARGET 512
@@ -335,19 +354,14 @@ __global__ __launch_bounds__(THREADS) void gram128_kernel(pcs_wgrad_args a, int6
   const int g = lane >> 4, l16 = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
   const int tr0 = 8 * g + q, tr1 = 8 * g + 4 + q;
   auto o_frag = [&](int u, int row) { return row * YROW + (((2 * u + (p >> 1)) ^ ftr(row)) << 4) + 8 * (p & 1); };
-#if GRAM_SYM
   // symmetric: wave w forms the 16-wide blocks (w, w + d mod 8), d = 0 .. 3 (and d = 4 for w < 4):
   // the 36 blocks of one triangle; the partial gets each block and its transpose
   constexpr int NU = 5;
   const int nu = wid < 4 ? 5 : 4;
-#else
-  constexpr int NU = 8;
-  const int nu = 8;
-#endif
   int o_u[NU][2];
 #pragma unroll
   for (int d = 0; d < NU; ++d) {
-    const int u = GRAM_SYM ? (wid + d) & 7 : d;
+    const int u = (wid + d) & 7;
     o_u[d][0] = o_frag(u, tr0);
     o_u[d][1] = o_frag(u, tr1);
   }
@@ -386,10 +400,10 @@ __global__ __launch_bounds__(THREADS) void gram128_kernel(pcs_wgrad_args a, int6
 #pragma unroll
   for (int d = 0; d < NU; ++d) {
     if (d >= nu) continue;
-    const int u = GRAM_SYM ? (wid + d) & 7 : d;
+    const int u = (wid + d) & 7;
     *reinterpret_cast<float4 *>(out + (int64_t)(16 * wid + l16) * CIN + 16 * u + 4 * g) =
         make_float4(acc[d][0], acc[d][1], acc[d][2], acc[d][3]);
-    if (GRAM_SYM && d > 0) {   // the transposed block
+    if (d > 0) {   // the transposed block
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[(int64_t)(16 * u + 4 * g + r) * CIN + 16 * wid + l16] = acc[d][r];
     }

@@ -58,6 +58,14 @@ def class_weights(labels_iterable, num_classes=None):
     counts = Counter(all_labels)
     if num_classes is None:
         num_classes = len(set(all_labels))
+    return class_weights_from_counts(counts, num_classes)
+
+
+def class_weights_from_counts(counts, num_classes):
+    """The P:168-183 formula from per-label counts (a mapping label -> count, or a sequence
+    indexed by label; labels with a zero count are absent, as in the reference's Counter)."""
+    if not hasattr(counts, "items"):
+        counts = {c: int(v) for c, v in enumerate(counts) if int(v) > 0}
     max_count = max(counts.values())
     w = []
     for c in range(num_classes):
@@ -70,6 +78,16 @@ def class_weights(labels_iterable, num_classes=None):
             w.append(1.0)
     s = sum(w)
     return [v * num_classes / s for v in w]
+
+
+def label_counts(labels_iterable, num_classes):
+    """Per-class counts (int64 [num_classes]) of the labels 0..num_classes-1 (pads, -1, skipped)."""
+    out = np.zeros(num_classes, dtype=np.int64)
+    for lab in labels_iterable:
+        a = np.asarray(lab).reshape(-1)
+        a = a[(a >= 0) & (a < num_classes)]
+        out += np.bincount(a.astype(np.int64), minlength=num_classes)[:num_classes]
+    return out
 
 
 def _scene(rng, grid, n_points, num_classes, dense):

@@ -177,6 +177,14 @@ class Engine:
         self.flags = 0       # L.FLAG_GENERIC forces the generic GEMM (cross-checks)
         self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
         self.timing_tags = None   # set of tags to bracket (None = every tagged launch)
+        # test hooks for the global max-pool's rows (P:114): record_pool_rows keeps a copy of
+        # the argmax rows [B, 1024] of the last forward in last_pool_rows; pool_rows_override
+        # (int32 [B, 1024] global rows) replaces them before the backward routes the pooled
+        # gradient, so a bf16 step can be compared with the fp32 step through the same rows
+        # (tests/test_gpu_fullsize.py).  Never set on the product path.
+        self.record_pool_rows = False
+        self.last_pool_rows = None
+        self.pool_rows_override = None
         L.load()
 
     def _launch(self, tag, name, *args):
@@ -502,6 +510,10 @@ class Engine:
         sv.ysel = torch.empty(B, 1024, dtype=torch.float32, device=dev)
         L.call("pcs_pool_finalize", L.ptr(pool), B, N, 1024, cps_g, L.ptr(cg.scale), L.ptr(cg.shift),
                L.ptr(sv.g), L.ptr(sv.am), L.ptr(sv.ysel), s)
+        if self.record_pool_rows:
+            self.last_pool_rows = sv.am.clone()
+        if self.pool_rows_override is not None:
+            sv.am.copy_(self.pool_rows_override)
 
         # seg_conv1 = local 64->512 GEMM + per-scene bias (W_global . g_b + b)   P:117-123
         # the per-scene bias is centred over the scenes; its mean joins the BN offset
@@ -770,6 +782,7 @@ class Engine:
         pc5 = sv.bn["bn5"]
         cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD)
         st5 = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
+        s1_5 = None   # bn5's S1 from conv5's R pass (the four-wave input-gradient kernel)
         if self.fp8:
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg[1], bufB, bias=cvec, Yp=a5,
                        w_scale=Hg[2], extra_flags=L.FLAG_AW_FP8, stats=st5, tag="dgrad:global_feat")
@@ -777,16 +790,24 @@ class Engine:
                    L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
         elif self.dt == L.BF16 and not (self.flags & (L.FLAG_GENERIC | L.FLAG_NO_GLDS)):
             # LDS-DMA kernel without the max-pool rows (no ordinary global loads in its
-            # epilogue), then their sparse term (pcs_pool_rows_add)
+            # epilogue), then their sparse term (pcs_pool_rows_add).  The four-wave kernel
+            # (csrc/gemm_w4.hip) keeps no statistics: bn5's S1 = the column sums of dz5 as
+            # stored comes from conv5's R pass below (dy_colsum); the 8-wave kernel
+            # (PCS_FLAG_GLDS8) sums S1 in its epilogue and in pcs_pool_rows_add
+            w4 = not (self.flags & L.FLAG_GLDS8)
+            if w4:
+                s1_5 = torch.empty(1024, dtype=torch.float32, device=dev)
+                st5.zero_()
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
-                       stats=st5, tag="dgrad:global_feat")
+                       stats=None if w4 else st5, tag="dgrad:global_feat")
             # the max-pool rows with the W the forward GEMM used (as the fp8 branch and the
             # Gram-form weight gradient do)
             L.call("pcs_pool_rows_add", L.ptr(bufB), self.dt, L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am),
-                   L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
+                   L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, None if w4 else L.ptr(st5), cps5, s)
         else:
+            # the max-pool rows with the W the forward GEMM used (fp32: the same tensor)
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
-                       pool_idx=sv.am, pool_coef=sp, pool_w=Wg, pool_ldw=Wg.shape[1], pool_c=1024,
+                       pool_idx=sv.am, pool_coef=sp, pool_w=Wg_r, pool_ldw=Wg_r.shape[1], pool_c=1024,
                        stats=st5, tag="dgrad:global_feat")
         dz5 = bufB
         # global_feat weight gradient from the Gram of a5: the symmetric a5^T a5 (upper tiles)
@@ -830,8 +851,11 @@ class Engine:
         #   dW5 = diag(alpha5) R + beta5 (x) colsum(a4) + diag(gamma5) W5 (a4^T a4)
         pc4 = sv.bn["bn4"]
         r5 = torch.empty(1024, 128, dtype=torch.float32, device=dev)
+        s1_kw = {"dy_colsum": s1_5} if s1_5 is not None else {}
         keepalive.append(self._wgrad(B, N, 1024, 128, L.PRO_RAW, L.PRO_BNRELU, r5, tag="wgrad:conv5",
-                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift))
+                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift, **s1_kw))
+        if s1_5 is not None:   # S1 of dz5 as one partial (chunk 0; the others zero)
+            st5[0, :, 0].copy_(s1_5)
         L.call("pcs_bn_s2_from_r", L.ptr(st5), B * cps5, 1024, L.ptr(r5), L.ptr(wc["conv5"][0]), self.dt,
                128, 128, L.ptr(pc5.mean), L.ptr(pc5.rstd), s)
         bn_bwd("bn5", "conv5", st5, cps5)

@@ -56,6 +56,10 @@ def sparse_from_keys(keys: torch.Tensor, grid: int) -> SparseVoxels:
         raise RuntimeError("pcs_amd sparse voxels run on a HIP device only (no CPU fallback)")
     keys = keys.to(torch.int64).contiguous()
     n, dev = keys.numel(), keys.device
+    # the open-addressing table keeps one row per key: duplicates (or negative keys, which as
+    # uint64 could equal the EMPTY sentinel) would silently alias rows
+    if n and (int(keys.min()) < 0 or torch.unique(keys).numel() != n):
+        raise ValueError("sparse_from_keys: keys must be unique and non-negative")
     cap = int(L.load().pcs_voxel_hash_capacity(n))
     if cap < 0:
         raise L.PcsError(L.load().pcs_last_error().decode())

@@ -27,8 +27,9 @@ def test_world_size_must_match_gpus():
 
 
 def test_rccl_refuses_more_gpus_than_visible():
-    # this container sees no GPU: --gpus 8 must exit non-zero instead of timing one device
-    r = _run(["--gpus", "8"])
+    # no visible GPU (hidden even on a GPU machine): --gpus 8 must exit non-zero instead of
+    # starting 8 ranks or timing one device
+    r = _run(["--gpus", "8"], HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
     assert r.returncode == 2
     assert "needs 8 visible GPUs" in r.stderr
 
