@@ -154,6 +154,20 @@ PCS_DEV uint32_t pos_bits8(const bf16x8 &f) {
   const uint32_t t = pos2(x.x) | (pos2(x.y) << 2) | (pos2(x.z) << 4) | (pos2(x.w) << 6);
   return (t | (t >> 15)) & 0xffu;
 }
+// pacing (pcs_gemm_args.sync_slots): the siblings' published (epoch << 16 | K-tile) words by a
+// scalar load that bypasses the scalar cache (glc: read from L2, where the siblings' vector stores
+// land); waited for by the caller's next s_waitcnt lgkmcnt(0), which the returned value is tied to
+typedef unsigned int su32x4 __attribute__((ext_vector_type(4)));
+PCS_DEV su32x4 sload4_glc(const uint32_t *p) {
+  su32x4 v;
+  asm volatile("s_load_dwordx4 %0, %1, 0x0 glc" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+PCS_DEV void wait_lgkm0_tied(su32x4 &v) {
+  sbar();
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)::"memory");
+  sbar();
+}
 // the W row a lane loads for MFMA row position m (see the lane maps above)
 PCS_DEV int wrow_of(int m) { return 16 * (m >> 4) + 8 * ((m >> 2) & 1) + (m & 3) + 4 * ((m >> 3) & 1); }
 PCS_DEV int swz64(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
@@ -278,12 +292,42 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   };
 
   f32x16 acc[4][4];
-  auto mfma_ks = [&](int set) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[set][j], af[set][i], acc[i][j], 0, 0, 0);
+  // One k-step as a hand-placed stream: the 16 MFMAs of fragment set SET, each followed by one
+  // piece of the next k-step's work -- slots 0-3 the next W fragments, 4-7 the next a5
+  // fragments (both from buffer nbuf, half NHH, k-step NT), 8-11 the DMA pieces of group G of half
+  // HH of K-tile qseq -- with scheduling barriers between slots, so that the fragment reads and
+  // the DMA issue run in the MFMAs' shadow instead of ahead of them.  The DMA is branch-free: a
+  // K-tile past the chunk re-reads the chunk's first rows into the (free) region it would use,
+  // so every wave issues the same pieces every k-step and one count serves every wait.
+  auto kstep = [&](auto SETc, auto NHHc, auto NTc, auto HHc, auto Gc, int nbuf, int qseq, int ptl, int ktl)
+      __attribute__((always_inline)) {
+    constexpr int SET = decltype(SETc)::value, NSET = SET ^ 1, NHH = decltype(NHHc)::value;
+    constexpr int NT = decltype(NTc)::value, HH = decltype(HHc)::value, G = decltype(Gc)::value;
+    const bool live = qseq < total;
+    const int64_t rb = row0 + (live ? (int64_t)ptl * BM : 0);
+    const int valid = (int)pcs_min64(BM, scene_end - rb);
+    const int kk = live ? ktl : 0;
+    const char *sa = Ab + rb * rowbytes + kk * 128 + HH * 64;
+    const char *sw = Wb + kk * 128 + HH * 64;
+    const uint32_t va0 = (uint32_t)min(prow + 32 * G, valid - 1) * rowbytes + lc16;
+    const uint32_t va1 = (uint32_t)min(prow + 32 * G + 16, valid - 1) * rowbytes + lc16;
+    const uint32_t mA = __builtin_amdgcn_readfirstlane(lds_m0 + (qseq & 1) * KBUF + HH * REG + wid * 4096);
+    const uint32_t mW = mA + 2 * REG;
+    const char *rbase = lds + nbuf * KBUF + NHH * REG;
+    sbar();
+    const uint32_t keep = m0_save();
+    sfor<16>([&](auto Sc) __attribute__((always_inline)) {
+      constexpr int S = decltype(Sc)::value, I = S >> 2, J = S & 3;
+      acc[I][J] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[SET][J], af[SET][I], acc[I][J], 0, 0, 0);
+      if constexpr (S < 4) wf[NSET][S] = *reinterpret_cast<const bf16x8 *>(rbase + oW[NT] + S * 32 * 64);
+      else if constexpr (S < 8) af[NSET][S - 4] = *reinterpret_cast<const bf16x8 *>(rbase + oA[NT] + (S - 4) * 32 * 64);
+      else if constexpr (S == 8) glds16o<2048 * G>(sa, va0, mA);
+      else if constexpr (S == 9) glds16o<2048 * G + 1024>(sa, va1, mA);
+      else if constexpr (S == 10) glds16o<2048 * G>(sw, vW[2 * G], mW);
+      else if constexpr (S == 11) glds16o<2048 * G + 1024>(sw, vW[2 * G + 1], mW);
+      sbar();
+    });
+    m0_restore(keep);
   };
   // bias as an MFMA: A' = the split bias of the lane's W row at k = 0..2 (lane half 0; half 1
   // reads the zero row), B' = ones at k = 0..2, so mfma(A', B', 0) = c[column] exactly
@@ -406,14 +450,15 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   // mask bits of k-step KS from the a5 fragments of set SET (DGRAD, the wave's mask K-tiles)
   auto mask_ks = [&](int set, auto KSc, int u) __attribute__((always_inline)) {
     constexpr int KS = decltype(KSc)::value;
+    // (both words updated through selects: an if / else on u lets LLVM index mcur by u, and
+    // the array then lives in memory -- promoted to LDS)
+    const bool u0 = u == 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint32_t b = pos_bits8(af[set][i]) << (8 * KS);
-      if (KS == 0) {
-        if (u == 0) mcur[i][0] = b; else mcur[i][1] = b;
-      } else {
-        if (u == 0) mcur[i][0] |= b; else mcur[i][1] |= b;
-      }
+      const uint32_t m0 = KS == 0 ? 0u : mcur[i][0], m1 = KS == 0 ? 0u : mcur[i][1];
+      mcur[i][0] = u0 ? (m0 | b) : mcur[i][0];
+      mcur[i][1] = u0 ? mcur[i][1] : (m1 | b);
     }
   };
   // deferred work of the previous tile (DGRAD): block (kt - 1, KS) at k-step KS of K-tiles 1..4
@@ -429,8 +474,26 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
     }
   };
 
+  // ---- pacing against the sibling column blocks of this chunk (wave 0; never for correctness:
+  // a bounded wait, switched off for the rest of the launch after a timeout)
+  uint32_t *slots = a.sync_slots;
+  bool pace = slots != nullptr && ncb == 4;
+  const uint32_t ep16 = (a.sync_epoch & 0xffffu) << 16;
+  const uint32_t *gslots = pace ? slots + (int64_t)chunk * 4 : nullptr;
+  su32x4 sib = {0u, 0u, 0u, 0u};
+  auto sib_min = [&](const su32x4 &v) __attribute__((always_inline)) {
+    uint32_t m = 0xffffu;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t w = v[c];
+      const uint32_t prog = (w & 0xffff0000u) == ep16 ? (w & 0xffffu) : 0u;   // not started: 0
+      m = c == cb ? m : (prog < m ? prog : m);
+    }
+    return m;
+  };
+
   // (row tile, K-tile) of qs+1 and qs+2 as loop counters (no divisions); p*: visiting order
-  int ka = 0, ta = 0, pa = 0;
+  int ka = 0, pa = 0;
   int qs = 0;
   int pcur = 0;
   int64_t rb_cur = row0;
@@ -448,7 +511,6 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
     for (int kt = 0; kt < nks; ++kt, ++qs) {
       const int buf = qs & 1;
       const bool w1 = kt + 1 == nks;
-      ta = w1 ? tcur + 1 : tcur;
       pa = w1 ? pnext(pcur) : pcur;
       ka = w1 ? 0 : kt + 1;
       const bool w2 = ka + 1 == nks;
@@ -459,41 +521,50 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
       const bool do_defer = MODE == MODE_DGRAD && tcur > 0 && kt >= 1 && kt <= 4;
 
       // ======== k-step 0: F(qs,0) in set 0; read F(qs,1); DMA group 1 of half 1 of qs+1
-      read_frags(1, buf, 0, 1);
-      issue(qs + 1, pa, ka, 1, 1);
-      mfma_ks(0);
+      if (pace && wid == 0) {   // publish this K-tile, fetch the siblings' (checked at k-step 2)
+        if (lane == 0)
+          __hip_atomic_store(slots + (int64_t)chunk * 4 + cb, ep16 | (uint32_t)qs, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        sib = sload4_glc(gslots);
+      }
+      kstep(IC<0>{}, IC<0>{}, IC<1>{}, IC<1>{}, IC<1>{}, buf, qs + 1, pa, ka);
       if (!(W4_ABL & 2) && do_mask) mask_ks(0, IC<0>{}, u);
       if (!(W4_ABL & 4) && do_defer) deferred(IC<0>{}, kt);
-      wait_lgkm0();
+      if (pace && wid == 0) wait_lgkm0_tied(sib); else wait_lgkm0();
       // barrier X: half 0 of buf is free (every wave retired its reads before arriving); half 1
-      // of qs landed (newer: both halves of qs+1, 16 pieces, when issued)
-      if (qs + 1 < total) wait_vm<16>(); else wait_vm<0>();
+      // of qs landed (newer: both halves of qs+1, 16 pieces)
+      wait_vm<16>();
       barrier_raw();
 
       // ======== k-step 1: F(qs,1) in set 1; read F(qs,2); DMA group 0 of half 0 of qs+2
-      read_frags(0, buf, 1, 0);
-      issue(qs + 2, pb, kb, 0, 0);
-      mfma_ks(1);
+      kstep(IC<1>{}, IC<1>{}, IC<0>{}, IC<0>{}, IC<0>{}, buf, qs + 2, pb, kb);
       if (!(W4_ABL & 2) && do_mask) mask_ks(1, IC<1>{}, u);
       if (!(W4_ABL & 4) && do_defer) deferred(IC<1>{}, kt);
       wait_lgkm0();
 
       // ======== k-step 2: F(qs,2) in set 0; read F(qs,3); DMA group 1 of half 0 of qs+2
-      read_frags(1, buf, 1, 1);
-      issue(qs + 2, pb, kb, 0, 1);
-      mfma_ks(0);
+      kstep(IC<0>{}, IC<1>{}, IC<1>{}, IC<0>{}, IC<1>{}, buf, qs + 2, pb, kb);
       if (!(W4_ABL & 2) && do_mask) mask_ks(0, IC<2>{}, u);
       if (!(W4_ABL & 4) && do_defer) deferred(IC<2>{}, kt);
       wait_lgkm0();
+      // pacing: more than 3 K-tiles ahead of the slowest sibling -> wait for it (the other waves
+      // wait at the barrier below); 96 polls (~25 k cycles) at most, then pacing is off
+      if (pace && wid == 0 && (uint32_t)qs > sib_min(sib) + 3u) {
+        int polls = 0;
+        do {
+          __builtin_amdgcn_s_sleep(2);
+          sib = sload4_glc(gslots);
+          wait_lgkm0_tied(sib);
+        } while ((uint32_t)qs > sib_min(sib) + 3u && ++polls < 96);
+        if (polls >= 96) pace = false;
+      }
       // barrier Y: half 1 of buf is free; half 0 of qs+1 landed (newer: half 1 of qs+1, half 0
       // of qs+2)
-      if (qs + 2 < total) wait_vm<16>(); else if (qs + 1 < total) wait_vm<8>(); else wait_vm<0>();
+      wait_vm<16>();
       barrier_raw();
 
       // ======== k-step 3: F(qs,3) in set 1; read F(qs+1,0); DMA group 0 of half 1 of qs+2
-      read_frags(0, buf ^ 1, 0, 0);
-      issue(qs + 2, pb, kb, 1, 0);
-      mfma_ks(1);
+      kstep(IC<1>{}, IC<0>{}, IC<0>{}, IC<1>{}, IC<0>{}, buf ^ 1, qs + 2, pb, kb);
       if (!(W4_ABL & 2) && do_mask) mask_ks(1, IC<3>{}, u);
       if (!(W4_ABL & 4) && do_defer) deferred(IC<3>{}, kt);
       wait_lgkm0();
@@ -514,6 +585,7 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  wait_vm<0>();   // the re-read DMAs past the chunk
 
   // ---- chunk end: the last tile
   if (W4_ABL & 8) return;

@@ -1,7 +1,7 @@
 // Small / bandwidth-light kernels of the PointNetSegmentation training step:
 // conv1 (Cin = 4) forward and weight gradient, BatchNorm statistic finalisation (forward
 // and backward), the global max-pool finalisation and its backward, the per-scene GEMV of
-// seg_conv1's global half, dropout keep bits (Philox4x32-10), the CE weight sum, fp32
+// seg_conv1's global half, dropout keep bits (Philox4x32-7), the CE weight sum, fp32
 // partial reduction, weight casting and the fused Adam step.
 #include "common.h"
 
@@ -1009,25 +1009,36 @@ PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
 
 __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbytes, uint32_t thr,
                                     uint8_t *bits) {
-  // byte j covers elements 8j..8j+7; one Philox call gives 8 16-bit uniforms.  A thread makes
-  // 4 consecutive bytes and stores them as one word (byte stores are issue-bound); a grid smaller
-  // than the words (pcs_dropout_bits_bounded) strides over them: the bits depend on j only
+  // bytes 2k and 2k+1 (elements 16k .. 16k+15) come from one Philox call (counter k): its 16
+  // random bytes r0..r15 give element e of the pair the 16-bit uniform (r_e << 8) | r_(e^1), so
+  // every element still keeps with probability exactly 1 - thr / 65536 (two independent bytes),
+  // and two paired elements depend on each other only through the low byte, i.e. only when one
+  // high byte equals thr >> 8.  Per 16-bit half x of an output word: element 2h+1 reads x
+  // itself, element 2h its byte swap.  Half the Philox calls of one call per byte (the kernel is
+  // ALU-bound on the 64-bit multiplies).  A thread makes 4 consecutive bytes (2 calls) and
+  // stores them as one word; a grid smaller than the words (pcs_dropout_bits_bounded) strides
+  // over them: the bits depend on j only
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; j0 < nbytes; j0 += stride) {
   uint32_t word = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t j = j0 + q;
-    uint32_t ctr[4] = {(uint32_t)j, (uint32_t)((uint64_t)j >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
+  for (int q = 0; q < 2; ++q) {
+    const int64_t k = (j0 >> 1) + q;
+    uint32_t ctr[4] = {(uint32_t)k, (uint32_t)((uint64_t)k >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
     philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
     uint32_t b = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t lo = ctr[i] & 0xffffu, hi = ctr[i] >> 16;
-      b |= (lo >= thr ? 1u : 0u) << (2 * i);
-      b |= (hi >= thr ? 1u : 0u) << (2 * i + 1);
+      const uint32_t x = ctr[i];
+      const uint32_t sw = __builtin_amdgcn_perm(0u, x, 0x02030001u);   // both halves byte-swapped
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t nat = (x >> (16 * h)) & 0xffffu, swp = (sw >> (16 * h)) & 0xffffu;
+        b |= (swp >= thr ? 1u : 0u) << (4 * i + 2 * h);
+        b |= (nat >= thr ? 1u : 0u) << (4 * i + 2 * h + 1);
+      }
     }
-    word |= b << (8 * q);
+    word |= b << (16 * q);
   }
   if (j0 + 4 <= nbytes && ((reinterpret_cast<uintptr_t>(bits) & 3) == 0)) {
     *reinterpret_cast<uint32_t *>(bits + j0) = word;

@@ -198,6 +198,19 @@ def test_dropout_bits_statistics_and_determinism():
     assert torch.equal(a, b) and not torch.equal(a, c)
     # channels are independent: per-channel keep rates all near 0.7
     assert np.abs(bits.mean(0) - 0.7).max() < 0.02
+    # elements 2i and 2i+1 of a 16-element group share one byte of their 16-bit uniforms (the
+    # high byte of one is the low byte of the other, csrc/small.hip dropout_bits_kernel): their
+    # joint keep rate is the exact enumeration over the two bytes, ~0.49 = 0.7^2
+    thr = int(0.3 * 65536.0 + 0.5)
+    r = np.arange(256)
+    u_a = (r[:, None] << 8) | r[None, :]
+    u_b = (r[None, :] << 8) | r[:, None]
+    joint = float(((u_a >= thr) & (u_b >= thr)).mean())
+    both = float((bits[:, 0::2] & bits[:, 1::2]).mean())
+    assert abs(joint - 0.49) < 5e-3 and abs(both - joint) < 3e-3, (joint, both)
+    # elements of different pairs are independent
+    cross = float((bits[:, 0::4] & bits[:, 2::4]).mean())
+    assert abs(cross - 0.49) < 3e-3, cross
     # a bounded grid (words strided over few workgroups) draws the same bits, ragged tail included
     for wg in (1, 7, 512):
         d = torch.zeros(M - 3, C // 8, dtype=torch.uint8, device=DEV)
