@@ -127,15 +127,6 @@ typedef struct {
   const uint8_t *w_scale; /* [Ncols] E8M0 scale of each W row (PCS_FLAG_AW_FP8) */
   const void *W2;       /* [Ncols, K - K1] dtype: the second W block (PCS_PRO_CAT) */
   int32_t K1;           /* PCS_PRO_CAT: width of A (a multiple of the 32/16-element k-step) */
-  /* Optional pacing of the four-wave global_feat kernel (csrc/gemm_w4.hip; ignored elsewhere):
-   * the Ncols / 256 column-block workgroups of a row chunk read the same operand rows, which
-   * come from HBM once only while they stay within a few K-tiles of each other.  Each
-   * workgroup publishes (sync_epoch << 16 | K-tile) in sync_slots[chunk * (Ncols/256) + block]
-   * and waits (bounded, never for correctness) when it runs ahead of its slowest sibling.
-   * sync_slots: >= B * chunks_per_scene * Ncols/256 u32 owned by the caller, any initial
-   * content; sync_epoch: a value that differs from the previous call's (low 16 bits used). */
-  uint32_t *sync_slots;
-  uint32_t sync_epoch;
 } pcs_gemm_args;
 
 /* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error.  The

@@ -39,7 +39,6 @@ class GemmArgs(ct.Structure):
         ("stats", _vp), ("pool", _vp), ("flags", _i32),
         ("pool_w", _vp), ("pool_ldw", _i64), ("pool_c", _i32), ("w_scale", _vp),
         ("W2", _vp), ("K1", _i32),
-        ("sync_slots", _vp), ("sync_epoch", ct.c_uint32),
     ]
 
 

@@ -608,7 +608,9 @@ extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
 
 extern "C" int pcs_gemm_w4_selected(const pcs_gemm_args *ap) {
   if (!ap) return pcs_set_einval("pcs_gemm_w4_selected", "null args");
-  return wide_class(*ap) && pcs_gemm_w4_applicable(*ap) ? 1 : 0;
+  pcs_gemm_args g = *ap;
+  if (pcs_gemm_geometry(&g) < 0) return 0;
+  return wide_class(g) && pcs_gemm_w4_applicable(g) ? 1 : 0;
 }
 
 extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {

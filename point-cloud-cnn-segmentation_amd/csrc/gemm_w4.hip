@@ -61,6 +61,9 @@ constexpr int LDS_BYTES = OFF_RUNN + 16;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+// W4_ABL (timing ablations, wrong results): 1 no tile readout, 2 no mask bits, 4 no deferred
+// stores, 8 no chunk-end epilogue, 16 no DMA waits in the loop, 32 no loop barriers, 64 no DMA
+// issue in the loop, 128 no fragment reads in the loop
 #ifndef W4_ABL
 #define W4_ABL 0
 #endif
@@ -154,20 +157,6 @@ PCS_DEV uint32_t pos_bits8(const bf16x8 &f) {
   const uint32_t t = pos2(x.x) | (pos2(x.y) << 2) | (pos2(x.z) << 4) | (pos2(x.w) << 6);
   return (t | (t >> 15)) & 0xffu;
 }
-// pacing (pcs_gemm_args.sync_slots): the siblings' published (epoch << 16 | K-tile) words by a
-// scalar load that bypasses the scalar cache (glc: read from L2, where the siblings' vector stores
-// land); waited for by the caller's next s_waitcnt lgkmcnt(0), which the returned value is tied to
-typedef unsigned int su32x4 __attribute__((ext_vector_type(4)));
-PCS_DEV su32x4 sload4_glc(const uint32_t *p) {
-  su32x4 v;
-  asm volatile("s_load_dwordx4 %0, %1, 0x0 glc" : "=s"(v) : "s"(p) : "memory");
-  return v;
-}
-PCS_DEV void wait_lgkm0_tied(su32x4 &v) {
-  sbar();
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)::"memory");
-  sbar();
-}
 // the W row a lane loads for MFMA row position m (see the lane maps above)
 PCS_DEV int wrow_of(int m) { return 16 * (m >> 4) + 8 * ((m >> 2) & 1) + (m & 3) + 4 * ((m >> 3) & 1); }
 PCS_DEV int swz64(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
@@ -214,6 +203,9 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   const char *Ab = reinterpret_cast<const char *>(a.A);
   const char *Wb = reinterpret_cast<const char *>(a.W) + (int64_t)n0 * K * 2;
   const uint32_t rowbytes = (uint32_t)K * 2u;
+  const char *Arow0 = Ab + row0 * rowbytes;
+  const uint32_t tile_bytes = (uint32_t)BM * rowbytes;
+  const int rows_left = (int)pcs_min64(scene_end - row0, (int64_t)ntl * BM);
 
   // ---- per-workgroup constants -> LDS (ordinary loads, all retired before the first DMA)
   if (tid < BN) {
@@ -244,6 +236,7 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
 #pragma unroll
   for (int q = 0; q < 4; ++q) vW[q] = (uint32_t)(prow + 16 * q) * rowbytes + lc16;
   const uint32_t lds_m0 = (uint32_t)(uintptr_t)(lds_void_t *)lds;
+  const uint32_t m0_wave = __builtin_amdgcn_readfirstlane(lds_m0 + wid * 4096);
   const int cw = wrow_of(lr);
   // (qseq, tile in visiting order, kt, half hh, group g): pieces q = 2g, 2g+1 of A-hh and W-hh
   auto issue = [&](int qseq, int ptl, int kt, int hh, int g) __attribute__((always_inline)) {
@@ -299,19 +292,20 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   // the DMA issue run in the MFMAs' shadow instead of ahead of them.  The DMA is branch-free: a
   // K-tile past the chunk re-reads the chunk's first rows into the (free) region it would use,
   // so every wave issues the same pieces every k-step and one count serves every wait.
-  auto kstep = [&](auto SETc, auto NHHc, auto NTc, auto HHc, auto Gc, int nbuf, int qseq, int ptl, int ktl)
-      __attribute__((always_inline)) {
+  auto kstep = [&](auto SETc, auto NHHc, auto NTc, auto HHc, auto Gc, int nbuf, int qseq, int ptl, int ktl,
+                   auto &&ex) __attribute__((always_inline)) {
     constexpr int SET = decltype(SETc)::value, NSET = SET ^ 1, NHH = decltype(NHHc)::value;
     constexpr int NT = decltype(NTc)::value, HH = decltype(HHc)::value, G = decltype(Gc)::value;
+    // 32-bit offsets from the chunk's first row (a chunk spans < 2^31 rows and < 2^32 bytes of
+    // row tiles: pcs_gemm_w4_applicable), so the per-k-step address work stays a few SALU ops
     const bool live = qseq < total;
-    const int64_t rb = row0 + (live ? (int64_t)ptl * BM : 0);
-    const int valid = (int)pcs_min64(BM, scene_end - rb);
-    const int kk = live ? ktl : 0;
-    const char *sa = Ab + rb * rowbytes + kk * 128 + HH * 64;
-    const char *sw = Wb + kk * 128 + HH * 64;
+    const int pt = live ? ptl : 0, kk = live ? ktl : 0;
+    const int valid = min(BM, rows_left - pt * BM);
+    const char *sa = Arow0 + ((uint32_t)pt * tile_bytes + (uint32_t)(kk * 128 + HH * 64));
+    const char *sw = Wb + (kk * 128 + HH * 64);
     const uint32_t va0 = (uint32_t)min(prow + 32 * G, valid - 1) * rowbytes + lc16;
     const uint32_t va1 = (uint32_t)min(prow + 32 * G + 16, valid - 1) * rowbytes + lc16;
-    const uint32_t mA = __builtin_amdgcn_readfirstlane(lds_m0 + (qseq & 1) * KBUF + HH * REG + wid * 4096);
+    const uint32_t mA = m0_wave + (uint32_t)(qseq & 1) * KBUF + HH * REG;
     const uint32_t mW = mA + 2 * REG;
     const char *rbase = lds + nbuf * KBUF + NHH * REG;
     sbar();
@@ -319,12 +313,14 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
     sfor<16>([&](auto Sc) __attribute__((always_inline)) {
       constexpr int S = decltype(Sc)::value, I = S >> 2, J = S & 3;
       acc[I][J] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[SET][J], af[SET][I], acc[I][J], 0, 0, 0);
-      if constexpr (S < 4) wf[NSET][S] = *reinterpret_cast<const bf16x8 *>(rbase + oW[NT] + S * 32 * 64);
-      else if constexpr (S < 8) af[NSET][S - 4] = *reinterpret_cast<const bf16x8 *>(rbase + oA[NT] + (S - 4) * 32 * 64);
+      if constexpr (S < 4) { if (!(W4_ABL & 128)) wf[NSET][S] = *reinterpret_cast<const bf16x8 *>(rbase + oW[NT] + S * 32 * 64); }
+      else if constexpr (S < 8) { if (!(W4_ABL & 128)) af[NSET][S - 4] = *reinterpret_cast<const bf16x8 *>(rbase + oA[NT] + (S - 4) * 32 * 64); }
+      else if constexpr (W4_ABL & 64) {}
       else if constexpr (S == 8) glds16o<2048 * G>(sa, va0, mA);
       else if constexpr (S == 9) glds16o<2048 * G + 1024>(sa, va1, mA);
       else if constexpr (S == 10) glds16o<2048 * G>(sw, vW[2 * G], mW);
       else if constexpr (S == 11) glds16o<2048 * G + 1024>(sw, vW[2 * G + 1], mW);
+      ex(Sc);   // the caller's work for this slot (epilogue pieces)
       sbar();
     });
     m0_restore(keep);
@@ -342,29 +338,32 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   // DGRAD state: the previous tile, bf16-packed, waiting for its mask and stores
   uint32_t pk[4][4][8];
   uint32_t mcur[4][2], mprev[4][2];   // mask bits [i][j >> 1]: bit 16 (j & 1) + q <-> register q
-  int64_t rb_prev = 0;
-  int valid_prev = 0;
-  const int kqa0 = (n0 + 128 * wn) / BK;   // K-tiles holding this wave's mask columns: kqa0, +1
+  // the previous tile's output rows through a buffer descriptor whose range ends at its last
+  // valid row: a store past it is dropped by the hardware, so every lane issues both stores of
+  // every block -- the counted waits below then see a fixed number of stores per k-step
   bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
-  // mask + 2 stores of block (I, J) of the previous tile
-  auto flush_block = [&](auto Ic, auto Jc, const uint32_t (&mw)[4][2], int64_t rbp, int vp) __attribute__((always_inline)) {
-    constexpr int I = decltype(Ic)::value, J = decltype(Jc)::value;
-    sbar();
-    const uint32_t w = mw[I][J >> 1] >> (16 * (J & 1));
-    uint32_t v[8];
+  auto tile_rsrc = [&](int64_t rb, int valid) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char *>(Cg + rb * (int64_t)Ncols), 0,
+                                             (int)((uint32_t)valid * (uint32_t)Ncols * 2u), 0x00020000);
+  };
+  __amdgpu_buffer_rsrc_t rs_prev = tile_rsrc(0, 0);
+  const int kqa0 = (n0 + 128 * wn) / BK;   // K-tiles holding this wave's mask columns: kqa0, +1
+  const uint32_t o_st = (uint32_t)(((wm * 128 + lr) * Ncols + n0 + wn * 128 + 8 * lh) * 2);
+  // mask + store of half H (columns 16 H + 8 lh + 0..7) of block (I, J) of a finished tile
+  auto flush_half = [&](auto Ic, auto Jc, auto Hc, const uint32_t (&mw)[4][2], __amdgpu_buffer_rsrc_t rs) __attribute__((always_inline)) {
+    constexpr int I = decltype(Ic)::value, J = decltype(Jc)::value, H = decltype(Hc)::value;
+    const uint32_t w = mw[I][J >> 1] >> (16 * (J & 1) + 8 * H);
+    uint32_t v[4];
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
+    for (int d = 0; d < 4; ++d) {
       const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)w, 2 * d, 1);
       const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)w, 2 * d + 1, 1);
-      v[d] = pk[I][J][d] & ((lo & 0xffffu) | (hi << 16));
+      v[d] = pk[I][J][4 * H + d] & ((lo & 0xffffu) | (hi << 16));
     }
-    const int rloc = wm * 128 + 32 * I + lr;
-    if (rloc < vp) {
-      bf16_t *p = Cg + (rbp + rloc) * (int64_t)Ncols + n0 + wn * 128 + 32 * J + 8 * lh;
-      *reinterpret_cast<u32x4 *>(p) = mk_u32x4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<u32x4 *>(p + 16) = mk_u32x4(v[4], v[5], v[6], v[7]);
-    }
-    sbar();
+    // one lane offset for every block: the block's row step on the scalar offset, its column
+    // step in the instruction's immediate
+    const int so = __builtin_amdgcn_readfirstlane(I * 32 * Ncols * 2);
+    __builtin_amdgcn_raw_buffer_store_b128(mk_u32x4(v[0], v[1], v[2], v[3]), rs, (int)o_st + 64 * J + 32 * H, so, 0);
   };
   // read out accumulator block (I, J) into pk (DGRAD)
   auto pack_block = [&](auto Ic, auto Jc) __attribute__((always_inline)) {
@@ -447,51 +446,64 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   read_frags(0, 0, 0, 0);
   wait_lgkm0();
 
-  // mask bits of k-step KS from the a5 fragments of set SET (DGRAD, the wave's mask K-tiles)
-  auto mask_ks = [&](int set, auto KSc, int u) __attribute__((always_inline)) {
-    constexpr int KS = decltype(KSc)::value;
-    // (both words updated through selects: an if / else on u lets LLVM index mcur by u, and
-    // the array then lives in memory -- promoted to LDS)
+  // DGRAD work placed in the MFMA slots of k-step KS (fragment set SET): the mask bits of the
+  // a5 fragments in the wave's two mask K-tiles (slots 1, 3, 5, 7: i = 0..3; mcur[i][u] collects
+  // k-steps 0..3 of K-tile kqa0 + u), and block (kt - 1, KS) of the previous tile in K-tiles
+  // 1..4 (slots 12, 14: its two halves).  Both words of mcur go through selects: an if / else
+  // on u lets LLVM index mcur by u, and the array then lives in memory.
+  auto mask_piece = [&](auto SETc, auto KSc, auto Ic, int u) __attribute__((always_inline)) {
+    constexpr int SET = decltype(SETc)::value, KS = decltype(KSc)::value, i = decltype(Ic)::value;
     const bool u0 = u == 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t b = pos_bits8(af[set][i]) << (8 * KS);
-      const uint32_t m0 = KS == 0 ? 0u : mcur[i][0], m1 = KS == 0 ? 0u : mcur[i][1];
-      mcur[i][0] = u0 ? (m0 | b) : mcur[i][0];
-      mcur[i][1] = u0 ? mcur[i][1] : (m1 | b);
-    }
+    const uint32_t b = pos_bits8(af[SET][i]) << (8 * KS);
+    const uint32_t m0 = KS == 0 ? 0u : mcur[i][0], m1 = KS == 0 ? 0u : mcur[i][1];
+    mcur[i][0] = u0 ? (m0 | b) : mcur[i][0];
+    mcur[i][1] = u0 ? mcur[i][1] : (m1 | b);
   };
-  // deferred work of the previous tile (DGRAD): block (kt - 1, KS) at k-step KS of K-tiles 1..4
-  auto deferred = [&](auto KSc, int kt) __attribute__((always_inline)) {
-    if constexpr (MODE == MODE_DGRAD) {
-      switch (kt) {
-        case 1: flush_block(IC<0>{}, KSc, mprev, rb_prev, valid_prev); break;
-        case 2: flush_block(IC<1>{}, KSc, mprev, rb_prev, valid_prev); break;
-        case 3: flush_block(IC<2>{}, KSc, mprev, rb_prev, valid_prev); break;
-        case 4: flush_block(IC<3>{}, KSc, mprev, rb_prev, valid_prev); break;
-        default: break;
+  auto slot_work = [&](auto SETc, auto KSc, bool do_mask, int u, bool do_defer, int kt) __attribute__((always_inline)) {
+    return [&, SETc, KSc, do_mask, u, do_defer, kt](auto Sc) __attribute__((always_inline)) {
+      constexpr int S = decltype(Sc)::value;
+      if constexpr (MODE != MODE_DGRAD) {
+        (void)SETc; (void)KSc; (void)do_mask; (void)u; (void)do_defer; (void)kt;
+      } else {
+        if constexpr ((S & 1) && S < 8) {
+          if (!(W4_ABL & 2) && do_mask) mask_piece(SETc, KSc, IC<(S >> 1)>{}, u);
+        } else if constexpr (S == 12 || S == 14) {
+          if (!(W4_ABL & 4) && do_defer) {
+            constexpr int H = S == 14;
+            switch (kt) {
+              case 1: flush_half(IC<0>{}, KSc, IC<H>{}, mprev, rs_prev); break;
+              case 2: flush_half(IC<1>{}, KSc, IC<H>{}, mprev, rs_prev); break;
+              case 3: flush_half(IC<2>{}, KSc, IC<H>{}, mprev, rs_prev); break;
+              default: flush_half(IC<3>{}, KSc, IC<H>{}, mprev, rs_prev); break;
+            }
+          }
+        }
       }
-    }
+    };
   };
 
-  // ---- pacing against the sibling column blocks of this chunk (wave 0; never for correctness:
-  // a bounded wait, switched off for the rest of the launch after a timeout)
-  uint32_t *slots = a.sync_slots;
-  bool pace = slots != nullptr && ncb == 4;
-  const uint32_t ep16 = (a.sync_epoch & 0xffffu) << 16;
-  const uint32_t *gslots = pace ? slots + (int64_t)chunk * 4 : nullptr;
-  su32x4 sib = {0u, 0u, 0u, 0u};
-  auto sib_min = [&](const su32x4 &v) __attribute__((always_inline)) {
-    uint32_t m = 0xffffu;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint32_t w = v[c];
-      const uint32_t prog = (w & 0xffff0000u) == ep16 ? (w & 0xffffu) : 0u;   // not started: 0
-      m = c == cb ? m : (prog < m ? prog : m);
+  // The counted waits at barriers X and Y: 16 DMA pieces are newer than the ones awaited, plus
+  // (DGRAD) the deferred stores issued since -- vector memory operations retire in order, so a
+  // count that left them out would wait for the stores too.  Two stores per k-step of K-tiles
+  // 1..4 (none in a chunk's first tile, K >= 6 * 64 so none in a tile's last K-tile):
+  //   X (awaits K-tile kt-1's k-step 0 DMA): + 8 [kt-1 in 1..4] + 2 [kt in 1..4]
+  //   Y (awaits K-tile kt-1's k-step 2 DMA): + 4 [kt-1 in 1..4] + 6 [kt in 1..4]
+  auto wait_x = [&](int dn) __attribute__((always_inline)) {
+    switch (dn) {
+      case 1: wait_vm<18>(); break;
+      case 2: case 3: case 4: wait_vm<26>(); break;
+      case 5: wait_vm<24>(); break;
+      default: wait_vm<16>(); break;
     }
-    return m;
   };
-
+  auto wait_y = [&](int dn) __attribute__((always_inline)) {
+    switch (dn) {
+      case 1: wait_vm<22>(); break;
+      case 2: case 3: case 4: wait_vm<26>(); break;
+      case 5: wait_vm<20>(); break;
+      default: wait_vm<16>(); break;
+    }
+  };
   // (row tile, K-tile) of qs+1 and qs+2 as loop counters (no divisions); p*: visiting order
   int ka = 0, pa = 0;
   int qs = 0;
@@ -519,54 +531,34 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
       const int u = kt - kqa0;                         // DGRAD: 0 / 1 in this wave's mask K-tiles
       const bool do_mask = MODE == MODE_DGRAD && (unsigned)u < 2u;
       const bool do_defer = MODE == MODE_DGRAD && tcur > 0 && kt >= 1 && kt <= 4;
+      const int dn = MODE == MODE_DGRAD && tcur > 0 ? kt : 0;   // the barriers' store counts
 
       // ======== k-step 0: F(qs,0) in set 0; read F(qs,1); DMA group 1 of half 1 of qs+1
-      if (pace && wid == 0) {   // publish this K-tile, fetch the siblings' (checked at k-step 2)
-        if (lane == 0)
-          __hip_atomic_store(slots + (int64_t)chunk * 4 + cb, ep16 | (uint32_t)qs, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        sib = sload4_glc(gslots);
-      }
-      kstep(IC<0>{}, IC<0>{}, IC<1>{}, IC<1>{}, IC<1>{}, buf, qs + 1, pa, ka);
-      if (!(W4_ABL & 2) && do_mask) mask_ks(0, IC<0>{}, u);
-      if (!(W4_ABL & 4) && do_defer) deferred(IC<0>{}, kt);
-      if (pace && wid == 0) wait_lgkm0_tied(sib); else wait_lgkm0();
+      kstep(IC<0>{}, IC<0>{}, IC<1>{}, IC<1>{}, IC<1>{}, buf, qs + 1, pa, ka,
+            slot_work(IC<0>{}, IC<0>{}, do_mask, u, do_defer, kt));
+      wait_lgkm0();
       // barrier X: half 0 of buf is free (every wave retired its reads before arriving); half 1
       // of qs landed (newer: both halves of qs+1, 16 pieces)
-      wait_vm<16>();
-      barrier_raw();
+      if (!(W4_ABL & 16)) wait_x(dn);
+      if (!(W4_ABL & 32)) barrier_raw();
 
       // ======== k-step 1: F(qs,1) in set 1; read F(qs,2); DMA group 0 of half 0 of qs+2
-      kstep(IC<1>{}, IC<1>{}, IC<0>{}, IC<0>{}, IC<0>{}, buf, qs + 2, pb, kb);
-      if (!(W4_ABL & 2) && do_mask) mask_ks(1, IC<1>{}, u);
-      if (!(W4_ABL & 4) && do_defer) deferred(IC<1>{}, kt);
+      kstep(IC<1>{}, IC<1>{}, IC<0>{}, IC<0>{}, IC<0>{}, buf, qs + 2, pb, kb,
+            slot_work(IC<1>{}, IC<1>{}, do_mask, u, do_defer, kt));
       wait_lgkm0();
 
       // ======== k-step 2: F(qs,2) in set 0; read F(qs,3); DMA group 1 of half 0 of qs+2
-      kstep(IC<0>{}, IC<1>{}, IC<1>{}, IC<0>{}, IC<1>{}, buf, qs + 2, pb, kb);
-      if (!(W4_ABL & 2) && do_mask) mask_ks(0, IC<2>{}, u);
-      if (!(W4_ABL & 4) && do_defer) deferred(IC<2>{}, kt);
+      kstep(IC<0>{}, IC<1>{}, IC<1>{}, IC<0>{}, IC<1>{}, buf, qs + 2, pb, kb,
+            slot_work(IC<0>{}, IC<2>{}, do_mask, u, do_defer, kt));
       wait_lgkm0();
-      // pacing: more than 3 K-tiles ahead of the slowest sibling -> wait for it (the other waves
-      // wait at the barrier below); 96 polls (~25 k cycles) at most, then pacing is off
-      if (pace && wid == 0 && (uint32_t)qs > sib_min(sib) + 3u) {
-        int polls = 0;
-        do {
-          __builtin_amdgcn_s_sleep(2);
-          sib = sload4_glc(gslots);
-          wait_lgkm0_tied(sib);
-        } while ((uint32_t)qs > sib_min(sib) + 3u && ++polls < 96);
-        if (polls >= 96) pace = false;
-      }
       // barrier Y: half 1 of buf is free; half 0 of qs+1 landed (newer: half 1 of qs+1, half 0
       // of qs+2)
-      wait_vm<16>();
-      barrier_raw();
+      if (!(W4_ABL & 16)) wait_y(dn);
+      if (!(W4_ABL & 32)) barrier_raw();
 
       // ======== k-step 3: F(qs,3) in set 1; read F(qs+1,0); DMA group 0 of half 1 of qs+2
-      kstep(IC<1>{}, IC<0>{}, IC<0>{}, IC<1>{}, IC<0>{}, buf ^ 1, qs + 2, pb, kb);
-      if (!(W4_ABL & 2) && do_mask) mask_ks(1, IC<3>{}, u);
-      if (!(W4_ABL & 4) && do_defer) deferred(IC<3>{}, kt);
+      kstep(IC<1>{}, IC<0>{}, IC<0>{}, IC<1>{}, IC<0>{}, buf ^ 1, qs + 2, pb, kb,
+            slot_work(IC<1>{}, IC<3>{}, do_mask, u, do_defer, kt));
       wait_lgkm0();
     }
     pcur = pa;
@@ -577,8 +569,7 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
     if constexpr (MODE == MODE_DGRAD) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) { mprev[i][0] = mcur[i][0]; mprev[i][1] = mcur[i][1]; }
-      rb_prev = rb_cur;
-      valid_prev = valid_cur;
+      rs_prev = tile_rsrc(rb_cur, valid_cur);
       if (!(W4_ABL & 1)) sfor<4>([&](auto Ic) __attribute__((always_inline)) { sfor<4>([&](auto Jc) __attribute__((always_inline)) { pack_block(Ic, Jc); }); });
     } else {
       if (!(W4_ABL & 1)) sfor<4>([&](auto Jc) __attribute__((always_inline)) { pool_block(Jc, rb_cur, valid_cur); });
@@ -590,8 +581,9 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
   // ---- chunk end: the last tile
   if (W4_ABL & 8) return;
   if constexpr (MODE == MODE_DGRAD) {
+    const __amdgpu_buffer_rsrc_t rs_last = tile_rsrc(rb_cur, valid_cur);
     sfor<4>([&](auto Ic) __attribute__((always_inline)) { sfor<4>([&](auto Jc) __attribute__((always_inline)) { pack_block(Ic, Jc); }); });
-    sfor<4>([&](auto Ic) __attribute__((always_inline)) { sfor<4>([&](auto Jc) __attribute__((always_inline)) { flush_block(Ic, Jc, mcur, rb_cur, valid_cur); }); });
+    sfor<4>([&](auto Ic) __attribute__((always_inline)) { sfor<4>([&](auto Jc) __attribute__((always_inline)) { flush_half(Ic, Jc, IC<0>{}, mcur, rs_last); flush_half(Ic, Jc, IC<1>{}, mcur, rs_last); }); });
   } else {
     sfor<4>([&](auto Jc) __attribute__((always_inline)) { pool_block(Jc, rb_cur, valid_cur); });
     __syncthreads();
@@ -617,10 +609,14 @@ bool pcs_gemm_w4_applicable(const pcs_gemm_args &a) {
   if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS | PCS_FLAG_GLDS8 | PCS_FLAG_AW_FP8)))
     return false;
   if (a.prologue != PCS_PRO_RAW || a.K % (2 * BK) != 0 || a.Ncols % BN != 0 || a.stats) return false;
+  // a chunk's row tiles addressed by 32-bit offsets (after pcs_gemm_geometry)
+  if (a.chunks_per_scene <= 0) return false;
+  const int64_t tps = (a.scene_rows + BM - 1) / BM, tpc = (tps + a.chunks_per_scene - 1) / a.chunks_per_scene;
+  if (tpc * BM * a.K * 2 > 0xffffffffLL) return false;
   if (a.epilogue == PCS_EPI_FWD)
     return a.C == nullptr && a.scene_bias == nullptr && a.pool && a.es && (a.flags & PCS_FLAG_POOL_SIGNED_W);
-  if (a.epilogue == PCS_EPI_DGRAD)   // the deferred stores use K-tiles 1..4: K >= 5 * 64
-    return a.K >= 5 * BK && a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask && !a.pool_w;
+  if (a.epilogue == PCS_EPI_DGRAD)   // the deferred stores use K-tiles 1..4 (not the last): K >= 6 * 64
+    return a.K >= 6 * BK && a.Yp == a.A && a.K == a.Ncols && !a.es && !a.et && !a.erstd && !a.addend && !a.c_mask && !a.pool_w;
   return false;
 }
 

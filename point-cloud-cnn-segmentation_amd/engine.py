@@ -174,8 +174,6 @@ class Engine:
         self.buckets = bucket_ranges(num_classes, input_dim)
         self._geo = {}
         self._side = {}   # device -> side stream
-        self._sync = {}   # device -> pacing words of the four-wave global_feat kernel
-        self._sync_epoch = 0
         self.flags = 0       # L.FLAG_GENERIC forces the generic GEMM (cross-checks)
         self.timing = None   # dict tag -> [(start, end) torch.cuda.Event] when profiling
         self.timing_tags = None   # set of tags to bracket (None = every tagged launch)
@@ -277,16 +275,6 @@ class Engine:
                    L.ptr(coef.shift), self._stream())
         return coef
 
-    def _sync_slots(self, dev, n):
-        """Pacing words for the four-wave global_feat kernel (pcs_gemm_args.sync_slots): one u32
-        per (row chunk, column block), any initial content, and a fresh epoch per call."""
-        t = self._sync.get(dev)
-        if t is None or t.numel() < n:
-            t = torch.zeros(max(n, 4096), dtype=torch.int32, device=dev)
-            self._sync[dev] = t
-        self._sync_epoch = (self._sync_epoch + 1) & 0xffff
-        return t, self._sync_epoch
-
     def _gemm(self, B, N, K, ncols, pro, epi, A, W, C, **kw):
         tag = kw.pop("tag", None)
         cps, _ = self.geometry(B, N, K, ncols, pro, epi)
@@ -297,9 +285,6 @@ class Engine:
                        a_keep_scale=kw.pop("a_keep_scale", 1.0),
                        c_keep_scale=kw.pop("c_keep_scale", 1.0),
                        pool_ldw=kw.pop("pool_ldw", 0), pool_c=kw.pop("pool_c", 0), K1=kw.pop("K1", 0))
-        if kw.pop("pace", False):
-            slots, a.sync_epoch = self._sync_slots(A.device, B * cps * max(1, ncols // 256))
-            a.sync_slots = slots.data_ptr()
         for k, v in kw.items():
             setattr(a, k, L.ptr(v))
         self._launch(tag, "pcs_gemm", ct.byref(a), self._stream())
@@ -516,7 +501,7 @@ class Engine:
                        w_scale=wc["global_feat_fp8"][1], extra_flags=L.FLAG_AW_FP8 | sflag, tag="fwd:global_feat")
         else:
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_FWD, a5, Wf, None, stats=st_g, pool=pool, es=gamma_g,
-                       extra_flags=sflag, pace=True, tag="fwd:global_feat")
+                       extra_flags=sflag, tag="fwd:global_feat")
         sv.bn["bn_global"] = self._bn_finalize("bn_global", st, B, N, 1024, cps_st, rpc_st, P, bufs,
                                                train, dev, offset=P["global_feat.bias"])
         cg = sv.bn["bn_global"]
@@ -814,7 +799,7 @@ class Engine:
                 s1_5 = torch.empty(1024, dtype=torch.float32, device=dev)
                 st5.zero_()
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
-                       stats=None if w4 else st5, pace=w4, tag="dgrad:global_feat")
+                       stats=None if w4 else st5, tag="dgrad:global_feat")
             # the max-pool rows with the W the forward GEMM used (as the fp8 branch and the
             # Gram-form weight gradient do)
             L.call("pcs_pool_rows_add", L.ptr(bufB), self.dt, L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am),

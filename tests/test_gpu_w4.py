@@ -75,10 +75,11 @@ def test_dgrad_bias_exact():
 
 def _pool(L, A, Ws, gamma, B, N, flags, cps):
     K, Nc = A.shape[1], Ws.shape[0]
-    a, _ = _args(L, B, N, K, Nc, L.EPI_FWD, flags | L.FLAG_POOL_SIGNED_W, cps)
+    a, rpc = _args(L, B, N, K, Nc, L.EPI_FWD, flags | L.FLAG_POOL_SIGNED_W, cps)
     pool = torch.full((B * a.chunks_per_scene, Nc, 4), float("nan"), device=DEV)
     a.A, a.W, a.C, a.pool, a.es = A.data_ptr(), Ws.data_ptr(), None, pool.data_ptr(), gamma.data_ptr()
     L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    _pool.rpc = rpc   # rows per chunk (whole row tiles: pcs_gemm_geometry)
     return pool
 
 
@@ -104,7 +105,7 @@ def test_forward_pool_signed(B, N, K, cps):
     sgn = torch.where(gamma > 0, 1.0, -1.0).double()
     nch = new.shape[0]
     cps_ = nch // B
-    rpc = -(-N // cps_)
+    rpc = _pool.rpc
     scl = y.abs().max().item()
     for ch in range(nch):
         b, ci = divmod(ch, cps_)

@@ -54,51 +54,42 @@ def main():
 
     keep = []
 
-    slots = torch.zeros(4096, dtype=torch.int32, device=dev)
-    epoch = [0]
-
-    def paced(a):
-        epoch[0] += 1
-        a.sync_slots, a.sync_epoch = slots.data_ptr(), epoch[0] & 0xffff
-        return a
-
-    def fwd(flags, pace=False):
+    def fwd(flags):
         a = args(L.EPI_FWD, flags | L.FLAG_POOL_SIGNED_W)
         pool = torch.empty(B * a.chunks_per_scene, Nc, 4, device=dev)
         keep.append(pool)
         a.A, a.W, a.C, a.pool, a.es = A.data_ptr(), Ws.data_ptr(), None, pool.data_ptr(), gsign.data_ptr()
-        if pace:
-            return lambda: L.call("pcs_gemm", ct.byref(paced(a)), L.stream_ptr()), pool
         return lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr()), pool
 
-    def dgrad(flags, out, stats=False, pace=False):
+    def dgrad(flags, out, stats=False):
         a = args(L.EPI_DGRAD, flags)
         a.A, a.W, a.C, a.Yp, a.bias = A.data_ptr(), H.data_ptr(), out.data_ptr(), A.data_ptr(), c.data_ptr()
         if stats:
             st = torch.empty(B * a.chunks_per_scene, Nc, 2, device=dev)
             keep.append(st)
             a.stats = st.data_ptr()
-        if pace:
-            return lambda: L.call("pcs_gemm", ct.byref(paced(a)), L.stream_ptr())
         return lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
 
     variants = [
         ("dgrad w4 (mask + store + bias)", dgrad(0, C1)),
-        ("dgrad w4 paced", dgrad(0, C1, pace=True)),
         ("dgrad glds8 (mask + store + bias)", dgrad(L.FLAG_GLDS8, C2)),
         ("dgrad glds8 + S1 (the r03 training call)", dgrad(L.FLAG_GLDS8, C2, stats=True)),
     ]
     f4, p4 = fwd(0)
-    f4p, _ = fwd(0, pace=True)
     f8, p8 = fwd(L.FLAG_GLDS8)
-    variants += [("fwd w4 (signed-W max-pool)", f4), ("fwd w4 paced", f4p), ("fwd glds8 (signed-W max-pool)", f8)]
+    variants += [("fwd w4 (signed-W max-pool)", f4), ("fwd glds8 (signed-W max-pool)", f8)]
+    if os.environ.get("W4_ONLY"):   # ablation builds: the two w4 calls only
+        variants = [variants[0], variants[3]]
+        rounds = 1
     for r in range(rounds):
         for name, fn in variants:
             ms = timeit(fn)
             print(f"[{r}] {name:44s} {ms:8.3f} ms  {flops / ms / 1e9:8.1f} TF/s  {flops / ms / 1e9 / 2516.6:6.3f}",
                   flush=True)
+    if os.environ.get("W4_ONLY"):
+        return
     variants[0][1]()   # w4 -> C1
-    variants[2][1]()   # glds8 -> C2
+    variants[1][1]()   # glds8 -> C2
     torch.cuda.synchronize()
     same = (C1.view(torch.int16) == C2.view(torch.int16)).float().mean().item()
     d = (C1.float() - C2.float()).abs().max().item()
