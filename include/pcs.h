@@ -45,9 +45,10 @@ enum {
                            W's rows (pcs_sign_rows) and bias by sign(es), so the pool keeps the
                            plain column max of acc (no multiply); es still names the sign.
                            Needs pool and es, no statistics (they would be of the signed y)  */
-  PCS_FLAG_GLDS8 = 32   /* bf16 global_feat GEMMs: the 8-wave 16x16x32 LDS-DMA kernel
-                           (gemm_glds.hip) instead of the 4-wave 32x32x16 one (gemm_w4.hip),
-                           for A/B timing and cross-checks                                   */
+  PCS_FLAG_W4 = 32      /* bf16 global_feat GEMMs (FWD signed-W pool / DGRAD without
+                           statistics) on the 4-wave 32x32x16 kernel (gemm_w4.hip) instead of
+                           the 8-wave 16x16x32 one (gemm_glds.hip): opt-in, slower at cfg2
+                           (DESIGN.md section 3), kept for A/B timing and cross-checks        */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */

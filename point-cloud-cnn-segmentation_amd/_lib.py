@@ -47,7 +47,7 @@ FLAG_NO_GLDS = 2
 FLAG_AW_FP8 = 4
 FLAG_C_FP8 = 8
 FLAG_POOL_SIGNED_W = 16
-FLAG_GLDS8 = 32
+FLAG_W4 = 32
 
 
 class WgradArgs(ct.Structure):

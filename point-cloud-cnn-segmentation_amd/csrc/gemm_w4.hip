@@ -606,7 +606,7 @@ void gemm_w4_kernel(pcs_gemm_args a, int tiles_per_scene, int tiles_per_chunk, i
 // form with bias, mask from the operand, no statistics / addend / sparse rows (those run
 // elsewhere); bf16, K % 128 == 0, Ncols % 256 == 0
 bool pcs_gemm_w4_applicable(const pcs_gemm_args &a) {
-  if (a.dtype != PCS_BF16 || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS | PCS_FLAG_GLDS8 | PCS_FLAG_AW_FP8)))
+  if (a.dtype != PCS_BF16 || !(a.flags & PCS_FLAG_W4) || (a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_NO_GLDS | PCS_FLAG_AW_FP8)))
     return false;
   if (a.prologue != PCS_PRO_RAW || a.K % (2 * BK) != 0 || a.Ncols % BN != 0 || a.stats) return false;
   // a chunk's row tiles addressed by 32-bit offsets (after pcs_gemm_geometry)

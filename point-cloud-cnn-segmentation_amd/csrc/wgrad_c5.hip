@@ -84,6 +84,9 @@ PCS_DEV bf16x8 tr_frag2(const char *p0, const char *p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// S1: also the column sums of dz5 (pcs_wgrad_args.dy_colsum; the opt-in four-wave global_feat
+// kernel's bn5 S1), a separate instantiation so that the default one keeps its registers
+template <bool S1>
 __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int64_t rows_per_split) {
   __shared__ __attribute__((aligned(16))) char lds[BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
     }
   };
 
-  const bool do_s1 = a.dy_colsum != nullptr;
+  constexpr bool do_s1 = S1;
   // x = relu(bn4(y4)) of step s into x buffer s & 1; rows past the slice -> 0
   const int o_yx = DZB + xrr * YROW + ((xlc ^ (xrr & 15)) << 4);
   const int o_xw = prow(xrr) * XR + xlc * 16;
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
     *reinterpret_cast<u32x4 *>(lds + OFF_X + (s & 1) * XB + o_xw) = out;
     // S1 (dy_colsum): a 17th 16-channel block of ones in the row's pad, zero past the slice,
     // so that the same transposed read gives the ones fragment with R's row (k) order
-    if (do_s1 && xlc < 2) {
+    if constexpr (do_s1) if (xlc < 2) {
       const uint32_t one = xrr < rem ? 0x3f803f80u : 0u;
       *reinterpret_cast<u32x4 *>(lds + OFF_X + (s & 1) * XB + prow(xrr) * XR + CIN * 2 + xlc * 16) =
           mk_u32x4(one, one, one, one);
@@ -222,7 +225,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
       for (int ob = 0; ob < OBW; ++ob)
         acc[ob][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u & 1], dt[ob], acc[ob][u], 0, 0, 0);
     }
-    if (do_s1) {   // uniform
+    if constexpr (do_s1) {
       const bf16x8 of = tr_frag2(xb + o_tx0 + 8 * 32, xb + o_tx1 + 8 * 32);
 #pragma unroll
       for (int ob = 0; ob < OBW; ++ob) acc1[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, dt[ob], acc1[ob], 0, 0, 0);
@@ -482,7 +485,10 @@ int pcs_wgrad_c5_splits(const pcs_wgrad_args &a) {
 int pcs_wgrad_c5_launch(const pcs_wgrad_args &a, int64_t rows_per_split, hipStream_t s) {
   if (rows_per_split % MS) return pcs_set_einval("pcs_wgrad", "conv5 R: rows per split must be a multiple of 32");
   const int nb = (int)(a.num_scenes * a.splits_per_scene) * (a.Cout / NB);
-  hipLaunchKernelGGL(wgrad_c5_kernel, dim3(nb), dim3(THREADS), 0, s, a, rows_per_split);
+  if (a.dy_colsum)
+    hipLaunchKernelGGL(wgrad_c5_kernel<true>, dim3(nb), dim3(THREADS), 0, s, a, rows_per_split);
+  else
+    hipLaunchKernelGGL(wgrad_c5_kernel<false>, dim3(nb), dim3(THREADS), 0, s, a, rows_per_split);
   PCS_CHECK_LAUNCH();
   return 0;
 }

@@ -790,11 +790,11 @@ class Engine:
                    L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
         elif self.dt == L.BF16 and not (self.flags & (L.FLAG_GENERIC | L.FLAG_NO_GLDS)):
             # LDS-DMA kernel without the max-pool rows (no ordinary global loads in its
-            # epilogue), then their sparse term (pcs_pool_rows_add).  The four-wave kernel
-            # (csrc/gemm_w4.hip) keeps no statistics: bn5's S1 = the column sums of dz5 as
-            # stored comes from conv5's R pass below (dy_colsum); the 8-wave kernel
-            # (PCS_FLAG_GLDS8) sums S1 in its epilogue and in pcs_pool_rows_add
-            w4 = not (self.flags & L.FLAG_GLDS8)
+            # epilogue), then their sparse term (pcs_pool_rows_add).  The 8-wave kernel sums
+            # S1 in its epilogue and in pcs_pool_rows_add; the opt-in four-wave kernel
+            # (PCS_FLAG_W4, csrc/gemm_w4.hip) keeps no statistics: bn5's S1 = the column sums
+            # of dz5 as stored then comes from conv5's R pass below (dy_colsum)
+            w4 = bool(self.flags & L.FLAG_W4)
             if w4:
                 s1_5 = torch.empty(1024, dtype=torch.float32, device=dev)
                 st5.zero_()

@@ -145,10 +145,10 @@ def test_cfg2_bf16_step_same_pool_rows_tight(cfg2_batch):
         assert torch.isfinite(a).all(), n
         worst[n] = 1 - float(a @ b / (a.norm() * b.norm() + 1e-30))
     print("cfg2 bf16 gradient 1-cos, fp32 pool rows:", {k: round(v, 5) for k, v in worst.items()})
-    bad = {k: v for k, v in worst.items() if v > W4_TIGHT_BOUND}
+    bad = {k: v for k, v in worst.items() if v > POOL_ROWS_TIGHT_BOUND}
     assert not bad, bad
 
 
 # measured at the bench size with the fp32 forward's pool rows (r04, see the test's print), plus
 # margin; the routing-dominated bound of test_cfg2_bf16_train_step_tracks_fp32 is 0.56
-W4_TIGHT_BOUND = 0.15
+POOL_ROWS_TIGHT_BOUND = 0.15

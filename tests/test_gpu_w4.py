@@ -1,6 +1,6 @@
 """The four-wave 32x32x16 LDS-DMA kernel for global_feat's bf16 GEMMs (csrc/gemm_w4.hip) through
 the C ABI, against torch fp64 on the same bf16 operands and against the 8-wave kernel
-(gemm_glds.hip, PCS_FLAG_GLDS8) on identical inputs:
+(gemm_glds.hip, the default; w4 is opt-in by PCS_FLAG_W4) on identical inputs:
 
 * folded input gradient (P:113 at P:254): dz = (a5 > 0) * (a5 H + c), bf16, the row tile's
   stores deferred into the next tile's K-tiles 1..4, the ragged last tile of a scene;
@@ -43,8 +43,8 @@ def test_dgrad_masked_bias(B, N, K, cps):
     A = A.to(DEV)
     H = (torch.randn(K, K, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
     c = (torch.randn(K, generator=g) * 0.1 + 1e-3 * torch.rand(K, generator=g)).to(DEV)
-    out = _dgrad(L, A, H, c, B, N, 0, cps)
-    old = _dgrad(L, A, H, c, B, N, L.FLAG_GLDS8, cps)
+    out = _dgrad(L, A, H, c, B, N, L.FLAG_W4, cps)
+    old = _dgrad(L, A, H, c, B, N, 0, cps)
     torch.cuda.synchronize()
     v = A.double() @ H.double().T + c.double()
     dz = torch.where(A.double() > 0, v, torch.zeros_like(v))
@@ -67,7 +67,7 @@ def test_dgrad_bias_exact():
     A = torch.relu(torch.randn(B * N, K, generator=g)).to(torch.bfloat16).to(DEV)
     H = torch.zeros(K, K, dtype=torch.bfloat16, device=DEV)
     c = (torch.randn(K, generator=g) * 3.0).to(DEV)
-    out = _dgrad(L, A, H, c, B, N, 0, 0)
+    out = _dgrad(L, A, H, c, B, N, L.FLAG_W4, 0)
     torch.cuda.synchronize()
     ref = torch.where(A > 0, c.to(torch.bfloat16)[None, :].expand(B * N, K), torch.zeros_like(A))
     assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
@@ -94,8 +94,8 @@ def test_forward_pool_signed(B, N, K, cps):
     gamma = torch.randn(Nc, generator=g).to(DEV)
     Ws = torch.empty_like(W)
     L.call("pcs_sign_rows", L.ptr(W), L.BF16, Nc, K, L.ptr(gamma), L.ptr(Ws), L.stream_ptr())
-    new = _pool(L, A, Ws, gamma, B, N, 0, cps)
-    old = _pool(L, A, Ws, gamma, B, N, L.FLAG_GLDS8, cps)
+    new = _pool(L, A, Ws, gamma, B, N, L.FLAG_W4, cps)
+    old = _pool(L, A, Ws, gamma, B, N, 0, cps)
     torch.cuda.synchronize()
     pos = gamma[None, :] > 0
     val = torch.where(pos, new[..., 0], new[..., 2])
@@ -135,7 +135,7 @@ def test_forward_pool_first_row_ties():
     A = base.repeat(N // 37 + 1, 1)[:N].to(torch.bfloat16).to(DEV)
     W = (torch.randn(Nc, K, generator=torch.Generator().manual_seed(4)) * 0.05).to(torch.bfloat16).to(DEV)
     gamma = torch.ones(Nc, device=DEV)
-    pool = _pool(L, A, W, gamma, B, N, 0, 1)
+    pool = _pool(L, A, W, gamma, B, N, L.FLAG_W4, 1)
     torch.cuda.synchronize()
     y = A.double() @ W.double().T
     first = y.argmax(0).int()
@@ -149,17 +149,17 @@ def test_bitwise_repeatable_and_applicability():
     A = torch.relu(torch.randn(B * N, K, generator=g)).to(torch.bfloat16).to(DEV)
     H = (torch.randn(K, K, generator=g) * 0.03).to(torch.bfloat16).to(DEV)
     c = torch.randn(K, generator=g).to(DEV)
-    outs = [_dgrad(L, A, H, c, B, N, 0, 2) for _ in range(4)]
+    outs = [_dgrad(L, A, H, c, B, N, L.FLAG_W4, 2) for _ in range(4)]
     torch.cuda.synchronize()
     for o in outs[1:]:
         assert torch.equal(o.view(torch.int16), outs[0].view(torch.int16))
     lib = L.load()
-    a, _ = _args(L, B, N, K, K, L.EPI_DGRAD, 0)
+    a, _ = _args(L, B, N, K, K, L.EPI_DGRAD, L.FLAG_W4)
     a.A, a.Yp, a.W = A.data_ptr(), A.data_ptr(), H.data_ptr()
     assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 1
     st = torch.empty(B * a.chunks_per_scene, K, 2, device=DEV)
     a.stats = st.data_ptr()                           # statistics: the 8-wave kernel's epilogue
     assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 0
     a.stats = None
-    a.flags = L.FLAG_GLDS8
+    a.flags = 0                                       # the default: the 8-wave kernel
     assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 0

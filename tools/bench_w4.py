@@ -1,7 +1,7 @@
 """Micro-benchmark of global_feat's two bf16 GEMMs at the cfg2 shape (M = 4 x 128^3 rows,
 1024 x 1024, a5-like ReLU operand on random data): the four-wave 32x32x16 kernel
 (csrc/gemm_w4.hip, the default) against the 8-wave 16x16x32 kernel (csrc/gemm_glds.hip,
-PCS_FLAG_GLDS8), alternating, several rounds in one process.  Prints ms and TF/s per variant
+the default), alternating, several rounds in one process.  Prints ms and TF/s per variant
 and the agreement of the two input gradients.  PCS_LIB selects another build (ablations)."""
 import ctypes as ct
 import os
@@ -71,12 +71,12 @@ def main():
         return lambda: L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
 
     variants = [
-        ("dgrad w4 (mask + store + bias)", dgrad(0, C1)),
-        ("dgrad glds8 (mask + store + bias)", dgrad(L.FLAG_GLDS8, C2)),
-        ("dgrad glds8 + S1 (the r03 training call)", dgrad(L.FLAG_GLDS8, C2, stats=True)),
+        ("dgrad w4 (mask + store + bias)", dgrad(L.FLAG_W4, C1)),
+        ("dgrad glds8 (mask + store + bias)", dgrad(0, C2)),
+        ("dgrad glds8 + S1 (the r03 training call)", dgrad(0, C2, stats=True)),
     ]
-    f4, p4 = fwd(0)
-    f8, p8 = fwd(L.FLAG_GLDS8)
+    f4, p4 = fwd(L.FLAG_W4)
+    f8, p8 = fwd(0)
     variants += [("fwd w4 (signed-W max-pool)", f4), ("fwd glds8 (signed-W max-pool)", f8)]
     if os.environ.get("W4_ONLY"):   # ablation builds: the two w4 calls only
         variants = [variants[0], variants[3]]

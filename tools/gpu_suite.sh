@@ -3,7 +3,7 @@
 set -e
 TAG=${1:-r02c}
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -v -rP --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
 tail -2 gpurun_out/pytest_gpu_$TAG.log
 timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
 tail -1 gpurun_out/smoke_$TAG.log
