@@ -45,10 +45,13 @@ enum {
                            W's rows (pcs_sign_rows) and bias by sign(es), so the pool keeps the
                            plain column max of acc (no multiply); es still names the sign.
                            Needs pool and es, no statistics (they would be of the signed y)  */
-  PCS_FLAG_W4 = 32      /* bf16 global_feat GEMMs (FWD signed-W pool / DGRAD without
+  PCS_FLAG_W4 = 32,     /* bf16 global_feat GEMMs (FWD signed-W pool / DGRAD without
                            statistics) on the 4-wave 32x32x16 kernel (gemm_w4.hip) instead of
                            the 8-wave 16x16x32 one (gemm_glds.hip): opt-in, slower at cfg2
                            (DESIGN.md section 3), kept for A/B timing and cross-checks        */
+  PCS_FLAG_SEG8 = 64    /* pcs_dgrad_wgrad_bn of seg_conv2 / seg_conv3: the 8-wave 128-column
+                           kernel (fused_seg.hip) instead of the 4-wave 256-column one
+                           (fused_seg4.hip), for A/B timing and cross-checks                 */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */

@@ -48,6 +48,7 @@ FLAG_AW_FP8 = 4
 FLAG_C_FP8 = 8
 FLAG_POOL_SIGNED_W = 16
 FLAG_W4 = 32
+FLAG_SEG8 = 64
 
 
 class WgradArgs(ct.Structure):

@@ -175,6 +175,9 @@ int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_
 bool pcs_gemm_w4_applicable(const pcs_gemm_args &a);
 int pcs_gemm_w4_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk, hipStream_t s);
 // fused seg_conv2 / seg_conv3 input + weight gradient (fused_seg.hip)
+bool pcs_seg4_applicable(const pcs_gemm_args &a);
+int64_t pcs_seg4_geometry(pcs_gemm_args *a);
+int pcs_seg4_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);
 bool pcs_seg_bwd_applicable(const pcs_gemm_args &a);
 int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a);
 int pcs_seg_bwd_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);

@@ -115,13 +115,27 @@ def test_dgrad_wgrad_rejects_other_shapes():
 @pytest.mark.parametrize("cout,cin,variant,B,N", [
     (64, 64, "plain", 3, 1000), (64, 64, "addend", 2, 4096 + 33), (128, 64, "plain", 4, 4096),
     (128, 64, "plain", 1, 64 * 40 + 5), (128, 64, "mask", 3, 777),
-    # seg_conv2 / seg_conv3 (LDS-DMA stream, csrc/fused_seg.hip): ragged slices, one-step slices
+    # seg_conv2 / seg_conv3 (LDS-DMA streams, csrc/fused_seg4.hip): ragged slices, one-step slices
     (256, 512, "mask", 2, 4096 + 33), (256, 512, "plain", 1, 70), (256, 512, "mask", 4, 65536 + 100),
     (128, 256, "mask", 3, 1000), (128, 256, "plain", 2, 64 * 40 + 5), (128, 256, "mask", 1, 31)])
 def test_dgrad_wgrad_bn_matches_torch(cout, cin, variant, B, N):
     """pcs_dgrad_wgrad_bn (conv2/3/4, seg_conv2/3) vs torch fp32 on the same bf16 inputs:
     dz' = (es*Yp + et > 0) * keep * ks * (dy W + addend), its per-chunk S1 / S2 statistics
-    (S2 = rstd * (sum dz' Yp - mean * S1)) and dW = dy^T x."""
+    (S2 = rstd * (sum dz' Yp - mean * S1)) and dW = dy^T x.  seg_conv2 / seg_conv3 run the
+    4-wave 256-column kernel (csrc/fused_seg4.hip) by default."""
+    _check_bn(cout, cin, variant, B, N, 0)
+
+
+@pytest.mark.parametrize("cout,cin,variant,B,N", [
+    (256, 512, "mask", 2, 4096 + 33), (256, 512, "plain", 1, 70), (128, 256, "mask", 3, 1000),
+    (128, 256, "plain", 2, 64 * 40 + 5)])
+def test_seg_bwd_8wave_matches_torch(cout, cin, variant, B, N):
+    """The same checks on the 8-wave 128-column kernel (csrc/fused_seg.hip, PCS_FLAG_SEG8)."""
+    import pcs_amd._lib as L
+    _check_bn(cout, cin, variant, B, N, L.FLAG_SEG8)
+
+
+def _check_bn(cout, cin, variant, B, N, flags):
     import pcs_amd._lib as L
     g = torch.Generator(device="cpu").manual_seed(cout * 31 + cin + N)
     M = B * N
@@ -144,7 +158,7 @@ def test_dgrad_wgrad_bn_matches_torch(cout, cin, variant, B, N):
     dW = torch.zeros(cout, cin, device=DEV)
     a = L.GemmArgs(num_scenes=B, scene_rows=N, K=cout, Ncols=cin, dtype=L.BF16, prologue=L.PRO_BWD,
                    epilogue=L.EPI_DGRAD, chunks_per_scene=0, A=dZ.data_ptr(), W=Wt.data_ptr(), C=out.data_ptr(),
-                   a_keep_scale=1.0, c_keep_scale=ks)
+                   a_keep_scale=1.0, c_keep_scale=ks, flags=flags)
     for k, v in dict(A2=Y, pa=al, pb=be, pc=ga, Yp=Yp, es=es, et=et, emean=emean, erstd=erstd,
                      c_mask=bits, addend=add).items():
         setattr(a, k, L.ptr(v))

@@ -36,7 +36,7 @@ def fused(B, N, cout, cin, reps, mask=True):
     keep = [v(cout), v(cout), v(cout), v(cin), v(cin), v(cin), v(cin)]
     a = L.GemmArgs(num_scenes=B, scene_rows=N, K=cout, Ncols=cin, dtype=L.BF16, prologue=L.PRO_BWD,
                    epilogue=L.EPI_DGRAD, chunks_per_scene=0, A=dz.data_ptr(), W=Wt.data_ptr(), C=out.data_ptr(),
-                   a_keep_scale=1.0, c_keep_scale=1.0 / 0.7)
+                   a_keep_scale=1.0, c_keep_scale=1.0 / 0.7, flags=int(os.environ.get("SEG_FLAGS", "0")))
     a.A2, a.pa, a.pb, a.pc, a.Yp = y.data_ptr(), *(t.data_ptr() for t in keep[:3]), yp.data_ptr()
     a.es, a.et, a.emean, a.erstd = (t.data_ptr() for t in keep[3:])
     if mask:

@@ -14,7 +14,7 @@ for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recurs
     with open(path) as f:
         for r in csv.DictReader(f):
             k = short(r["Kernel_Name"])
-            if "gemm" not in k:
+            if os.environ.get("PMC_FILTER", "gemm") not in k:
                 continue
             acc[k][r["Counter_Name"]].append((float(r["Counter_Value"]),
                                               (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
