@@ -96,3 +96,34 @@ def test_conv3d_argument_validation_without_gpu():
     assert lib.pcs_conv3d_wgrad_workspace(ct.byref(geom(Cin=32))) == -1000
     up = geom(Di=4, Hi=4, Wi=4, k=2, s=2, p=0, transposed=1)     # 4^3 -> 8^3
     assert lib.pcs_conv3d_wgrad_workspace(ct.byref(up)) > 0
+
+
+def test_seg_backward_geometry_without_gpu():
+    """seg_conv2 / seg_conv3 backward (pcs_dgrad_wgrad_bn): the default four-wave kernel's
+    slices (fused_seg4.hip: 16-row steps, one 256-column workgroup per CU) and the 8-wave
+    kernel's under PCS_FLAG_SEG8 (fused_seg.hip: 32-row steps, 128-column workgroups)."""
+    import pcs_amd._lib as L
+    lib = L.load()
+    for cout, cin in ((256, 512), (128, 256)):
+        for flags, nblk in ((0, cin // 256), (L.FLAG_SEG8, cin // 128)):
+            a = L.GemmArgs(num_scenes=4, scene_rows=128 ** 3, K=cout, Ncols=cin, dtype=L.BF16,
+                           prologue=L.PRO_BWD, epilogue=L.EPI_DGRAD, flags=flags)
+            nbytes = lib.pcs_dgrad_wgrad_bn_workspace(ct.byref(a))
+            cps = a.chunks_per_scene
+            assert nbytes == 4 * cps * cout * cin * 4
+            assert cps * 4 * nblk >= 256 and cps * 4 * nblk < 2 * 256   # about one workgroup per CU
+
+
+def test_w4_selection_without_gpu():
+    """The four-wave global_feat kernel is opt-in (PCS_FLAG_W4) and serves only the shapes it
+    was written for (host-side selection query, no kernel runs)."""
+    import pcs_amd._lib as L
+    lib = L.load()
+    a = L.GemmArgs(num_scenes=2, scene_rows=4096, K=1024, Ncols=1024, dtype=L.BF16,
+                   prologue=L.PRO_RAW, epilogue=L.EPI_DGRAD, flags=0)
+    a.A = a.Yp = a.W = a.C = 1 << 20   # (any non-null pointers: never dereferenced here)
+    assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 0
+    a.flags = L.FLAG_W4
+    assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 1
+    a.K = a.Ncols = 256                # K < 6 K-tiles: the deferred stores need K-tiles 1..4 and a spare
+    assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 0
