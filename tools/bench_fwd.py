@@ -17,15 +17,17 @@ def run(B, N, K, C, kind, reps):
     M = B * N
     yp = (torch.randn(M, K, device=dev) + 0.2).to(torch.bfloat16)
     W = (torch.randn(C, K, device=dev) / K ** 0.5).to(torch.bfloat16)
-    out = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    c8 = kind == "bnrelu8"   # conv5 with the fp8 e4m3 a5 store (cfg5)
+    out = torch.empty(M, C, device=dev, dtype=torch.uint8 if c8 else torch.bfloat16)
     v = lambda n: torch.rand(n, device=dev) + 0.5   # noqa: E731
     keep = [v(K), v(K) - 1.0, v(C), v(C) - 1.0, torch.randn(B, C, device=dev)]
-    epi = L.EPI_BNRELU if kind == "bnrelu" else L.EPI_FWD
+    epi = L.EPI_BNRELU if kind in ("bnrelu", "bnrelu8") else L.EPI_FWD
     a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=C, dtype=L.BF16, prologue=L.PRO_BNRELU, epilogue=epi,
                    chunks_per_scene=0, A=yp.data_ptr(), W=W.data_ptr(), C=out.data_ptr(),
-                   a_keep_scale=1.0 / 0.7 if kind == "mask" else 1.0, c_keep_scale=1.0)
+                   a_keep_scale=1.0 / 0.7 if kind == "mask" else 1.0, c_keep_scale=1.0,
+                   flags=L.FLAG_C_FP8 if c8 else 0)
     a.pa, a.pb = keep[0].data_ptr(), keep[1].data_ptr()
-    if kind == "bnrelu":
+    if kind in ("bnrelu", "bnrelu8"):
         a.es, a.et = keep[2].data_ptr(), keep[3].data_ptr()
     if kind == "bias":
         a.bias = keep[2].data_ptr()
@@ -47,7 +49,7 @@ def run(B, N, K, C, kind, reps):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    gb = M * (K + C) * 2 / 1e9 + (M * K / 8 / 1e9 if kind == "mask" else 0)
+    gb = M * (K * 2 + C * (1 if c8 else 2)) / 1e9 + (M * K / 8 / 1e9 if kind == "mask" else 0)
     print(f"{kind:7s} {K:4d}->{C:4d}: {ms:7.3f} ms  {gb / ms:6.2f} TB/s", flush=True)
 
 
@@ -57,6 +59,8 @@ def main():
     shapes = [(64, 512, "scene"), (512, 256, "mask"), (256, 128, "mask"), (128, 1024, "bnrelu")]
     if os.environ.get("FS_SHAPES") == "small":   # conv4, conv2 / conv3
         shapes = [(64, 128, "bias"), (64, 64, "bias")]
+    if os.environ.get("FS_SHAPES") == "conv5":   # conv5 with the bf16 and the fp8 a5 store
+        shapes = [(128, 1024, "bnrelu"), (128, 1024, "bnrelu8")]
     for K, C, kind in shapes:
         run(B, N, K, C, kind, reps)
 
