@@ -425,6 +425,8 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const bool live = full || rbase + 16 * rt + l16 < rem;
+      const float livef = live ? 1.f : 0.f;   // BNRELU: the column sums add d * livef by v_fma
+                                              // (exact: d or +0), no per-element select
       uint32_t pk[CT][2];
       if constexpr (FS_ABL == 2) {
 #pragma unroll
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
         }
         if constexpr (EPI == PCS_EPI_BNRELU) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s1[ct][r] += live ? d[r] : 0.f;
+          for (int r = 0; r < 4; ++r) s1[ct][r] = fmaf(d[r], livef, s1[ct][r]);
         } else {
           if (t == 0 && rt == 0) {   // uniform: the lane's first value shifts its sums
 #pragma unroll
@@ -470,7 +472,7 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
           }
         }
       }
-      nrow += live ? 1.f : 0.f;
+      nrow += livef;
       if constexpr (F::STG) {
         // 8-B granule 4 ct + g of the wave's row 16 rt + l16, at granule (4 ct + g) ^ (row & 15):
         // the 16 rows a lane group writes at one granule hit 16 distinct granules of the bank row
@@ -500,36 +502,33 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       }
     }
     if constexpr (C8) {
-      // rows back: lane = row 16 i + lane / 4, 16-B chunk c = lane % 4 (logical granules 4c .. 4c+3
-      // sit in physical chunk c ^ ((row >> 2) & 3), granule e at e ^ (row & 3))
+      // rows back: lane = row 16 i + lane / 4, logical granules 4c .. 4c+3 (c = lane % 4), granule
+      // G of a row at physical granule G ^ (row & 15): four 4-B reads at lane-constant offsets
+      // (row & 15 = lane / 4 for every i), no per-lane selects
       const int c = lane & 3;
 #pragma unroll
       for (int i = 0; i < F::RW / 16; ++i) {
         const int row = 16 * i + (lane >> 2);
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + F::OFF_STG + wid * (F::RW * 64) + row * 64 +
-                                                         ((c ^ ((row >> 2) & 3)) << 4));
-        const int x = row & 3;
+        const char *rp = lds + F::OFF_STG + wid * (F::RW * 64) + row * 64;
         u32x4 w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t a01 = (x & 1) ? v[e ^ 1] : v[e];
-          const uint32_t a23 = (x & 1) ? v[e ^ 3] : v[e ^ 2];
-          w[e] = (x & 2) ? a23 : a01;
-        }
+        for (int e = 0; e < 4; ++e) w[e] = *reinterpret_cast<const uint32_t *>(rp + (((4 * c + e) ^ (row & 15)) << 2));
         store16(o_stg + (uint32_t)(i * 16 * NCOLS), w);
       }
       o_stg += MS * NCOLS;
     } else if constexpr (F::STG == 1) {
-      // rows back from the wave's tile: lane = row 8 i + lane / 8, 16-B chunk lane % 8 (logical
-      // granules 2c, 2c+1 share physical chunk c ^ ((row >> 1) & 7), swapped on odd rows)
-      const int c = lane & 7;
+      // rows back from the wave's tile: lane = row 8 i + lane / 8, logical 8-B granules 2c, 2c+1
+      // (c = lane % 8) at physical granules G ^ (row & 15): two 8-B reads at lane offsets that
+      // depend on i only through its parity, no per-lane selects
+      const uint32_t gl = (uint32_t)((2 * (lane & 7)) ^ (lane >> 3)) << 3;   // granule 2c, even i
 #pragma unroll
       for (int i = 0; i < F::RW / 8; ++i) {
         const int row = 8 * i + (lane >> 3);
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(lds + F::OFF_STG + wid * (F::RW * 128) + row * 128 +
-                                                         ((c ^ ((row >> 1) & 7)) << 4));
-        const u32x4 w = (row & 1) ? mk_u32x4(v[2], v[3], v[0], v[1]) : v;
-        store16(o_stg + (uint32_t)(i * 8 * NCOLS * 2), w);
+        const char *rp = lds + F::OFF_STG + wid * (F::RW * 128) + row * 128;
+        const uint32_t go = (i & 1) ? gl ^ 64u : gl;   // row & 15 = lane / 8 + 8 (i & 1)
+        const uint2 lo8 = *reinterpret_cast<const uint2 *>(rp + go);
+        const uint2 hi8 = *reinterpret_cast<const uint2 *>(rp + (go ^ 8u));
+        store16(o_stg + (uint32_t)(i * 8 * NCOLS * 2), mk_u32x4(lo8.x, lo8.y, hi8.x, hi8.y));
       }
       o_stg += MS * NCOLS * 2;
     }

@@ -59,6 +59,8 @@ def main():
     shapes = [(64, 512, "scene"), (512, 256, "mask"), (256, 128, "mask"), (128, 1024, "bnrelu")]
     if os.environ.get("FS_SHAPES") == "small":   # conv4, conv2 / conv3
         shapes = [(64, 128, "bias"), (64, 64, "bias")]
+    if os.environ.get("FS_SHAPES") == "all":   # the four wide shapes and conv5's fp8 store
+        shapes.append((128, 1024, "bnrelu8"))
     if os.environ.get("FS_SHAPES") == "conv5":   # conv5 with the bf16 and the fp8 a5 store
         shapes = [(128, 1024, "bnrelu"), (128, 1024, "bnrelu8")]
     for K, C, kind in shapes:
