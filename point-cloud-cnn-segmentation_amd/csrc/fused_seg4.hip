@@ -338,7 +338,9 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
       const u32x4 out = pack_chunk(v);
-      const bool in = r < rem;
+      // (MASK: rows past the slice need no zeroing -- their keep bits read as 0 from the range-
+      // checked DMA, so their x, v and dW terms are 0 whatever dy holds)
+      const bool in = MASK || r < rem;
       *reinterpret_cast<u32x4 *>(st + o) = mk_u32x4(in ? out.x : 0u, in ? out.y : 0u, in ? out.z : 0u, in ? out.w : 0u);
     }
   };
@@ -424,7 +426,9 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       for (int r = 0; r < 4; ++r) {
         const float y = (r & 1) ? bf_hi(yv[ct][r >> 1]) : bf_lo(yv[ct][r >> 1]);
         const uint32_t wb = ct < 2 ? bb[r].x : bb[r].y;
-        const int keep = (4 * g + r < rem) ? __builtin_amdgcn_sbfe((int)wb, 16 * (ct & 1) + l16, 1) : 0;
+        // MASK: the keep bits of rows past the slice are 0 (range-checked DMA), no row test
+        const int kb = __builtin_amdgcn_sbfe((int)wb, 16 * (ct & 1) + l16, 1);
+        const int keep = (MASK || 4 * g + r < rem) ? kb : 0;
         if constexpr (SEG4_ABL & 4) {
           xv[r] = y;
           v[r] = dacc[ct][r];
