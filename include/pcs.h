@@ -559,6 +559,18 @@ int pcs_pad_scatter(const float *points, const void *labels, int32_t label_bytes
 int pcs_round_weight(const float *W, int64_t n, int32_t dtype, float *out, pcs_stream_t stream);
 
 /*
+ * Bridge of the bf16 / fp8 EVAL forward's fp32 trunk (BatchNorm eval, P:106-110 with
+ * model.eval(), P:313): a = relu(Y*s[k] + t[k]) of an fp32 pre-BN output Y [M, K] (row
+ * stride K), stored as bf16 for a bf16 GEMM.  split = 0: out [M, K] = bf16(a).  split = 1:
+ * out [M, 2K] = [hi | lo] with hi = bf16(a), lo = bf16(a - hi), so that a GEMM over 2K
+ * against [W | W] sees a to 16 significant bits (conv5's input a4 in eval: the trained
+ * network amplifies a4's bf16 rounding into logit-margin error).
+ * K % 8 == 0.
+ */
+int pcs_bnrelu_bf16(const float *Y, int64_t M, int32_t K, const float *s, const float *t, int32_t split,
+                    void *out, pcs_stream_t stream);
+
+/*
  * Point -> voxel path (north-star voxel vocabulary; build-defined, the
  * reference has no voxelisation: parity is against oracle/voxel_oracle.py, not the reference).
  * Voxel id of a point: ix = clamp(floor((x - lo_x) / (hi_x - lo_x) * G), 0, G-1) (fp32, in this

@@ -28,6 +28,12 @@ global_feat's weight and the folded H are e4m3 rows with one power-of-two scale 
 Gram-form weight gradient use the dequantized global_feat weight, as the HIP path does.
 ``return_logits=True`` also returns the logits (float32 [M, C]).
 
+``eval_logits(sd, x, sites)`` is the EVAL forward (BatchNorm running statistics, no dropout;
+P:98-133 under model.eval(), P:313) in float32 with a chosen set of bf16 rounding sites, as
+the HIP bf16 eval path (engine.Engine.forward, train=False) rounds them; ``eval_sites(trunk)``
+names the sites of that path with ``eval_trunk`` = "bf16" or "fp32" (tools/miou_attr.py
+attributes the eval logit error site by site).
+
 Memory is kept to the tensors the backward needs (about 9 KB per point plus a few [M, 1024]
 temporaries), so 4 scenes x 64^3 points run on a 64 GB host.
 """
@@ -296,3 +302,77 @@ def train_step(sd, x, labels, weight, masks, store="bf16", p=DROPOUT_P, return_l
     if return_logits:
         return loss, grads, logits
     return loss, grads
+
+
+# ------------------------------------------------------------------ eval forward
+EVAL_LAYERS = ("conv1", "conv2", "conv3", "conv4", "seg_conv1", "seg_conv2", "seg_conv3")
+_TRUNK = ("conv1", "conv2", "conv3", "conv4")
+
+
+def eval_sites(trunk="bf16"):
+    """bf16 rounding sites of the HIP eval forward.  Names: W<l> (GEMM weight), Y<l> (stored
+    pre-BN output), A<l> (relu(bn(Y_l)) as the next GEMM's operand; "Aconv2s" is seg_conv1's
+    copy of a2), "a5" (stored relu(bn5(y5))).  trunk="fp32": conv1..conv4 stored and computed
+    in fp32, seg_conv1 fed a bf16 a2, conv5 fed a 16-bit split of a4 (treated as exact)."""
+    s = {"a5", "Wglobal_feat", "Wconv5", "Aconv2s"}
+    for l in EVAL_LAYERS:
+        s |= {f"Y{l}", f"A{l}"}
+        if l != "conv1":
+            s.add(f"W{l}")
+    s.discard("Aseg_conv3")           # the head reads bn_seg3's output in fp32
+    if trunk == "fp32":
+        s -= {f"{k}{l}" for l in _TRUNK for k in "YAW"}
+    return frozenset(s)
+
+
+def eval_logits(sd, x, sites, fp8=False):
+    """float32 eval forward with the bf16 rounding ``sites`` (eval_sites); logits [B, N, C].
+    Stored pre-BN outputs omit the conv bias as the HIP path's do (seg_conv1's per-scene bias
+    centred over the scenes).  fp8=True: a5 in e4m3 and global_feat's weight as e4m3 rows with
+    one power-of-two scale each (the compute dtype "fp8"), whatever ``sites`` holds for them."""
+    def R(a, site):
+        if fp8 and site == "a5":
+            return round_e4m3(a)
+        if fp8 and site == "Wglobal_feat":
+            return quant_rows_e4m3(a)
+        return round_bf16(a) if site in sites else np.ascontiguousarray(a, dtype=F32)
+    B, N, D = x.shape
+    M = B * N
+    X = x.reshape(M, D).astype(F32)
+    W = {n: _w(sd, n, F32) for n in ("conv1", "conv2", "conv3", "conv4", "conv5", "global_feat",
+                                    "seg_conv1", "seg_conv2", "seg_conv3", "seg_conv4")}
+
+    def coefs(bn, off):
+        g = sd[f"{bn}.weight"].astype(np.float64)
+        rm = sd[f"{bn}.running_mean"].astype(np.float64)
+        sc = g / np.sqrt(sd[f"{bn}.running_var"].astype(np.float64) + BN_EPS)
+        return sc.astype(F32), (sd[f"{bn}.bias"].astype(np.float64) - (rm - off) * sc).astype(F32)
+
+    def layer(A, conv, bn, Wt):
+        Y = R(A @ Wt.T, f"Y{conv}")
+        return Y, *coefs(bn, sd[f"{conv}.bias"].astype(np.float64))
+
+    def relu_bn(Y, s, t):
+        return np.maximum(Y * s + t, F32(0))
+
+    Y, s, t = layer(X, "conv1", "bn1", W["conv1"])
+    Y, s, t = layer(R(relu_bn(Y, s, t), "Aconv1"), "conv2", "bn2", R(W["conv2"], "Wconv2"))
+    A2 = relu_bn(Y, s, t)
+    Y, s, t = layer(R(A2, "Aconv2"), "conv3", "bn3", R(W["conv3"], "Wconv3"))
+    Y, s, t = layer(R(relu_bn(Y, s, t), "Aconv3"), "conv4", "bn4", R(W["conv4"], "Wconv4"))
+    A4 = R(relu_bn(Y, s, t), "Aconv4")
+    s5, t5 = coefs("bn5", sd["conv5.bias"].astype(np.float64))
+    a5 = R(relu_bn(A4 @ R(W["conv5"], "Wconv5").T, s5, t5), "a5")          # fp32 accumulators
+    sg, tg = coefs("bn_global", sd["global_feat.bias"].astype(np.float64))
+    zg = ((a5 @ R(W["global_feat"], "Wglobal_feat").T) * sg + tg).reshape(B, N, -1)
+    g = np.maximum(zg.max(axis=1), 0).astype(np.float64)                   # P:114
+    del zg
+    sb = g @ W["seg_conv1"][:, 64:].T.astype(np.float64) + sd["seg_conv1.bias"]   # [B, 512]
+    soff = sb.mean(axis=0)
+    a2s = R(A2, "Aconv2" if "Aconv2" in sites else "Aconv2s")
+    Ys1 = R((a2s @ R(W["seg_conv1"][:, :64], "Wseg_conv1").T).reshape(B, N, -1)
+            + (sb - soff)[:, None, :].astype(F32), "Yseg_conv1").reshape(M, -1)
+    s, t = coefs("bn_seg1", soff)
+    Y, s, t = layer(R(relu_bn(Ys1, s, t), "Aseg_conv1"), "seg_conv2", "bn_seg2", R(W["seg_conv2"], "Wseg_conv2"))
+    Y, s, t = layer(R(relu_bn(Y, s, t), "Aseg_conv2"), "seg_conv3", "bn_seg3", R(W["seg_conv3"], "Wseg_conv3"))
+    return (relu_bn(Y, s, t) @ W["seg_conv4"].T + sd["seg_conv4.bias"].astype(F32)).reshape(B, N, -1)

@@ -167,6 +167,7 @@ SIGNATURES = [
     ("pcs_dgrad_wgrad_bn_workspace", _i64, [ct.POINTER(GemmArgs)]),
     ("pcs_dgrad_wgrad_bn", ct.c_int, [ct.POINTER(GemmArgs), _vp, _vp, _i64, _vp]),
     ("pcs_round_weight", ct.c_int, [_vp, _i64, _i32, _vp, _vp]),
+    ("pcs_bnrelu_bf16", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     ("pcs_voxel_ids", ct.c_int, [_vp, _i64, _i32, _f, _f, _f, _f, _f, _f, _vp, _vp]),
     ("pcs_voxelize_workspace", _i64, [_i64]),
     ("pcs_voxelize", ct.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _f, _f, _f, _f, _f, _f, _i32, _vp, _i64,

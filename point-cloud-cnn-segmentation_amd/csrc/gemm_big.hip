@@ -318,15 +318,20 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       }
     }
 
-    // phase 1: tile -> LDS (bf16)
+    // phase 1: tile -> LDS (bf16; fp8 store: e4m3 bytes rounded once from fp32, in the first
+    // half of each tile row)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = wm * 128 + i * 16 + lrow;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = wn * 64 + j * 16 + lcol;
-        *reinterpret_cast<uint2 *>(lds + m * CROW + n * 2) =
-            make_uint2(pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3]));
+        if constexpr (C8)
+          *reinterpret_cast<uint32_t *>(lds + m * CROW + n) =
+              pack4fp8(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        else
+          *reinterpret_cast<uint2 *>(lds + m * CROW + n * 2) =
+              make_uint2(pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3]));
       }
     }
     __syncthreads();
@@ -434,11 +439,9 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       for (int p = 0; p < NPASS; ++p) {
         const int rr = er0 + RPP * p;
         if (rr < valid) {
-          const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
           if constexpr (C8) {   // fp8 e4m3 activation (8 B)
-            float v[EPC];
-            unpack_chunk(raw, v);
-            const uint32_t lo = pack4fp8(v[0], v[1], v[2], v[3]), hi = pack4fp8(v[4], v[5], v[6], v[7]);
+            const uint2 w8 = *reinterpret_cast<const uint2 *>(lds + rr * CROW + ecc * 8);
+            const uint32_t lo = w8.x, hi = w8.y;
             __builtin_nontemporal_store((uint64_t)hi << 32 | lo,
                                         reinterpret_cast<uint64_t *>(reinterpret_cast<fp8_t *>(a.C) +
                                                                      (row_base + rr) * Ncols + ecol));
@@ -450,6 +453,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
               }
             }
           } else {
+            const u32x4 raw = *reinterpret_cast<const u32x4 *>(lds + rr * CROW + ecc * 16);
             st16(Cg + (row_base + rr) * Ncols + ecol, raw);
             if constexpr (EPI == PCS_EPI_BNRELU) {
               if (do_stats) {   // column sums of the stored (bf16-rounded) activation
@@ -567,7 +571,9 @@ int pcs_gemm_big_launch(const pcs_gemm_args &g, int tps, int tpc, hipStream_t s)
       return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_FWD, true>(g, tps, tpc, s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_FWD, false>(g, tps, tpc, s);
     case PCS_EPI_BNRELU:
-      if (g.prologue == PCS_PRO_RAW) return launch<PCS_PRO_RAW, PCS_EPI_BNRELU, false>(g, tps, tpc, s);
+      if (g.prologue == PCS_PRO_RAW)   // (fp8 store: the eval path's split a4, pcs_bnrelu_bf16)
+        return (g.flags & PCS_FLAG_C_FP8) ? launch<PCS_PRO_RAW, PCS_EPI_BNRELU, false, true>(g, tps, tpc, s)
+                                          : launch<PCS_PRO_RAW, PCS_EPI_BNRELU, false>(g, tps, tpc, s);
       if (g.flags & PCS_FLAG_C_FP8) return launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, false, true>(g, tps, tpc, s);
       return g.a_mask ? launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, true>(g, tps, tpc, s)
                       : launch<PCS_PRO_BNRELU, PCS_EPI_BNRELU, false>(g, tps, tpc, s);

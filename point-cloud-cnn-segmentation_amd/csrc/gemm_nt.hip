@@ -654,9 +654,11 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if ((a.flags & PCS_FLAG_AW_FP8) && !(wide_class(a) && pcs_gemm_glds_applicable(a)))
     return pcs_set_einval("pcs_gemm", "fp8 operands (PCS_FLAG_AW_FP8) need the LDS-DMA kernel: bf16 C, RAW prologue, "
                                       "K % 256 == 0, Ncols % 256 == 0, w_scale, FWD (no C) or folded DGRAD");
-  if ((a.flags & PCS_FLAG_C_FP8) && !(a.epilogue == PCS_EPI_BNRELU && a.prologue == PCS_PRO_BNRELU && !a.a_mask &&
+  if ((a.flags & PCS_FLAG_C_FP8) && !(a.epilogue == PCS_EPI_BNRELU &&
+                                      (a.prologue == PCS_PRO_BNRELU || a.prologue == PCS_PRO_RAW) && !a.a_mask &&
                                       wide_class(a) && (pcs_gemm_wres_applicable(a) || pcs_gemm_big_applicable(a))))
-    return pcs_set_einval("pcs_gemm", "fp8 output (PCS_FLAG_C_FP8) needs PRO_BNRELU (no dropout) + EPI_BNRELU on the bf16 256-wide kernel");
+    return pcs_set_einval("pcs_gemm", "fp8 output (PCS_FLAG_C_FP8) needs PRO_BNRELU (no dropout) or PRO_RAW + EPI_BNRELU "
+                                      "on the bf16 256-wide kernel");
   if ((a.flags & PCS_FLAG_POOL_SIGNED_W) && !(a.epilogue == PCS_EPI_FWD && a.pool && a.es && !a.stats &&
                                              wide_class(a) && pcs_gemm_glds_applicable(a)))
     return pcs_set_einval("pcs_gemm", "PCS_FLAG_POOL_SIGNED_W needs EPI_FWD with pool and es, no statistics, on the "

@@ -1486,3 +1486,48 @@ extern "C" int pcs_round_weight(const float *W, int64_t n, int32_t dtype, float 
   PCS_CHECK_LAUNCH();
   return 0;
 }
+
+namespace {
+// one thread per 8 channels of a row: two 16-B loads of Y, one (two, split) 16-B bf16 stores
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void bnrelu_bf16_kernel(const float *__restrict__ Y, int64_t M, int K,
+                                                         const float *__restrict__ s, const float *__restrict__ t,
+                                                         bf16_t *__restrict__ out) {
+  const int K8 = K >> 3;
+  const int64_t n = M * K8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / K8;
+    const int k = (int)(i - m * K8) * 8;
+    const float4 y0 = *reinterpret_cast<const float4 *>(Y + m * K + k);
+    const float4 y1 = *reinterpret_cast<const float4 *>(Y + m * K + k + 4);
+    const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    float hi[8], lo[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float a = fmaxf(fmaf(yv[e], s[k + e], t[k + e]), 0.f);
+      hi[e] = bf2f(pack2bf(a, 0.f) & 0xffffu);
+      lo[e] = a - hi[e];   // exact in fp32
+    }
+    const int64_t ld = SPLIT ? 2 * (int64_t)K : K;
+    *reinterpret_cast<u32x4 *>(out + m * ld + k) = pack_chunk(hi);
+    if constexpr (SPLIT) *reinterpret_cast<u32x4 *>(out + m * ld + K + k) = pack_chunk(lo);
+  }
+}
+}  // namespace
+
+extern "C" int pcs_bnrelu_bf16(const float *Y, int64_t M, int32_t K, const float *s, const float *t, int32_t split,
+                               void *out, pcs_stream_t stream) {
+  if (!Y || !s || !t || !out || M < 0 || K <= 0 || K % 8 != 0)
+    return pcs_set_einval("pcs_bnrelu_bf16", "bad arguments (K must be a positive multiple of 8)");
+  if (M == 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nb = (int)pcs_min64(blocks_for(M * (K / 8), 256), 8192);
+  if (split)
+    hipLaunchKernelGGL(bnrelu_bf16_kernel<true>, dim3(nb), dim3(256), 0, st, Y, M, K, s, t,
+                       reinterpret_cast<bf16_t *>(out));
+  else
+    hipLaunchKernelGGL(bnrelu_bf16_kernel<false>, dim3(nb), dim3(256), 0, st, Y, M, K, s, t,
+                       reinterpret_cast<bf16_t *>(out));
+  PCS_CHECK_LAUNCH();
+  return 0;
+}

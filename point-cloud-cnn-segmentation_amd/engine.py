@@ -158,8 +158,10 @@ class Saved:
 class Engine:
     """Launches the PointNetSegmentation kernels for one compute dtype and device."""
 
-    def __init__(self, num_classes: int, dtype: str = "fp32", input_dim: int = 4):
+    def __init__(self, num_classes: int, dtype: str = "fp32", input_dim: int = 4, eval_trunk: str = "fp32"):
         check_dims(num_classes, input_dim)
+        if eval_trunk not in ("fp32", "bf16"):
+            raise ValueError(f"eval_trunk must be 'fp32' or 'bf16', got {eval_trunk!r}")
         self.input_dim = input_dim
         self.C = num_classes
         self.dtype = dtype
@@ -168,6 +170,12 @@ class Engine:
         # quantized with one E8M0 scale each, pcs_quant_fp8_rows), forward and input gradient
         self.fp8 = dtype == "fp8"
         self.a5_dt = L.FP8 if self.fp8 else self.dt
+        # bf16 / fp8 EVAL forward: the narrow trunk conv1..conv4 (<= 128 channels, 10 % of the
+        # activation bytes) stored and computed in fp32, conv5 on a 16-bit split of a4
+        # (pcs_bnrelu_bf16); the trained network amplifies the trunk's bf16 rounding into
+        # logit-margin error that moves mIoU by > 1e-3.  "bf16" keeps
+        # the whole eval forward on bf16 storage (the training step's precision).
+        self.eval_trunk = eval_trunk
         self.layout = param_layout(num_classes, input_dim)          # registration order
         self.numel = {n: int(torch.Size(s).numel()) for n, s in self.layout}
         self.offsets, self.total_params = flat_offsets(num_classes, input_dim)   # flat order
@@ -210,11 +218,12 @@ class Engine:
             st = self._side.setdefault(dev, torch.cuda.Stream(device=dev))
         return st
 
-    def geometry(self, B, N, K, ncols, pro=L.PRO_BNRELU, epi=L.EPI_FWD):
+    def geometry(self, B, N, K, ncols, pro=L.PRO_BNRELU, epi=L.EPI_FWD, dtype=None):
         """(chunks_per_scene, rows_per_chunk) of the kernel pcs_gemm picks for these args."""
-        key = (B, N, K, ncols, pro, epi, self.flags)
+        dtype = self.dt if dtype is None else dtype
+        key = (B, N, K, ncols, pro, epi, self.flags, dtype)
         if key not in self._geo:
-            a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
+            a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=dtype,
                            prologue=pro, epilogue=epi, chunks_per_scene=0, flags=self.flags)
             rpc = L.load().pcs_gemm_geometry(ct.byref(a))
             if rpc <= 0:
@@ -277,8 +286,9 @@ class Engine:
 
     def _gemm(self, B, N, K, ncols, pro, epi, A, W, C, **kw):
         tag = kw.pop("tag", None)
-        cps, _ = self.geometry(B, N, K, ncols, pro, epi)
-        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=self.dt,
+        dtype = kw.pop("dtype", self.dt)
+        cps, _ = self.geometry(B, N, K, ncols, pro, epi, dtype)
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=K, Ncols=ncols, dtype=dtype,
                        prologue=pro, epilogue=epi, chunks_per_scene=cps,
                        flags=self.flags | kw.pop("extra_flags", 0),
                        A=L.ptr(A), W=L.ptr(W), C=L.ptr(C),
@@ -391,14 +401,17 @@ class Engine:
 
         # Stored pre-BN activations omit the conv bias (BN cancels it exactly; it only
         # shifts running_mean), which keeps them centred: full precision in fp32/bf16.
+        # bf16 / fp8 eval: conv1..conv4 in fp32 (self.eval_trunk, see __init__)
+        trunk32 = not train and self.dt == L.BF16 and self.eval_trunk == "fp32"
+        tdt = L.F32 if trunk32 else self.dt
         # conv1 (K=4)
-        y1 = self._empty(M, 64, device=dev)
+        y1 = self._empty(M, 64, device=dev, dtype=torch.float32 if trunk32 else None)
         a = L.GemmArgs(num_scenes=B, scene_rows=N, K=D, Ncols=64, dtype=L.F32, chunks_per_scene=0,
                        flags=L.FLAG_GENERIC)
         rpc = L.load().pcs_gemm_geometry(ct.byref(a))    # conv1: generic 128-row geometry
         cps = a.chunks_per_scene
         st = torch.empty(B * cps, 64, 2, dtype=torch.float32, device=dev) if train else None
-        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=D, Ncols=64, dtype=self.dt,
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=D, Ncols=64, dtype=tdt,
                        chunks_per_scene=cps, A=L.ptr(x), W=L.ptr(P["conv1.weight"]),
                        C=L.ptr(y1), bias=None, stats=L.ptr(st))
         self._launch("fwd:conv1", "pcs_conv1_fwd", ct.byref(a), s)
@@ -407,18 +420,36 @@ class Engine:
                                          offset=P["conv1.bias"])
 
         def layer(conv, src_conv, src_bn, K, ncols, bnname, offset, **kw):
-            y = self._empty(M, ncols, device=dev)
             st, cps, rpc = stats_buf(K, ncols) if train else (None, 0, 0)
-            self._gemm(B, N, K, ncols, L.PRO_BNRELU, L.EPI_FWD, sv.ys[src_conv], wc[conv][0], y,
-                       stats=st, tag=f"fwd:{conv}", **bnrelu(src_bn), **kw)
+            if kw.get("dtype") == L.F32:       # the eval path's fp32 trunk
+                y = self._empty(M, ncols, device=dev, dtype=torch.float32)
+                self._gemm(B, N, K, ncols, L.PRO_BNRELU, L.EPI_FWD, sv.ys[src_conv], P[f"{conv}.weight"], y,
+                           stats=st, tag=f"fwd:{conv}", **bnrelu(src_bn), **kw)
+            elif "A_raw" in kw:                # bf16 GEMM on an activation bridged from the trunk
+                y = self._empty(M, ncols, device=dev)
+                self._gemm(B, N, K, ncols, L.PRO_RAW, L.EPI_FWD, kw.pop("A_raw"), wc[conv][0], y,
+                           stats=st, tag=f"fwd:{conv}", **kw)
+            else:
+                y = self._empty(M, ncols, device=dev)
+                self._gemm(B, N, K, ncols, L.PRO_BNRELU, L.EPI_FWD, sv.ys[src_conv], wc[conv][0], y,
+                           stats=st, tag=f"fwd:{conv}", **bnrelu(src_bn), **kw)
             sv.ys[conv] = y
             sv.bn[bnname] = self._bn_finalize(bnname, st, B, N, ncols, cps, rpc, P, bufs, train,
                                               dev, offset=offset)
             return y
 
-        layer("conv2", "conv1", "bn1", 64, 64, "bn2", P["conv2.bias"])
-        layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"])
-        layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"])
+        tkw = {"dtype": L.F32} if trunk32 else {}
+        layer("conv2", "conv1", "bn1", 64, 64, "bn2", P["conv2.bias"], **tkw)
+        layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"], **tkw)
+        layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"], **tkw)
+
+        def bridge(conv, bn, K, split):
+            """relu(bn(Y)) of an fp32 trunk output as bf16 (split: [hi | lo], pcs_bnrelu_bf16)."""
+            out = self._empty(M, 2 * K if split else K, device=dev)
+            c = sv.bn[bn]
+            L.call("pcs_bnrelu_bf16", L.ptr(sv.ys[conv]), M, K, L.ptr(c.scale), L.ptr(c.shift), int(split),
+                   L.ptr(out), s)
+            return out
 
         # conv5 (P:110): bn5's statistics first, then the GEMM with bn5 + ReLU applied in the
         # epilogue, storing a5 = relu(bn5(y5)) for global_feat.  fp32: a statistics-only pass
@@ -445,9 +476,15 @@ class Engine:
         if train and self._raw_gram():
             cps5c, _ = self.geometry(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU)
             sv.a5_colsum = torch.empty(B * cps5c, 1024, 2, dtype=torch.float32, device=dev)
-        self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU, sv.ys["conv4"], wc["conv5"][0], a5,
-                   es=c5.scale, et=c5.shift, stats=sv.a5_colsum, tag="fwd:conv5",
-                   extra_flags=L.FLAG_C_FP8 if self.fp8 else 0, **bnrelu("bn4"))
+        if trunk32:
+            # a4 to 16 significant bits: [hi | lo] (K = 256) against [W5 | W5]
+            W5s = torch.cat([wc["conv5"][0], wc["conv5"][0]], dim=1)
+            self._gemm(B, N, 256, 1024, L.PRO_RAW, L.EPI_BNRELU, bridge("conv4", "bn4", 128, True), W5s, a5,
+                       es=c5.scale, et=c5.shift, tag="fwd:conv5", extra_flags=L.FLAG_C_FP8 if self.fp8 else 0)
+        else:
+            self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU, sv.ys["conv4"], wc["conv5"][0], a5,
+                       es=c5.scale, et=c5.shift, stats=sv.a5_colsum, tag="fwd:conv5",
+                       extra_flags=L.FLAG_C_FP8 if self.fp8 else 0, **bnrelu("bn4"))
         sv.ys["a5"] = a5
 
         # global_feat (P:113-114): a5 W^T with max-pool partials (and, on the fp32 / generic
@@ -523,7 +560,11 @@ class Engine:
         L.call("pcs_scene_gemv", L.ptr(sv.g), B, 1024, L.ptr(Ws1), Ws1.shape[1], 64,
                L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), L.ptr(soff), s)
         sv.sbias_s1 = sbias   # the stored Y'_seg1 = a2 W_l^T + sbias[b] (the folded backward)
-        layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", soff, scene_bias=sbias)
+        if trunk32:
+            layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", soff, scene_bias=sbias,
+                  A_raw=bridge("conv2", "bn2", 64, False))
+        else:
+            layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", soff, scene_bias=sbias)
 
         # dropout keep bits (P:124, P:126)
         if train:

@@ -86,9 +86,15 @@ class PointNetSegmentation(nn.Module):
     (the bf16 path with the 1024-wide layer in e4m3: conv5 stores a5 as fp8 and global_feat's
     forward, input gradient and Gram run on MX-scaled fp8 MFMA with per-row E8M0 weight
     scales; fp32 accumulation and BN statistics throughout).
+
+    ``eval_trunk`` (bf16 / fp8 only): precision of the EVAL forward's narrow trunk conv1..conv4.
+    ``"fp32"`` (default) stores and computes it in fp32 and feeds conv5 a 16-bit split of a4:
+    with trained weights, bf16 storage there moves mIoU by more than the north star's 1e-3
+    (DESIGN.md section 4).  ``"bf16"`` keeps the eval forward on the training step's bf16
+    storage.  Training always uses the compute dtype throughout.
     """
 
-    def __init__(self, num_classes, input_dim=4, *, compute_dtype: str = "fp32"):
+    def __init__(self, num_classes, input_dim=4, *, compute_dtype: str = "fp32", eval_trunk: str = "fp32"):
         super().__init__()
         # Point-wise MLPs for feature extraction (P:70-74)
         self.conv1 = nn.Conv1d(input_dim, 64, 1)
@@ -114,6 +120,7 @@ class PointNetSegmentation(nn.Module):
         self.num_classes = num_classes
         self.input_dim = input_dim
         self.compute_dtype = compute_dtype
+        self.eval_trunk = eval_trunk
         check_dims(num_classes, input_dim)   # fail at construction, not at the first forward
         # created lazily (it loads libpcs.so); it holds no per-call state (only a geometry
         # cache), so DataParallel replicas may share it
@@ -123,8 +130,9 @@ class PointNetSegmentation(nn.Module):
 
     # ---------------------------------------------------------------- internals
     def _engine(self) -> Engine:
-        if self._eng is None or self._eng.dtype != self.compute_dtype:
-            self._eng = Engine(self.num_classes, self.compute_dtype, self.input_dim)
+        if (self._eng is None or self._eng.dtype != self.compute_dtype
+                or self._eng.eval_trunk != self.eval_trunk):
+            self._eng = Engine(self.num_classes, self.compute_dtype, self.input_dim, self.eval_trunk)
         return self._eng
 
     def _params(self):

@@ -49,3 +49,20 @@ def test_e4m3_rounding_matches_torch():
     e = np.ceil(np.log2(mx / 448.0))
     ref = torch.from_numpy(W * np.exp2(-e)[:, None].astype(np.float32)).to(torch.float8_e4m3fn).double().numpy()
     assert np.array_equal(quant_rows_e4m3(W), (ref * np.exp2(e)[:, None]).astype(np.float32))
+
+
+def test_eval_logits_without_rounding_is_the_reference_eval():
+    """eval_logits with no rounding site is the reference's eval forward (P:98-133 under
+    model.eval()): the reference-written eval fixture's logits and the fp64 oracle."""
+    g = load("eval_c2_bnrand")
+    sd, pts, _, _, _ = inputs(g)
+    l64, _ = orc.forward(sd, pts, train=False)
+    l32 = emu.eval_logits(sd, pts, frozenset())
+    scale = np.abs(l64).max()
+    assert np.abs(l32 - l64).max() <= 1e-4 * scale
+    assert np.abs(l32 - np.asarray(g["logits"])).max() <= 1e-4 * scale
+    # the site sets: the fp32 trunk drops exactly conv1..conv4's sites, bf16 storage is lossy
+    b, f = emu.eval_sites("bf16"), emu.eval_sites("fp32")
+    assert b - f == {f"{k}conv{i}" for k in "YA" for i in (1, 2, 3, 4)} | {"Wconv2", "Wconv3", "Wconv4"}
+    lb = emu.eval_logits(sd, pts, b)
+    assert 0 < np.abs(lb - l64).max() <= 0.1 * scale

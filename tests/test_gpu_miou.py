@@ -10,16 +10,15 @@
 
 Seeded random weights predict one class almost everywhere, which makes mIoU uninformative, so
 the main case first trains the model for 300 fused steps on the device (weighted CE, P:216) and
-then scores THOSE weights on both sides.  fp32 is held to 1e-3; bf16 (the bench dtype) to the
-change its flipped near-boundary points account for (the test's comment).
+then scores THOSE weights on both sides.  fp32 and bf16 are both held to the north star's 1e-3.
 
-Why 300 steps: after only 40 the model is barely past chance and keeps dozens of val points
-within a few 1e-2 of the decision boundary; bf16 storage then flips 48 of 27K points (oracle
-logit margin at the flips: median 2.2e-2, max 5.4e-2) and mIoU moves 1.2e-3, while fp32 flips
-none.  After 300 steps bf16 flips 16 points and mIoU moves 1.3e-4 (tools/miou_margin.py,
-profiles/miou_margin_r02.log).  The flipped points are additionally required to lie within the
-bf16 path's logit error of the boundary (oracle margin < MARGIN), which is what separates
-storage rounding from a kernel error."""
+bf16 here is the bf16 model's eval forward as shipped (eval_trunk="fp32": conv1..conv4 in
+fp32, conv5 fed a 16-bit split of a4; every layer from conv5 on in bf16).  On these trained
+weights bf16 STORAGE of the narrow trunk alone moves mIoU by 1.27e-3 (81 flipped points,
+logit-margin error p50 5.6e-2): the numpy restatement of that storage
+(oracle/bf16_emulation.eval_logits) reproduces the device's error to p50 1.1e-3, so it is the
+arithmetic's, not a kernel's (tools/miou_attr.py).
+test_bf16_storage_eval_is_its_emulation pins exactly that and reports the number."""
 import numpy as np
 import pytest
 import torch
@@ -30,7 +29,6 @@ from golden_util import inputs, load
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 TOL = 1e-3
-MARGIN = 0.25   # floor of the flip bound (bf16 margin at the flips: max 0.17 / 0.42 on two trajectories)
 
 
 def _sk_miou(pred, lab):
@@ -39,10 +37,10 @@ def _sk_miou(pred, lab):
     return float(jaccard_score(lab[v], pred[v], average="macro"))
 
 
-def _device_eval(sd, pts, lab, C, dtype):
+def _device_eval(sd, pts, lab, C, dtype, eval_trunk="fp32"):
     from pcs_amd.metrics import ConfusionMeter
     from pcs_amd.model import PointNetSegmentation
-    m = PointNetSegmentation(C, compute_dtype=dtype).to(DEV)
+    m = PointNetSegmentation(C, compute_dtype=dtype, eval_trunk=eval_trunk).to(DEV)
     m.load_state_dict({k: torch.as_tensor(np.array(v)) for k, v in sd.items()})
     m.eval()
     meter = ConfusionMeter(C, DEV)
@@ -88,44 +86,66 @@ def trained():
     return C, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_miou_of_trained_weights_matches_oracle(trained, dtype):
-    """Ragged val batch (pads labelled -1 enter BN / max-pool as in collate_fn) scored with
-    the trained weights by the device path and by the fp64 oracle."""
+def _val_case(trained):
     import pcs_amd.data as pdata
     C, sd = trained
     pts, lab, _ = pdata.synthetic_batch(4242, [8192, 6000, 8192, 5000], C, grid=32)
     logits, _ = orc.forward({k: np.asarray(v, np.float64) if v.dtype.kind == "f" else v
                              for k, v in sd.items()}, pts, train=False)
+    return C, sd, pts, lab, logits
+
+
+def _margin(lg):
+    return (lg[..., 1] - lg[..., 0]).reshape(-1)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_miou_of_trained_weights_matches_oracle(trained, dtype):
+    """Ragged val batch (pads labelled -1 enter BN / max-pool as in collate_fn) scored with
+    the trained weights by the device path and by the fp64 oracle."""
+    C, sd, pts, lab, logits = _val_case(trained)
     pred = logits.argmax(-1).reshape(-1)
     v = lab.reshape(-1) >= 0
     hist = np.bincount(pred[v], minlength=C)
     ref = _sk_miou(pred, lab.reshape(-1))
     got, dpred, dlog = _device_eval(sd, pts, lab, C, dtype)
-    marg = np.abs(logits[..., 1] - logits[..., 0]).reshape(-1)
     flips = (dpred != pred) & v
-    # the path's own logit-margin error over the valid points: flips must come from its bulk
-    # (oracle margin below twice its 99.9th percentile, or MARGIN), not from outliers
-    dm = np.abs((dlog[..., 1] - dlog[..., 0]).reshape(-1) - (logits[..., 1] - logits[..., 0]).reshape(-1))[v]
-    bound = max(MARGIN, 2.0 * float(np.quantile(dm, 0.999)))
-    print(f"trained {dtype}: mIoU {got:.6f} vs oracle {ref:.6f}, oracle prediction histogram {hist}, "
-          f"flipped {int(flips.sum())}, max oracle margin at flips {marg[flips].max() if flips.any() else 0:.3e}, "
-          f"margin error p50 {np.median(dm):.3e} p99.9 {np.quantile(dm, 0.999):.3e} max {dm.max():.3e}, "
-          f"max |logit| {np.abs(logits).max():.3e}")
+    dm = np.abs(_margin(dlog) - _margin(logits))[v]
+    print(f"trained {dtype}: mIoU {got:.6f} vs oracle {ref:.6f} (diff {got - ref:+.2e}), oracle prediction "
+          f"histogram {hist}, flipped {int(flips.sum())}, margin error p50 {np.median(dm):.3e} "
+          f"p99.9 {np.quantile(dm, 0.999):.3e} max {dm.max():.3e}, max |logit| {np.abs(logits).max():.3e}")
     assert hist.min() > 0.01 * v.sum(), "training left a degenerate (one-class) predictor"
     # the device confusion matrix and mIoU are exact for the predictions the path made
     assert abs(got - _sk_miou(dpred, lab.reshape(-1))) <= 1e-9
+    assert abs(got - ref) <= TOL
     if dtype == "fp32":
-        assert abs(got - ref) <= TOL
         assert flips.sum() == 0
-    else:
-        # bf16: the mIoU difference is the flipped points' (each moves one class's IoU by at most
-        # 1 / its union, >= the smaller class count), and they must be near-boundary points: the
-        # 1e-3 north-star holds where the prediction margins exceed bf16's logit error (the fp32
-        # case above, and both dtypes on the reference-written logits of the golden test).  How
-        # many points sit that close depends on the trained weights (16 flips / 1.3e-4 in r02,
-        # 81 / 1.3e-3 after r04's dropout stream change).
-        assert abs(got - ref) <= max(TOL, float(flips.sum()) / float(hist.min()))
-        # the logits themselves within the bf16 parity bound (a kernel error would break this)
-        assert dm.max() <= 0.1 * np.abs(logits).max()
-        assert flips.sum() <= 0.005 * v.sum() and (not flips.any() or marg[flips].max() < bound)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_storage_eval_is_its_emulation(trained, dtype):
+    """The eval forward on the training step's storage (eval_trunk="bf16": every layer bf16,
+    fp8 a5 / global_feat weight rows for "fp8") and as shipped (eval_trunk="fp32") against the
+    numpy restatement of exactly that storage (oracle/bf16_emulation.eval_logits): their logit
+    margins agree to within 1/8 of what the storage itself costs, so a mIoU miss of the
+    storage path is a property of its number format, not of a kernel.  The misses are
+    reported, not bounded (fp8: ~100 flipped points either way, see the print)."""
+    from bf16_emulation import eval_logits, eval_sites
+    C, sd, pts, lab, logits = _val_case(trained)
+    pred = logits.argmax(-1).reshape(-1)
+    v = lab.reshape(-1) >= 0
+    ref = _sk_miou(pred, lab.reshape(-1))
+    p = lambda a: float(np.quantile(a, 0.999))   # noqa: E731
+    fp8 = dtype == "fp8"
+    cost = None
+    for trunk in ("bf16", "fp32"):
+        got, dpred, dlog = _device_eval(sd, pts, lab, C, dtype, eval_trunk=trunk)
+        emu = eval_logits(sd, pts, eval_sites(trunk), fp8=fp8)
+        err = np.abs(_margin(emu) - _margin(logits))[v]        # what the storage costs
+        cost = p(err) if cost is None else cost                # yardstick: the all-storage path
+        diff = np.abs(_margin(dlog) - _margin(emu))[v]         # device vs its restatement
+        print(f"{dtype} eval_trunk={trunk}: mIoU {got:.6f} vs oracle {ref:.6f} (diff {got - ref:+.2e}, "
+              f"emulation {_sk_miou(emu.argmax(-1).reshape(-1), lab.reshape(-1)) - ref:+.2e}), flipped "
+              f"{int(((dpred != pred) & v).sum())}; margin error p99.9: format {p(err):.3e}, device vs "
+              f"emulation {p(diff):.3e} (p50 {np.median(diff):.2e})")
+        assert p(diff) <= cost / 8
