@@ -45,10 +45,6 @@ enum {
                            W's rows (pcs_sign_rows) and bias by sign(es), so the pool keeps the
                            plain column max of acc (no multiply); es still names the sign.
                            Needs pool and es, no statistics (they would be of the signed y)  */
-  PCS_FLAG_W4 = 32,     /* bf16 global_feat GEMMs (FWD signed-W pool / DGRAD without
-                           statistics) on the 4-wave 32x32x16 kernel (gemm_w4.hip) instead of
-                           the 8-wave 16x16x32 one (gemm_glds.hip): opt-in, slower at cfg2
-                           (DESIGN.md section 3), kept for A/B timing and cross-checks        */
   PCS_FLAG_SEG8 = 64    /* pcs_dgrad_wgrad_bn of seg_conv2 / seg_conv3: the 8-wave 128-column
                            kernel (fused_seg.hip) instead of the 4-wave 256-column one
                            (fused_seg4.hip), for A/B timing and cross-checks                 */
@@ -137,10 +133,6 @@ typedef struct {
  * kernel (and so the row tile: 256 for the bf16 wide-layer kernel, 128 otherwise) is chosen
  * from dtype, K, Ncols and flags, so call it with the same values as pcs_gemm. */
 int64_t pcs_gemm_geometry(pcs_gemm_args *args);
-/* 1 when pcs_gemm would run these arguments on the four-wave 32x32x16 LDS-DMA kernel
- * (csrc/gemm_w4.hip: bf16 global_feat forward max-pool on sign-folded W rows, or the folded
- * input gradient without statistics), 0 otherwise.  No GPU work. */
-int pcs_gemm_w4_selected(const pcs_gemm_args *args);
 /* Launch the GEMM. */
 int pcs_gemm(const pcs_gemm_args *args, pcs_stream_t stream);
 /* conv1 (Cin = K = input_dim, 1..8; the reference's points carry 4, P:70, P:106) forward:

@@ -47,7 +47,6 @@ FLAG_NO_GLDS = 2
 FLAG_AW_FP8 = 4
 FLAG_C_FP8 = 8
 FLAG_POOL_SIGNED_W = 16
-FLAG_W4 = 32
 FLAG_SEG8 = 64
 
 
@@ -102,7 +101,6 @@ class HeadArgs(ct.Structure):
 # (name, restype, argtypes) of every exported symbol declared in include/pcs.h
 SIGNATURES = [
     ("pcs_gemm_geometry", _i64, [ct.POINTER(GemmArgs)]),
-    ("pcs_gemm_w4_selected", ct.c_int, [ct.POINTER(GemmArgs)]),
     ("pcs_gemm", ct.c_int, [ct.POINTER(GemmArgs), _vp]),
     ("pcs_conv1_fwd", ct.c_int, [ct.POINTER(GemmArgs), _vp]),
     ("pcs_wgrad_workspace", _i64, [ct.POINTER(WgradArgs)]),

@@ -171,9 +171,6 @@ bool pcs_gemm_wres_applicable(const pcs_gemm_args &a);
 int pcs_gemm_wres_launch(const pcs_gemm_args &g, int64_t rows_per_chunk, hipStream_t s);
 int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                          hipStream_t s);
-// four-wave 32x32x16 LDS-DMA kernel for the bf16 global_feat GEMMs of the training step (gemm_w4.hip)
-bool pcs_gemm_w4_applicable(const pcs_gemm_args &a);
-int pcs_gemm_w4_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk, hipStream_t s);
 // fused seg_conv2 / seg_conv3 input + weight gradient (fused_seg.hip)
 bool pcs_seg4_applicable(const pcs_gemm_args &a);
 int64_t pcs_seg4_geometry(pcs_gemm_args *a);

@@ -147,11 +147,6 @@ template <int N, int I = 0, typename Fn> PCS_DEV void sfor(Fn &&fn) {
   }
 }
 
-// SEG4_ABL (timing ablations, wrong results): 1 no DMA in the loop, 2 no dy transform, 4 no
-// epilogue arithmetic (stores kept), 8 no weight-gradient MFMAs, 16 no input-gradient MFMAs
-#ifndef SEG4_ABL
-#define SEG4_ABL 0
-#endif
 template <int COUT, int CIN, bool MASK>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_split) {
@@ -408,14 +403,13 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
         bf16x8 w;
         if constexpr (kk < F::WLK) w = wl[kk & 1][ct];
         else w = wt[ct][kk - F::WLK];
-        if (!(SEG4_ABL & 16)) dacc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[kk & 1], w, dacc[ct], 0, 0, 0);
-        else dacc[ct] += __builtin_bit_cast(f32x4, w) * 0.f + __builtin_bit_cast(f32x4, bq[kk & 1]);
+        dacc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[kk & 1], w, dacc[ct], 0, 0, 0);
       }
-      if constexpr (kk <= F::NPW && !(SEG4_ABL & 1)) dma_piece(IC<kk>{}, sdma, sd);
+      if constexpr (kk <= F::NPW) dma_piece(IC<kk>{}, sdma, sd);
       __builtin_amdgcn_sched_barrier(0);
     });
     sfor<F::VM_STEP - (F::KSD < F::VM_STEP ? F::KSD : F::VM_STEP)>([&](auto Ic) __attribute__((always_inline)) {
-      if constexpr (!(SEG4_ABL & 1)) dma_piece(IC<F::KSD + decltype(Ic)::value>{}, sdma, sd);   // (seg_conv3: 4 k-steps, 5 pieces)
+      dma_piece(IC<F::KSD + decltype(Ic)::value>{}, sdma, sd);   // (seg_conv3: 4 k-steps, 5 pieces)
     });
 
     // ---- epilogue of step t: masks, S1 / S2, x^T and v^T into the wave's tiles
@@ -429,17 +423,11 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
         // MASK: the keep bits of rows past the slice are 0 (range-checked DMA), no row test
         const int kb = __builtin_amdgcn_sbfe((int)wb, 16 * (ct & 1) + l16, 1);
         const int keep = (MASK || 4 * g + r < rem) ? kb : 0;
-        if constexpr (SEG4_ABL & 4) {
-          xv[r] = y;
-          v[r] = dacc[ct][r];
-          (void)keep;
-        } else {
-          const float z = fmaf(y, esk[ct], etk[ct]);
-          xv[r] = __int_as_float(__float_as_int(fmaxf(z, 0.f)) & keep);
-          v[r] = xv[r] > 0.f ? dacc[ct][r] * ks : 0.f;
-          s1[ct] += v[r];
-          s2[ct] = fmaf(v[r], y, s2[ct]);
-        }
+        const float z = fmaf(y, esk[ct], etk[ct]);
+        xv[r] = __int_as_float(__float_as_int(fmaxf(z, 0.f)) & keep);
+        v[r] = xv[r] > 0.f ? dacc[ct][r] * ks : 0.f;
+        s1[ct] += v[r];
+        s2[ct] = fmaf(v[r], y, s2[ct]);
       }
       *reinterpret_cast<uint2 *>(xw + o_tw + ((520 * ct) ^ twx)) = make_uint2(pack2bf(xv[0], xv[1]), pack2bf(xv[2], xv[3]));
       *reinterpret_cast<uint2 *>(xw + F::TILE + o_tw + ((520 * ct) ^ twx)) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
@@ -508,22 +496,20 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       constexpr int o = decltype(Oc)::value;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
-        if (!(SEG4_ABL & 8)) acc[o][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afq[o % 3], xf[nb], acc[o][nb], 0, 0, 0);
+        acc[o][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afq[o % 3], xf[nb], acc[o][nb], 0, 0, 0);
       if constexpr (o + 3 < F::NO) afq[o % 3] = rd_af(o + 3);
       if constexpr (o >= 1 && o - 1 < F::TPASS) {
-        if (!(SEG4_ABL & 2)) {
-          constexpr int ps = o - 1;
-          const int r = trow + ps * (THREADS / F::CPR);
-          float vv[8], yy[8];
-          unpack_chunk(tdz[ps], vv);
-          unpack_chunk(tyy[ps], yy);
+        constexpr int ps = o - 1;
+        const int r = trow + ps * (THREADS / F::CPR);
+        float vv[8], yy[8];
+        unpack_chunk(tdz[ps], vv);
+        unpack_chunk(tyy[ps], yy);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) vv[e] = fmaf(ca[e], vv[e], fmaf(cg[e], yy[e], cb[e]));
-          const u32x4 out = pack_chunk(vv);
-          const bool in = r < remn;   // (past the last step: a stage nobody reads)
-          *reinterpret_cast<u32x4 *>(stn + r * ROWB + ((lc ^ fdz(r)) << 4)) =
-              mk_u32x4(in ? out.x : 0u, in ? out.y : 0u, in ? out.z : 0u, in ? out.w : 0u);
-        }
+        for (int e = 0; e < 8; ++e) vv[e] = fmaf(ca[e], vv[e], fmaf(cg[e], yy[e], cb[e]));
+        const u32x4 out = pack_chunk(vv);
+        const bool in = r < remn;   // (past the last step: a stage nobody reads)
+        *reinterpret_cast<u32x4 *>(stn + r * ROWB + ((lc ^ fdz(r)) << 4)) =
+            mk_u32x4(in ? out.x : 0u, in ? out.y : 0u, in ? out.z : 0u, in ? out.w : 0u);
       }
       __builtin_amdgcn_sched_barrier(0);
     });

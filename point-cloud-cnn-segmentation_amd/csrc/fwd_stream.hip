@@ -95,9 +95,6 @@ template <> struct FsCfg<64, 64> {     // conv2, conv3
 #ifndef FS_STG
 #define FS_STG 1
 #endif
-#ifndef FS_ABL
-#define FS_ABL 0   // timing ablations (wrong outputs): 1 no MFMAs, 2 no epilogue math, 3 no transform
-#endif
 #ifndef FS_ILV
 #define FS_ILV 1
 #endif
@@ -298,7 +295,6 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
 
   // ---- in-place BN + ReLU (+ dropout) of a landed stage: each element once
   auto transform_pass = [&](int sidx, int p) {
-    if constexpr (FS_ABL == 3) return;
     char *st = lds + sidx * F::STAGE;
     {
       const int r = trow + p * (THREADS / SPR);
@@ -402,13 +398,8 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-          if constexpr (FS_ABL == 1) {
-            asm volatile("" ::"v"(wfr[ct][kk]), "v"(xf[rt]));
-            acc[ct][rt][0] += 1.f;
-          } else {
-            acc[ct][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wfr[ct][kk]), xf[rt],
-                                                                 acc[ct][rt], 0, 0, 0);
-          }
+          acc[ct][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wfr[ct][kk]), xf[rt],
+                                                               acc[ct][rt], 0, 0, 0);
         }
       if constexpr (F::ILV) {
         constexpr int PER = KS / F::TPASS;   // MFMA k-steps per transform pass
@@ -428,13 +419,6 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       const float livef = live ? 1.f : 0.f;   // BNRELU: the column sums add d * livef by v_fma
                                               // (exact: d or +0), no per-element select
       uint32_t pk[CT][2];
-      if constexpr (FS_ABL == 2) {
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          pk[ct][0] = __float_as_uint(acc[ct][rt][0]) ^ __float_as_uint(acc[ct][rt][1]);
-          pk[ct][1] = __float_as_uint(acc[ct][rt][2]) ^ __float_as_uint(acc[ct][rt][3]);
-        }
-      } else
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         float v[4];

@@ -606,13 +606,6 @@ extern "C" int64_t pcs_gemm_geometry(pcs_gemm_args *a) {
   return pcs_fill_geometry(a, GEMM_BM, 2048, ncb);                 // ~8 WGs per CU
 }
 
-extern "C" int pcs_gemm_w4_selected(const pcs_gemm_args *ap) {
-  if (!ap) return pcs_set_einval("pcs_gemm_w4_selected", "null args");
-  pcs_gemm_args g = *ap;
-  if (pcs_gemm_geometry(&g) < 0) return 0;
-  return wide_class(g) && pcs_gemm_w4_applicable(g) ? 1 : 0;
-}
-
 extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   if (!ap) return pcs_set_einval("pcs_gemm", "null args");
   pcs_gemm_args a = *ap;
@@ -670,10 +663,6 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (pcs_fwd_stream_applicable(a)) return pcs_fwd_stream_launch(a, rpc, s);
   if (wide_class(a) && pcs_gemm_wres_applicable(a)) return pcs_gemm_wres_launch(a, rpc, s);
-  if (wide_class(a) && pcs_gemm_w4_applicable(a)) {
-    const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
-    return pcs_gemm_w4_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);
-  }
   if (wide_class(a) && pcs_gemm_glds_applicable(a)) {
     const int tps = (int)((a.scene_rows + PCS_BIG_BM - 1) / PCS_BIG_BM);
     return pcs_gemm_glds_launch(a, tps, (int)(rpc / PCS_BIG_BM), s);

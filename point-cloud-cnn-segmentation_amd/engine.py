@@ -193,6 +193,13 @@ class Engine:
         self.record_pool_rows = False
         self.last_pool_rows = None
         self.pool_rows_override = None
+        # test hooks for the pre-pool backward at full size (tests/test_gpu_fullsize.py):
+        # capture (a dict) receives the operands and outputs of global_feat's input gradient and
+        # conv5's backward kernels; perturb = {"dz5": (c0, c1, scale)} scales columns c0..c1 of
+        # dz5 after global_feat's input gradient (a simulated kernel error, the negative
+        # control).  Never set on the product path.
+        self.capture = None
+        self.perturb = None
         L.load()
 
     def _launch(self, tag, name, *args):
@@ -823,7 +830,6 @@ class Engine:
         pc5 = sv.bn["bn5"]
         cps5, _ = self.geometry(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD)
         st5 = torch.empty(B * cps5, 1024, 2, dtype=torch.float32, device=dev)
-        s1_5 = None   # bn5's S1 from conv5's R pass (the four-wave input-gradient kernel)
         if self.fp8:
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg[1], bufB, bias=cvec, Yp=a5,
                        w_scale=Hg[2], extra_flags=L.FLAG_AW_FP8, stats=st5, tag="dgrad:global_feat")
@@ -831,26 +837,25 @@ class Engine:
                    L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
         elif self.dt == L.BF16 and not (self.flags & (L.FLAG_GENERIC | L.FLAG_NO_GLDS)):
             # LDS-DMA kernel without the max-pool rows (no ordinary global loads in its
-            # epilogue), then their sparse term (pcs_pool_rows_add).  The 8-wave kernel sums
-            # S1 in its epilogue and in pcs_pool_rows_add; the opt-in four-wave kernel
-            # (PCS_FLAG_W4, csrc/gemm_w4.hip) keeps no statistics: bn5's S1 = the column sums
-            # of dz5 as stored then comes from conv5's R pass below (dy_colsum)
-            w4 = bool(self.flags & L.FLAG_W4)
-            if w4:
-                s1_5 = torch.empty(1024, dtype=torch.float32, device=dev)
-                st5.zero_()
+            # epilogue), then their sparse term (pcs_pool_rows_add); S1 in both
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
-                       stats=None if w4 else st5, tag="dgrad:global_feat")
+                       stats=st5, tag="dgrad:global_feat")
             # the max-pool rows with the W the forward GEMM used (as the fp8 branch and the
             # Gram-form weight gradient do)
             L.call("pcs_pool_rows_add", L.ptr(bufB), self.dt, L.ptr(a5), self.dt, B, N, 1024, L.ptr(sv.am),
-                   L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, None if w4 else L.ptr(st5), cps5, s)
+                   L.ptr(sp), L.ptr(Wg_r), Wg_r.shape[1], 1024, L.ptr(st5), cps5, s)
         else:
             # the max-pool rows with the W the forward GEMM used (fp32: the same tensor)
             self._gemm(B, N, 1024, 1024, L.PRO_RAW, L.EPI_DGRAD, a5, Hg, bufB, bias=cvec, Yp=a5,
                        pool_idx=sv.am, pool_coef=sp, pool_w=Wg_r, pool_ldw=Wg_r.shape[1], pool_c=1024,
                        stats=st5, tag="dgrad:global_feat")
         dz5 = bufB
+        if self.perturb is not None and "dz5" in self.perturb:
+            c0, c1, scale = self.perturb["dz5"]
+            dz5.view(M, 1024)[:, c0:c1].mul_(scale)
+        if self.capture is not None:
+            self.capture.update(dz5=dz5.view(M, 1024).clone(), a5=a5, H=Hg, cvec=cvec, am=sv.am.clone(),
+                                sp=sp.clone(), Wg_r=Wg_r)
         # global_feat weight gradient from the Gram of a5: the symmetric a5^T a5 (upper tiles)
         # + an O(C^3) assemble instead of the M x 1024 x 1024 GEMM
         ones = torch.ones(1024, dtype=torch.float32, device=dev)
@@ -892,11 +897,10 @@ class Engine:
         #   dW5 = diag(alpha5) R + beta5 (x) colsum(a4) + diag(gamma5) W5 (a4^T a4)
         pc4 = sv.bn["bn4"]
         r5 = torch.empty(1024, 128, dtype=torch.float32, device=dev)
-        s1_kw = {"dy_colsum": s1_5} if s1_5 is not None else {}
         keepalive.append(self._wgrad(B, N, 1024, 128, L.PRO_RAW, L.PRO_BNRELU, r5, tag="wgrad:conv5",
-                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift, **s1_kw))
-        if s1_5 is not None:   # S1 of dz5 as one partial (chunk 0; the others zero)
-            st5[0, :, 0].copy_(s1_5)
+                                     dZ=dz5, X=ys["conv4"], s=pc4.scale, t=pc4.shift))
+        if self.capture is not None:
+            self.capture.update(r5=r5.clone(), y4=ys["conv4"], s4=pc4.scale, t4=pc4.shift)
         L.call("pcs_bn_s2_from_r", L.ptr(st5), B * cps5, 1024, L.ptr(r5), L.ptr(wc["conv5"][0]), self.dt,
                128, 128, L.ptr(pc5.mean), L.ptr(pc5.rstd), s)
         bn_bwd("bn5", "conv5", st5, cps5)
@@ -914,6 +918,8 @@ class Engine:
         self._gemm(B, N, 1024 + 128, 128, L.PRO_CAT, L.EPI_DGRAD, dz5, ws_t, bufA, K1=1024, A2=ys["conv4"],
                    W2=h4, pa=pc4.scale, pb=pc4.shift, bias=c5, Yp=ys["conv4"], es=pc4.scale, et=pc4.shift,
                    emean=pc4.mean, erstd=pc4.rstd, stats=st, tag="dgrad:conv5")
+        if self.capture is not None:
+            self.capture.update(dz4=bufA[:M * 128].view(M, 128).clone(), ws_t=ws_t, h4=h4, c5=c5)
         g4, s4, ws4 = sv.gram4 if sv.gram4 is not None else \
             self._gram(ys["conv4"], pc4.scale, pc4.shift, B, N, 128, tag="gram:conv4")
         self._launch("wgrad_asm:conv5", "pcs_gram_wgrad", L.ptr(g4), L.ptr(s4), L.ptr(W5_r), 128, L.ptr(be5),

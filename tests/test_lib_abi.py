@@ -112,18 +112,3 @@ def test_seg_backward_geometry_without_gpu():
             cps = a.chunks_per_scene
             assert nbytes == 4 * cps * cout * cin * 4
             assert cps * 4 * nblk >= 256 and cps * 4 * nblk < 2 * 256   # about one workgroup per CU
-
-
-def test_w4_selection_without_gpu():
-    """The four-wave global_feat kernel is opt-in (PCS_FLAG_W4) and serves only the shapes it
-    was written for (host-side selection query, no kernel runs)."""
-    import pcs_amd._lib as L
-    lib = L.load()
-    a = L.GemmArgs(num_scenes=2, scene_rows=4096, K=1024, Ncols=1024, dtype=L.BF16,
-                   prologue=L.PRO_RAW, epilogue=L.EPI_DGRAD, flags=0)
-    a.A = a.Yp = a.W = a.C = 1 << 20   # (any non-null pointers: never dereferenced here)
-    assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 0
-    a.flags = L.FLAG_W4
-    assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 1
-    a.K = a.Ncols = 256                # K < 6 K-tiles: the deferred stores need K-tiles 1..4 and a spare
-    assert lib.pcs_gemm_w4_selected(ct.byref(a)) == 0
