@@ -116,6 +116,12 @@ PCS_DEV float max2f(float a, float b) {
   asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// 0 / 1 per 16-bit half: bf16 x > 0 <=> x > 0 as a signed 16-bit integer (-0 = 0x8000 is not)
+PCS_DEV uint32_t pos01(uint32_t x, uint32_t one2) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0\n\tv_pk_min_i16 %0, %0, %2" : "=&v"(r) : "v"(x), "v"(one2));
+  return r;
+}
 PCS_DEV int row_mini(int v) {
   v = min(v, dppi<0xB1>(v)); v = min(v, dppi<0x4E>(v)); v = min(v, dppi<0x141>(v));
   return min(v, dppi<0x140>(v));
@@ -309,16 +315,15 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       mbits[par * 2048 + t * 8 + kq * 4 + h] = w;
       return;
     }
+    // bf16: two packed 16-bit ops per word give 0 / 1 per element (bit 0: element 2d, bit 16:
+    // element 2d + 1); a chunk's 8 elements fold to one byte with the even elements in bits 0-3
+    // and the odd ones in bits 4-7 (the epilogue reads that order)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t x = v[d];
-        const uint32_t pos = ((x & 0x7fff7fffu) + 0x7fff7fffu) & ~x & 0x80008000u;
-        w |= ((pos >> 15) & 1u) << (c * 8 + d * 2);
-        w |= (pos >> 31) << (c * 8 + d * 2 + 1);
-      }
+      const uint32_t tb = pos01(v[0], 0x10001u) | (pos01(v[1], 0x10001u) << 1) | (pos01(v[2], 0x10001u) << 2) |
+                         (pos01(v[3], 0x10001u) << 3);
+      w |= ((tb | (tb >> 12)) & 0xffu) << (8 * c);
     }
     reinterpret_cast<uint16_t *>(mbits + par * 2048 + t * 8 + kq * 2)[h] = (uint16_t)w;
   };
@@ -609,11 +614,13 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         for (int j = 0; j < 4; ++j) {
           // rows past the scene (a partial tile) get an all-zero mask word: their v is 0, so S1
           // sums v unconditionally (one select per word, not one per element); they are not stored
-          const int word = ok ? (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + 4 * lg)) : 0;
+          // bf16 bitmap bytes: columns 8b + 2d at bit d, 8b + 2d + 1 at bit 4 + d (extract_mask);
+          // the lane's columns 4 lg + r, r = 0..3, sit at bits {0, 4, 1, 5} after the shift
+          const int word = ok ? (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + (FP8 ? 4 * lg : 8 * (lg >> 1) + 2 * (lg & 1)))) : 0;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, r, 1);
+            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, FP8 ? r : (r >> 1) + 4 * (r & 1), 1);
             v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
             s1[j][r] += v[r];
           }
