@@ -551,6 +551,51 @@ int pcs_pad_scatter(const float *points, const void *labels, int32_t label_bytes
 int pcs_round_weight(const float *W, int64_t n, int32_t dtype, float *out, pcs_stream_t stream);
 
 /*
+ * seg_conv1's local half and seg_conv2 in one streaming pass (the bf16 training forward,
+ * P:117-125; csrc/fwd_s12.hip), replacing pcs_gemm's seg_conv1 pass plus its seg_conv2 pass:
+ *   a2 = relu(y2 * s2 + t2);  Y1 = a2 W1^T + sbias[b]  (stored bf16 [M, 512], as pcs_gemm's
+ *   FWD with scene_bias would store it);  x = relu(Y1 * s1 + t1) * keep * keep_scale, from the
+ *   stored (rounded) Y1;  Y2 = x W2^T  (stored bf16 [M, 256]) with per-chunk (mean, M2) of the
+ *   stored values in stats [B * chunks_per_scene, 256, 2] (pcs_bn_fwd_finalize's partials).
+ * W1 is bf16 [512, 64] (seg_conv1's local half, pcs_cast_weight), W2 bf16 [256, 512]; s1 / t1
+ * are bn_seg1's coefficients from batch statistics known before Y1 exists
+ * (pcs_bn_stats_gram_sbias).  keep1 [M, 64] keep bits (bit i of byte j = channel 8j + i) or
+ * NULL (no dropout).  pcs_fwd_seg12_geometry fills chunks_per_scene (0 = auto) and returns the
+ * rows per chunk.
+ */
+typedef struct {
+  int64_t num_scenes;
+  int64_t scene_rows;
+  int32_t chunks_per_scene;
+  const void *y2;       /* [M, 64] bf16: conv2's stored pre-BN output */
+  const float *s2, *t2; /* [64] bn2 scale / shift */
+  const void *W1;       /* [512, 64] bf16 */
+  const float *sbias;   /* [B, 512] per-scene bias of the stored Y1 (pcs_scene_gemv, centred) */
+  void *Y1;             /* [M, 512] bf16 out */
+  const float *s1, *t1; /* [512] bn_seg1 scale / shift */
+  const uint8_t *keep1; /* [M, 64] dropout keep bits after bn_seg1 (P:124) or NULL */
+  float keep_scale;     /* 1 / (1 - p) */
+  const void *W2;       /* [256, 512] bf16 */
+  void *Y2;             /* [M, 256] bf16 out */
+  float *stats;         /* [B * chunks_per_scene, 256, 2] or NULL */
+} pcs_seg12_args;
+int64_t pcs_fwd_seg12_geometry(pcs_seg12_args *args);
+int pcs_fwd_seg12(const pcs_seg12_args *args, pcs_stream_t stream);
+
+/*
+ * BatchNorm statistics of y = a W^T + sbias[b] (W [C, Cin] fp32, row stride ldw; Cin <= 64)
+ * from the Gram of a (G = a^T a over all rows, fp32 [Cin, Cin]) and per-scene column sums Sb
+ * [num_scenes, Cin] (scene_rows rows each): per-scene partials stats[b, c] = (mean_b,
+ * M2w / num_scenes) with mean_b = Sb_b w / N + sbias[b, c] and M2w = w (G - sum_b Sb_b Sb_b^T /
+ * N) w^T (fp64), for pcs_bn_fwd_finalize with chunks_per_scene = 1, rows_per_chunk = scene_rows
+ * (its Chan merge adds the between-scene term).  bn_seg1's statistics for pcs_fwd_seg12
+ * (P:123): seg_conv1's output is never read back for them.  sbias may be NULL.
+ */
+int pcs_bn_stats_gram_sbias(const float *G, const float *Sb, int64_t num_scenes, int64_t scene_rows,
+                            const float *W, int64_t ldw, int32_t Cin, int32_t C, const float *sbias,
+                            float *stats, pcs_stream_t stream);
+
+/*
  * Bridge of the bf16 / fp8 EVAL forward's fp32 trunk (BatchNorm eval, P:106-110 with
  * model.eval(), P:313): a = relu(Y*s[k] + t[k]) of an fp32 pre-BN output Y [M, K] (row
  * stride K), stored as bf16 for a bf16 GEMM.  split = 0: out [M, K] = bf16(a).  split = 1:

@@ -63,6 +63,15 @@ class WgradArgs(ct.Structure):
     ]
 
 
+class Seg12Args(ct.Structure):
+    _fields_ = [
+        ("num_scenes", _i64), ("scene_rows", _i64), ("chunks_per_scene", _i32),
+        ("y2", _vp), ("s2", _vp), ("t2", _vp), ("W1", _vp), ("sbias", _vp), ("Y1", _vp),
+        ("s1", _vp), ("t1", _vp), ("keep1", _vp), ("keep_scale", _f), ("W2", _vp), ("Y2", _vp),
+        ("stats", _vp),
+    ]
+
+
 class Conv3dGeom(ct.Structure):
     _fields_ = [
         ("B", _i64), ("Di", _i32), ("Hi", _i32), ("Wi", _i32), ("Do", _i32), ("Ho", _i32), ("Wo", _i32),
@@ -166,6 +175,9 @@ SIGNATURES = [
     ("pcs_dgrad_wgrad_bn", ct.c_int, [ct.POINTER(GemmArgs), _vp, _vp, _i64, _vp]),
     ("pcs_round_weight", ct.c_int, [_vp, _i64, _i32, _vp, _vp]),
     ("pcs_bnrelu_bf16", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
+    ("pcs_fwd_seg12_geometry", _i64, [ct.POINTER(Seg12Args)]),
+    ("pcs_fwd_seg12", ct.c_int, [ct.POINTER(Seg12Args), _vp]),
+    ("pcs_bn_stats_gram_sbias", ct.c_int, [_vp, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     ("pcs_voxel_ids", ct.c_int, [_vp, _i64, _i32, _f, _f, _f, _f, _f, _f, _vp, _vp]),
     ("pcs_voxelize_workspace", _i64, [_i64]),
     ("pcs_voxelize", ct.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _f, _f, _f, _f, _f, _f, _i32, _vp, _i64,

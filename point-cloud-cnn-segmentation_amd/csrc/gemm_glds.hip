@@ -301,6 +301,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     const char *base = lds + buf * KBUF + region * REG + q * 128;
     uint32_t w = 0;
     if constexpr (FP8) {   // 32 columns (bytes) per thread: x > 0 <=> sign clear, 7 low bits nonzero
+      // word d (columns 4d .. 4d + 3) flags each byte in its bit 7; shifting word d right by
+      // 7 - d and OR-ing the 8 words puts column 4d + k at bit 8k + d (the epilogue's order)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
@@ -308,8 +310,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
         for (int d = 0; d < 4; ++d) {
           const uint32_t x = v[d];
           const uint32_t pos = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) & ~x & 0x80808080u;
-          const uint32_t nib = ((pos >> 7) & 1u) | ((pos >> 14) & 2u) | ((pos >> 21) & 4u) | ((pos >> 28) & 8u);
-          w |= nib << (c * 16 + d * 4);
+          w |= pos >> (7 - (4 * c + d));
         }
       }
       mbits[par * 2048 + t * 8 + kq * 4 + h] = w;
@@ -616,11 +617,13 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
           // sums v unconditionally (one select per word, not one per element); they are not stored
           // bf16 bitmap bytes: columns 8b + 2d at bit d, 8b + 2d + 1 at bit 4 + d (extract_mask);
           // the lane's columns 4 lg + r, r = 0..3, sit at bits {0, 4, 1, 5} after the shift
-          const int word = ok ? (int)((j < 2 ? mw.x : mw.y) >> ((j & 1) * 16 + (FP8 ? 4 * lg : 8 * (lg >> 1) + 2 * (lg & 1)))) : 0;
+          // fp8 bitmap words: column e of the word's 32 at bit 8 (e % 4) + e / 4 (extract_mask);
+          // the lane's columns 16 (j & 1) + 4 lg + r sit at bits 8 r after the shift
+          const int word = ok ? (int)((j < 2 ? mw.x : mw.y) >> (FP8 ? 4 * (j & 1) + lg : (j & 1) * 16 + 8 * (lg >> 1) + 2 * (lg & 1))) : 0;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, FP8 ? r : (r >> 1) + 4 * (r & 1), 1);
+            const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, FP8 ? 8 * r : (r >> 1) + 4 * (r & 1), 1);
             v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
             s1[j][r] += v[r];
           }

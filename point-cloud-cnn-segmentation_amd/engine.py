@@ -200,6 +200,10 @@ class Engine:
         # control).  Never set on the product path.
         self.capture = None
         self.perturb = None
+        # bf16 / fp8 training forward: seg_conv1's local half and seg_conv2 in one streaming pass
+        # (pcs_fwd_seg12, bn_seg1's statistics from the Gram of a2); False runs the two pcs_gemm
+        # passes (cross-checks)
+        self.fused_seg12 = True
         L.load()
 
     def _launch(self, tag, name, *args):
@@ -567,7 +571,10 @@ class Engine:
         L.call("pcs_scene_gemv", L.ptr(sv.g), B, 1024, L.ptr(Ws1), Ws1.shape[1], 64,
                L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), L.ptr(soff), s)
         sv.sbias_s1 = sbias   # the stored Y'_seg1 = a2 W_l^T + sbias[b] (the folded backward)
-        if trunk32:
+        fused12 = train and self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC) and self.fused_seg12
+        if fused12:
+            pass   # with seg_conv2 below (pcs_fwd_seg12)
+        elif trunk32:
             layer("seg_conv1", "conv2", "bn2", 64, 512, "bn_seg1", soff, scene_bias=sbias,
                   A_raw=bridge("conv2", "bn2", 64, False))
         else:
@@ -593,8 +600,11 @@ class Engine:
             m1 = m2 = None
             sv.masks = (None, None)
             keep = 1.0
-        layer("seg_conv2", "seg_conv1", "bn_seg1", 512, 256, "bn_seg2", P["seg_conv2.bias"],
-              a_mask=m1, a_keep_scale=keep)
+        if fused12:
+            self._seg12(P, bufs, sv, wc, sbias, soff, m1, keep)
+        else:
+            layer("seg_conv2", "seg_conv1", "bn_seg1", 512, 256, "bn_seg2", P["seg_conv2.bias"],
+                  a_mask=m1, a_keep_scale=keep)
         layer("seg_conv3", "seg_conv2", "bn_seg2", 256, 128, "bn_seg3", P["seg_conv3.bias"],
               a_mask=m2, a_keep_scale=keep)
 
@@ -607,6 +617,44 @@ class Engine:
         else:
             self._head(P, sv, L.HEAD_FWD)
         return sv
+
+    def _seg12(self, P, bufs, sv, wc, sbias, soff, m1, keep):
+        """seg_conv1 (local half + scene bias) and seg_conv2 forward in one pass (P:117-125;
+        pcs_fwd_seg12).  bn_seg1's batch statistics come first, from the Gram of a2 =
+        relu(bn2(y2)) and its per-scene column sums (pcs_gram, pcs_bn_stats_gram_sbias), with
+        the bf16-rounded W_l the pass multiplies by."""
+        B, N = sv.B, sv.N
+        M = B * N
+        dev = sv.x.device
+        s = self._stream()
+        c2 = sv.bn["bn2"]
+        G2, _, gws = self._gram(sv.ys["conv2"], c2.scale, c2.shift, B, N, 64, tag="fwd_stats:seg_conv1")
+        sps = ct.c_int32(0)
+        L.load().pcs_gram_workspace(B, N, 64, self.dt, ct.byref(sps))
+        Sb = torch.empty(B, 64, dtype=torch.float32, device=dev)
+        L.call("pcs_reduce_partials_grouped", L.ptr(gws[B * sps.value * 64 * 64:]), B, sps.value, 64, 1.0, L.ptr(Sb), s)
+        Ws1 = P["seg_conv1.weight"]
+        Ws1_r = self._rounded(Ws1)
+        st1 = torch.empty(B, 512, 2, dtype=torch.float32, device=dev)
+        L.call("pcs_bn_stats_gram_sbias", L.ptr(G2), L.ptr(Sb), B, N, L.ptr(Ws1_r), Ws1.shape[1], 64, 512,
+               L.ptr(sbias), L.ptr(st1), s)
+        sv.bn["bn_seg1"] = c1 = self._bn_finalize("bn_seg1", st1, B, N, 512, 1, N, P, bufs, True, dev, offset=soff)
+        y1 = self._empty(M, 512, device=dev)
+        y2 = self._empty(M, 256, device=dev)
+        a = L.Seg12Args(num_scenes=B, scene_rows=N, chunks_per_scene=0, y2=L.ptr(sv.ys["conv2"]), s2=L.ptr(c2.scale),
+                        t2=L.ptr(c2.shift), W1=L.ptr(wc["seg_conv1"][0]), sbias=L.ptr(sbias), Y1=L.ptr(y1),
+                        s1=L.ptr(c1.scale), t1=L.ptr(c1.shift), keep1=L.ptr(m1), keep_scale=keep,
+                        W2=L.ptr(wc["seg_conv2"][0]), Y2=L.ptr(y2))
+        rpc = L.load().pcs_fwd_seg12_geometry(ct.byref(a))
+        if rpc <= 0:
+            raise L.PcsError(L.load().pcs_last_error().decode())
+        cps = a.chunks_per_scene
+        st2 = torch.empty(B * cps, 256, 2, dtype=torch.float32, device=dev)
+        a.stats = L.ptr(st2)
+        self._launch("fwd:seg_conv1+2", "pcs_fwd_seg12", ct.byref(a), s)
+        sv.ys["seg_conv1"], sv.ys["seg_conv2"] = y1, y2
+        sv.bn["bn_seg2"] = self._bn_finalize("bn_seg2", st2, B, N, 256, cps, rpc, P, bufs, True, dev,
+                                             offset=P["seg_conv2.bias"])
 
     def _head(self, P, sv, mode, labels=None, class_weight=None, wsum=None, dlogits=None):
         """seg_conv4 + (CE | given dlogits) + head backward; returns the backward buffers."""

@@ -1,0 +1,159 @@
+"""The fused seg_conv1 + seg_conv2 forward (csrc/fwd_s12.hip, pcs_fwd_seg12; P:117-125) and
+bn_seg1's statistics from the Gram of a2 (pcs_bn_stats_gram_sbias):
+
+* the fused pass against the two streaming passes it replaces (pcs_gemm FWD for seg_conv1 with
+  the scene bias, then for seg_conv2 with bn_seg1 + ReLU + dropout in its prologue) on the same
+  operands and coefficients: Y1 and Y2 bit for bit (same bf16 operands, same fp32 summation
+  order), bn_seg2's statistics merged per scene within 1e-5;
+* the Gram statistics against torch fp64 of the same y = a W^T + sbias;
+* one bf16 training step with the fused pass against the same step with the two passes."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _ops(B, N, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    M = B * N
+    r = lambda *s: torch.randn(*s, generator=g)   # noqa: E731
+    y2 = r(M, 64).to(torch.bfloat16).to(DEV)
+    s2, t2 = (r(64) * 0.5 + 1.0).to(DEV), (r(64) * 0.3).to(DEV)
+    W1 = (r(512, 64) * 0.15).to(torch.bfloat16).to(DEV)
+    sbias = (r(B, 512) * 0.2).to(DEV)
+    s1, t1 = (r(512) * 0.3 + 0.8).to(DEV), (r(512) * 0.2).to(DEV)
+    bits = torch.randint(0, 256, (M, 64), generator=g, dtype=torch.uint8).to(DEV)
+    W2 = (r(256, 512) * 0.05).to(torch.bfloat16).to(DEV)
+    return y2, s2, t2, W1, sbias, s1, t1, bits, W2
+
+
+def _two_pass(L, B, N, y2, s2, t2, W1, sbias, s1, t1, bits, W2, ks):
+    lib = L.load()
+    M = B * N
+    y1 = torch.empty(M, 512, dtype=torch.bfloat16, device=DEV)
+    out = torch.empty(M, 256, dtype=torch.bfloat16, device=DEV)
+    a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=512, dtype=L.BF16, prologue=L.PRO_BNRELU,
+                   epilogue=L.EPI_FWD, chunks_per_scene=0, A=y2.data_ptr(), W=W1.data_ptr(), C=y1.data_ptr(),
+                   pa=s2.data_ptr(), pb=t2.data_ptr(), scene_bias=sbias.data_ptr(), a_keep_scale=1.0, c_keep_scale=1.0)
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    b = L.GemmArgs(num_scenes=B, scene_rows=N, K=512, Ncols=256, dtype=L.BF16, prologue=L.PRO_BNRELU,
+                   epilogue=L.EPI_FWD, chunks_per_scene=0, A=y1.data_ptr(), W=W2.data_ptr(), C=out.data_ptr(),
+                   pa=s1.data_ptr(), pb=t1.data_ptr(), a_mask=L.ptr(bits), a_keep_scale=ks, c_keep_scale=1.0)
+    lib.pcs_gemm_geometry(ct.byref(b))
+    st = torch.empty(B * b.chunks_per_scene, 256, 2, device=DEV)
+    b.stats = st.data_ptr()
+    L.call("pcs_gemm", ct.byref(b), L.stream_ptr())
+    return y1, out, st
+
+
+def _fused(L, B, N, y2, s2, t2, W1, sbias, s1, t1, bits, W2, ks):
+    lib = L.load()
+    M = B * N
+    y1 = torch.empty(M, 512, dtype=torch.bfloat16, device=DEV)
+    out = torch.empty(M, 256, dtype=torch.bfloat16, device=DEV)
+    a = L.Seg12Args(num_scenes=B, scene_rows=N, chunks_per_scene=0, y2=y2.data_ptr(), s2=s2.data_ptr(),
+                    t2=t2.data_ptr(), W1=W1.data_ptr(), sbias=sbias.data_ptr(), Y1=y1.data_ptr(),
+                    s1=s1.data_ptr(), t1=t1.data_ptr(), keep1=L.ptr(bits), keep_scale=ks, W2=W2.data_ptr(),
+                    Y2=out.data_ptr())
+    rpc = lib.pcs_fwd_seg12_geometry(ct.byref(a))
+    assert rpc > 0 and rpc % 32 == 0
+    st = torch.empty(B * a.chunks_per_scene, 256, 2, device=DEV)
+    a.stats = st.data_ptr()
+    L.call("pcs_fwd_seg12", ct.byref(a), L.stream_ptr())
+    return y1, out, st, rpc
+
+
+@pytest.mark.parametrize("B,N,mask", [(2, 3000, True), (3, 4097, True), (1, 100, False), (4, 2 ** 16, True)])
+def test_fused_matches_two_passes(B, N, mask):
+    import pcs_amd._lib as L
+    ops = list(_ops(B, N, seed=B * 7 + N))
+    if not mask:
+        ops[7] = None
+    ks = 1.0 / 0.7 if mask else 1.0
+    ry1, ry2, rst = _two_pass(L, B, N, *ops, ks)
+    fy1, fy2, fst, rpc = _fused(L, B, N, *ops, ks)
+    torch.cuda.synchronize()
+    assert torch.equal(ry1.view(torch.int16), fy1.view(torch.int16)), "Y1 differs"
+    neq = int((ry2.view(torch.int16) != fy2.view(torch.int16)).sum())
+    print(f"B={B} N={N}: Y2 elements differing {neq} of {fy2.numel()}")
+    assert neq == 0
+    # bn_seg2's statistics: the fused pass's chunk partials merged per scene against fp64
+    # statistics of the stored Y2
+    y = fy2.float().view(B, N, 256).double()
+    ref_mean, ref_m2 = y.mean(1), ((y - y.mean(1, keepdim=True)) ** 2).sum(1)
+    cps = fst.shape[0] // B
+    rows = [min(rpc, N - c * rpc) for c in range(cps)]
+    st = fst.double().view(B, cps, 256, 2)
+    n = torch.tensor(rows, dtype=torch.float64, device=DEV)[None, :, None]
+    mean = (st[..., 0] * n).sum(1) / N
+    m2 = st[..., 1].sum(1) + (n * (st[..., 0] - mean[:, None, :]) ** 2).sum(1)
+    assert torch.allclose(mean, ref_mean, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(m2, ref_m2, rtol=1e-4, atol=1e-4 * float(ref_m2.abs().max()))
+
+
+def test_bn_stats_from_gram_of_a2():
+    import pcs_amd._lib as L
+    B, N = 3, 5000
+    y2, s2, t2, W1, sbias, *_ = _ops(B, N, seed=5)
+    a2 = torch.relu(y2.float() * s2 + t2).to(torch.bfloat16).float()
+    G = (a2.double().T @ a2.double()).float()
+    Sb = a2.view(B, N, 64).double().sum(1).float()
+    W = W1.float().contiguous()
+    st = torch.empty(B, 512, 2, device=DEV)
+    L.call("pcs_bn_stats_gram_sbias", L.ptr(G), L.ptr(Sb), B, N, L.ptr(W), 64, 64, 512, L.ptr(sbias), L.ptr(st),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    y = (a2.double() @ W.double().T).view(B, N, 512) + sbias.double()[:, None, :]
+    mean_b = y.mean(1)
+    m2w = ((y - mean_b[:, None, :]) ** 2).sum((0, 1))
+    assert torch.allclose(st[..., 0].double(), mean_b, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(st[..., 1].double().sum(0), m2w, rtol=1e-4)
+
+
+def test_train_step_fused_vs_two_passes():
+    """A bf16 training step (replayed dropout masks) with the fused pass and with the two passes:
+    same loss and gradients up to the Gram statistics' rounding (bn_seg1 from the Gram of a2 in
+    fp32 instead of the stored Y1's own statistics)."""
+    from pcs_amd.data import class_weights, synthetic_batch
+    from pcs_amd.model import PointNetSegmentation
+    import pointnet_oracle as orc
+    B, G, C = 2, 24, 2
+    pts, lab, _ = synthetic_batch(99, [G ** 3] * B, C, grid=G, dense=True)
+    w = class_weights([lab[b] for b in range(B)], num_classes=C)
+    sd = orc.init_params(C, 3)
+    M = B * G ** 3
+    gen = torch.Generator().manual_seed(1)
+    m1 = torch.randint(0, 256, (M, 64), generator=gen, dtype=torch.uint8).to(DEV)
+    m2 = torch.randint(0, 256, (M, 32), generator=gen, dtype=torch.uint8).to(DEV)
+    x, y = torch.from_numpy(pts).to(DEV), torch.from_numpy(lab).to(DEV).view(-1)
+    crit = torch.nn.CrossEntropyLoss(ignore_index=-1, weight=torch.tensor(w, device=DEV))
+    res = {}
+    for fused in (True, False):
+        m = PointNetSegmentation(C, compute_dtype="bf16").to(DEV)
+        m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in sd.items()})
+        m.train()
+        m._engine().fused_seg12 = fused
+        m.set_dropout_masks(m1, m2)
+        loss = crit(m(x).contiguous().view(-1, C), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[fused] = (float(loss), {n: p.grad.detach().double().flatten() for n, p in m.named_parameters()},
+                      {n: b.detach().double() for n, b in m.named_buffers() if "running" in n})
+    (lf, gf, bf), (lt, gt, bt) = res[True], res[False]
+    print(f"loss fused {lf:.6f} two-pass {lt:.6f}")
+    assert abs(lf - lt) < 2e-3 * max(1.0, abs(lt))
+    worst = {}
+    for n in gt:
+        if (n.endswith(".bias") and not n.startswith(("bn", "seg_conv4"))) or n == "bn_global.bias":
+            continue
+        a, b = gf[n], gt[n]
+        worst[n] = 1 - float(a @ b / (a.norm() * b.norm() + 1e-30))
+    print("1 - cos fused vs two-pass:", {k: round(v, 6) for k, v in worst.items()})
+    assert max(worst.values()) < 1e-3   # measured r05: 8e-5
+    for n in bt:
+        e = float((bf[n] - bt[n]).norm() / bt[n].norm())
+        assert e < 1e-3, (n, e)
