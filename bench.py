@@ -249,7 +249,10 @@ def shared_class_weights(label_arrays, num_classes, world):
     """One class-weight vector for every rank (P:168-189, P:216: the reference builds a single
     weight tensor from the labels it scans): the per-class counts of this rank's scenes are
     summed over the process group, so every rank derives the weights of the global batch (the
-    concatenation of all ranks' scenes), not of its own shard."""
+    concatenation of all ranks' scenes), not of its own shard.  ``label_arrays`` are the scenes'
+    own labels: the reference scans dataset events (P:148-166), which never hold collate pads, so
+    pad labels (-1) are skipped here and must not reach ``class_weights`` either (its Counter
+    would count them)."""
     counts = label_counts(label_arrays, num_classes)
     if world > 1:
         t = torch.from_numpy(counts)
@@ -347,7 +350,7 @@ def main():
     else:
         N = G ** 3
         pts, lab, _ = synthetic_batch(1234 + rank, [N] * B, C, grid=G, dense=True)
-        w = shared_class_weights([lab[b] for b in range(B)], C, world)
+        w = shared_class_weights([lab[b][lab[b] >= 0] for b in range(B)], C, world)
         x = torch.from_numpy(pts).to(dev)
         y = torch.from_numpy(lab).to(dev)
         real_points = B * N

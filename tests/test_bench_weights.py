@@ -17,7 +17,7 @@ def _rank_labels(rank, C):
     sys.path.insert(0, REPO)
     from pcs_amd.data import synthetic_batch
     _, lab, _ = synthetic_batch(1234 + rank, [4096, 3000], C, grid=16)
-    return [lab[0], lab[1]]
+    return [lab[0], lab[1][:3000]]   # the scenes' own labels (the reference scans unpadded events)
 
 
 def _worker(rank, world, port, C, q):
@@ -60,3 +60,15 @@ def test_class_weights_world_one_is_local():
     from pcs_amd.data import class_weights
     labs = _rank_labels(0, 3)
     assert bench.shared_class_weights(labs, 3, 1) == class_weights(labs, num_classes=3)
+
+
+def test_class_weights_skip_pads_even_when_they_dominate():
+    """Pads (-1) never enter the weights: a scene padded far past its largest class gives the
+    unpadded scene's weights (class_weights' Counter would take max_count from the pads)."""
+    sys.path.insert(0, REPO)
+    import bench
+    from pcs_amd.data import class_weights
+    own = _rank_labels(0, 3)
+    padded = [np.concatenate([l, np.full(5 * l.size, -1, l.dtype)]) for l in own]
+    assert bench.shared_class_weights(padded, 3, 1) == class_weights(own, num_classes=3)
+    assert class_weights(padded, num_classes=3) != class_weights(own, num_classes=3)
