@@ -294,6 +294,8 @@ def main():
     ap.add_argument("--classes", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--draw-at-start", action="store_true",
+                    help="bf16: draw the dropout bits at the start of the forward (A/B)")
     ap.add_argument("--no-fused-seg12", action="store_true",
                     help="A/B: seg_conv1 and seg_conv2 forward as two passes instead of pcs_fwd_seg12")
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],
@@ -364,6 +366,8 @@ def main():
 
     torch.manual_seed(0)
     model = PointNetSegmentation(C, compute_dtype=args.dtype).to(dev)
+    if args.draw_at_start:
+        model._engine().draw_beside_gram = False
     if args.no_fused_seg12:
         model._engine().fused_seg12 = False
     if world > 1:   # identical initial weights on every rank (DataParallel replicates them)

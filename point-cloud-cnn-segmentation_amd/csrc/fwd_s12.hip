@@ -66,7 +66,7 @@ PCS_DEV int xcd_remap(int bid, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 template <int N> PCS_DEV float row_ror(float v) {   // rotate within the 16 lanes of a DPP row
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + N, 0xf, 0xf, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x120 + N, 0xf, 0xf, true));
 }
 PCS_DEV int f64s(int r) { return (r >> 1) & 7; }   // slot permutation of 128-B rows
 

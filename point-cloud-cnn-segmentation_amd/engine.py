@@ -204,6 +204,9 @@ class Engine:
         # (pcs_fwd_seg12, bn_seg1's statistics from the Gram of a2); False runs the two pcs_gemm
         # passes (cross-checks)
         self.fused_seg12 = True
+        # bf16 training step: draw the dropout keep bits beside the Gram of a5 (bounded grid, in
+        # its idle VALU issue) instead of at the start of the forward with a full grid
+        self.draw_beside_gram = True
         L.load()
 
     def _launch(self, tag, name, *args):
@@ -396,7 +399,7 @@ class Engine:
         # bf16 (stored-a5 Gram): draw beside the Gram of a5, MFMA-bound at 214 VGPRs x 2 waves per
         # SIMD, with two 256-thread workgroups per CU (24 VGPRs a wave: they fit beside it and use
         # its idle VALU issue); otherwise at the start of the forward with a full grid
-        draw_beside_gram = train and masks is None and self._raw_gram() and not self.fp8
+        draw_beside_gram = train and masks is None and self._raw_gram() and not self.fp8 and self.draw_beside_gram
         if train and masks is None and not draw_beside_gram:
             draw_masks()
         sv.wc = wc = self.cast_weights(P)
