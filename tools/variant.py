@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "point-cloud-cnn-segmentation_amd", "csrc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall", "-Wno-unused-function"]
 EXTRA = {"gemm_glds": ["-mllvm", "-disable-machine-sink"], "gram_glds": ["-mllvm", "-disable-machine-sink"],
-         "fused_seg4": ["-fno-slp-vectorize"]}
+         "fused_seg4": ["-fno-slp-vectorize"], "fwd_s12": ["-fno-slp-vectorize"]}
 
 
 def build(spec_path):
