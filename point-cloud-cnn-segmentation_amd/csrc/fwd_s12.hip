@@ -53,11 +53,14 @@ constexpr int OFF_SQ = OFF_SS + N2 * 4;
 constexpr int BYTES = OFF_SQ + N2 * 4;
 static_assert(BYTES <= 160 * 1024, "LDS budget");
 constexpr int KS2 = K2 / 32;                  // stage-2 k-steps
-// vector-memory operations per wave per loop iteration, in issue order: 3 DMA pieces, 4 Y1 stores
-// (step t + 1), 2 Y2 stores (step t); the wait at the top of iteration t retires the DMA of step
-// t + 1, issued NST - 1 iterations earlier: newer are that iteration's 6 stores and (NST - 2)
-// whole iterations
-constexpr int VM_WAIT = 6 + (NST - 2) * 9;
+// Ring of three stages: in iteration t, step t + 1's stage feeds stage 1, step t + 2's (DMA'd in
+// iteration t - 1) gets bn2 + ReLU for the next iteration, and step t's (consumed in iteration
+// t - 1) takes the DMA of step t + 3; so one barrier per step.  Vector-memory operations per wave
+// per iteration, in issue order: 3 DMA pieces, 4 Y1 stores (step t + 1), 2 Y2 stores (step t);
+// the wait at the top of iteration t retires the DMA of step t + 2, issued one iteration
+// earlier: newer are that iteration's 6 stores
+static_assert(NST == 3, "the ring's roles assume three stages");
+constexpr int VM_WAIT = 6;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -179,19 +182,19 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
     m0_restore(keep);
   };
 
-  // ---- bn2 + ReLU in place, each element once (threads < 256: row tid / 8, logical slot tid % 8)
+  // ---- bn2 + ReLU in place, each element once (thread: row tid / 16, logical slot (tid / 2) % 8,
+  // its half tid % 2: 4 elements)
   auto transform = [&](int sidx) {
-    if (tid < MS * 8) {
-      const int r = tid >> 3, ls = tid & 7;
-      u32x4 *q = reinterpret_cast<u32x4 *>(lds + sidx * STAGE + r * ROW1 + ((ls ^ f64s(r)) << 4));
-      const float *s2 = reinterpret_cast<const float *>(lds + OFF_S2) + 8 * ls;
-      const float *t2 = reinterpret_cast<const float *>(lds + OFF_T2) + 8 * ls;
-      float v[8];
-      unpack_chunk(*q, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], s2[e], t2[e]), 0.f);
-      *q = pack_chunk(v);
-    }
+    const int r = tid >> 4, ls = (tid >> 1) & 7, hf = tid & 1;
+    uint2 *q = reinterpret_cast<uint2 *>(lds + sidx * STAGE + r * ROW1 + ((ls ^ f64s(r)) << 4) + 8 * hf);
+    const f32x4 s2 = *reinterpret_cast<const f32x4 *>(lds + OFF_S2 + (8 * ls + 4 * hf) * 4);
+    const f32x4 t2 = *reinterpret_cast<const f32x4 *>(lds + OFF_T2 + (8 * ls + 4 * hf) * 4);
+    const uint2 u = *q;
+    const float v0 = fmaxf(fmaf(bf2f(u.x & 0xffffu), s2[0], t2[0]), 0.f);
+    const float v1 = fmaxf(fmaf(bf2f(u.x >> 16), s2[1], t2[1]), 0.f);
+    const float v2 = fmaxf(fmaf(bf2f(u.y & 0xffffu), s2[2], t2[2]), 0.f);
+    const float v3 = fmaxf(fmaf(bf2f(u.y >> 16), s2[3], t2[3]), 0.f);
+    *q = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
   };
 
   // ---- outputs through buffer descriptors over the slice's rows (stores past them are dropped)
@@ -278,9 +281,10 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
     }
   };
 
-  // ---- prologue: the DMAs of steps 0 .. NST-1 (each followed by 6 stores, as in the loop:
+  // ---- prologue: the DMAs of steps 0, 1, 2 (each followed by 6 stores, as in the loop:
   // placeholders at distinct out-of-range offsets -- hipcc merges identical stores -- except the
-  // last group, which holds step 0's Y1 stores), step 0 through stage 1 into x tile 0
+  // last group, which holds step 0's Y1 stores), steps 0 and 1 transformed, step 0 through stage
+  // 1 into x tile 0
   auto pad_stores = [&](int s, int n1, int n2) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -291,17 +295,16 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
       if (q < n2)
         __builtin_amdgcn_raw_buffer_store_b128(mk_u32x4(0, 0, 0, 0), rs2, (int)(0xFFF00000u + (uint32_t)(s * 8 + 4 + q) * 4096u), 0, 0);
   };
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s) {
-    dma_step(s, s);
-    pad_stores(s, 4, 2);
-  }
-  // step 0 landed: newer are its 6 stores and NST - 2 (DMA, 6 stores) groups
-  wait_vm<6 + (NST - 2) * 9>();
+  dma_step(0, 0);
+  pad_stores(0, 4, 2);
+  dma_step(1, 1);
+  pad_stores(1, 4, 2);
+  wait_vm<6>();   // steps 0 and 1 landed
   barrier_lds();
   transform(0);
+  transform(1);
   barrier_lds();
-  dma_step(NST - 1, NST - 1);
+  dma_step(2, 2);
   {
     f32x4 acc1[2];
     uint32_t pa[2][2], pb[2][2];
@@ -314,18 +317,17 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
       store1(pa, pb, hq, o1);
     }
   }
-  pad_stores(NST - 1, 0, 2);
+  pad_stores(2, 0, 2);
 
   uint32_t out1 = o1 + MS * N1 * 2, out2 = o2;
   for (int t = 0; t < nsteps; ++t) {
-    const int s1i = (t + 1) % NST;   // stage of step t + 1
-    // step t + 1 landed (newer: 6 stores and NST - 2 iterations); every wave is past iteration
-    // t - 1, so x tile t & 1 is complete and the stage of step t is free
+    const int s1i = (t + 1) % NST;   // stage of step t + 1 (transformed in iteration t - 1)
+    // step t + 2 landed; every wave is past iteration t - 1, so x tile t & 1 and step t + 1's
+    // transform are complete and the stage of step t is free
     wait_vm<VM_WAIT>();
     barrier_lds();
-    dma_step(t + NST, t % NST);
-    transform(s1i);
-    barrier_lds();
+    dma_step(t + 3, t % NST);
+    transform((t + 2) % NST);
     const char *st1 = lds + s1i * STAGE;
     const char *xr = lds + OFF_X + (t & 1) * XT;
     char *xw = lds + OFF_X + ((t + 1) & 1) * XT;
