@@ -127,6 +127,11 @@ typedef struct {
   const uint8_t *w_scale; /* [Ncols] E8M0 scale of each W row (PCS_FLAG_AW_FP8) */
   const void *W2;       /* [Ncols, K - K1] dtype: the second W block (PCS_PRO_CAT) */
   int32_t K1;           /* PCS_PRO_CAT: width of A (a multiple of the 32/16-element k-step) */
+  /* bf16 EPI_FWD / PRO_BNRELU with K = Ncols = 64 and no dropout bits (conv3 on the streaming
+   * kernel): per chunk [K*K + K] fp32 = x^T x and the column sums of the prologue's output
+   * x = relu(A*s + t) as rounded to bf16 -- conv3's input a2, whose Gram gives bn_seg1's
+   * statistics (pcs_bn_stats_gram_sbias).  [B*chunks_per_scene][K*K + K]; NULL = none. */
+  float *gram;
 } pcs_gemm_args;
 
 /* Fills chunks_per_scene (if 0) and returns rows per chunk (>0) or a negative error.  The

@@ -38,7 +38,7 @@ class GemmArgs(ct.Structure):
         ("Yp", _vp), ("es", _vp), ("et", _vp), ("emean", _vp), ("erstd", _vp),
         ("stats", _vp), ("pool", _vp), ("flags", _i32),
         ("pool_w", _vp), ("pool_ldw", _i64), ("pool_c", _i32), ("w_scale", _vp),
-        ("W2", _vp), ("K1", _i32),
+        ("W2", _vp), ("K1", _i32), ("gram", _vp),
     ]
 
 

@@ -460,7 +460,10 @@ __global__ __launch_bounds__(256) void bn_stats_gram_sbias_kernel(const float *_
                                                                   int64_t B, int64_t N, const float *__restrict__ W,
                                                                   int64_t ldw, int Cin, int C,
                                                                   const float *__restrict__ sbias, float *__restrict__ stats) {
+  // a workgroup: 16 channels x 16 threads; thread e of a channel takes rows p = e, e + 16, ..
+  // of Cw w and of S_b . w, and the 16 partial sums meet by shuffles
   __shared__ double cw[64 * 64];
+  __shared__ double wl[16][64];
   const int tid = threadIdx.x;
   for (int i = tid; i < Cin * Cin; i += 256) {
     const int p = i / Cin, q = i % Cin;
@@ -468,27 +471,28 @@ __global__ __launch_bounds__(256) void bn_stats_gram_sbias_kernel(const float *_
     for (int b = 0; b < B; ++b) s += (double)Sb[b * Cin + p] * (double)Sb[b * Cin + q];
     cw[i] = (double)G[(int64_t)p * Cin + q] - s / (double)N;
   }
+  const int cl = tid >> 4, e = tid & 15;
+  const int c = blockIdx.x * 16 + cl;
+  for (int q = e; q < 64; q += 16) wl[cl][q] = (c < C && q < Cin) ? (double)W[(int64_t)c * ldw + q] : 0.0;
   __syncthreads();
-  const int c = blockIdx.x * 256 + tid;
-  if (c >= C) return;
-  const float *wr = W + (int64_t)c * ldw;
-  double wv[64];   // (fixed trip counts: the vector stays in registers)
-#pragma unroll
-  for (int p = 0; p < 64; ++p) wv[p] = p < Cin ? (double)wr[p] : 0.0;
   double m2 = 0.0;
-  for (int p = 0; p < Cin; ++p) {
+  for (int p = e; p < Cin; p += 16) {
     double u = 0.0;
-#pragma unroll
-    for (int q = 0; q < 64; ++q) u += q < Cin ? cw[p * Cin + q] * wv[q] : 0.0;
-    m2 += (double)wr[p] * u;
+    for (int q = 0; q < Cin; ++q) u += cw[p * Cin + q] * wl[cl][q];
+    m2 += wl[cl][p] * u;
   }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) m2 += __shfl_xor(m2, o);
   if (m2 < 0.0) m2 = 0.0;
   for (int b = 0; b < B; ++b) {
     double sw = 0.0;
+    for (int p = e; p < Cin; p += 16) sw += (double)Sb[b * Cin + p] * wl[cl][p];
 #pragma unroll
-    for (int p = 0; p < 64; ++p) sw += p < Cin ? (double)Sb[b * Cin + p] * wv[p] : 0.0;
-    const double mean = sw / (double)N + (sbias ? (double)sbias[b * C + c] : 0.0);
-    *reinterpret_cast<float2 *>(stats + ((int64_t)b * C + c) * 2) = make_float2((float)mean, (float)(m2 / (double)B));
+    for (int o = 1; o < 16; o <<= 1) sw += __shfl_xor(sw, o);
+    if (e == 0 && c < C) {
+      const double mean = sw / (double)N + (sbias ? (double)sbias[b * C + c] : 0.0);
+      *reinterpret_cast<float2 *>(stats + ((int64_t)b * C + c) * 2) = make_float2((float)mean, (float)(m2 / (double)B));
+    }
   }
 }
 
@@ -530,7 +534,7 @@ extern "C" int pcs_bn_stats_gram_sbias(const float *G, const float *Sb, int64_t 
                                        float *stats, pcs_stream_t stream) {
   if (!G || !Sb || !W || !stats || num_scenes <= 0 || scene_rows <= 0 || Cin <= 0 || Cin > 64 || C <= 0 || ldw < Cin)
     return pcs_set_einval("pcs_bn_stats_gram_sbias", "bad arguments (1 <= Cin <= 64, ldw >= Cin)");
-  hipLaunchKernelGGL(bn_stats_gram_sbias_kernel, dim3((C + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(bn_stats_gram_sbias_kernel, dim3((C + 15) / 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      G, Sb, num_scenes, scene_rows, W, ldw, Cin, C, sbias, stats);
   PCS_CHECK_LAUNCH();
   return 0;

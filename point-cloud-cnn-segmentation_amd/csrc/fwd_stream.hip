@@ -33,6 +33,9 @@ namespace {
 constexpr int THREADS = 512;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 PCS_DEV int xcd_remap(int bid, int nb) {
   const int q = nb >> 3, r = nb & 7, x = bid & 7;
@@ -153,10 +156,18 @@ template <int K, int NCOLS, bool MASK, bool C8 = false> struct FsGeo {
 // ds_read_b128 lane group touches at one logical slot (128-B rows hold two rows per bank row)
 template <int K> PCS_DEV int fsw(int r) { return K == 64 ? ((r >> 1) & 7) : (r & 15); }
 
-template <int K, int NCOLS, int EPI, bool MASK, bool SBIAS, bool C8 = false>
+// GRAM (conv3: K = NCOLS = 64, one workgroup per chunk): the chunk's x^T x and column sums of
+// the transformed operand x = relu(bn2(y2)) = a2, from the stage the MFMAs read (transposed
+// ds_read_b64_tr_b16 fragments, k = rows; rows past the slice are zeroed by the transform).
+// Wave w accumulates the 16 x 16 blocks (w / 2, 2 (w % 2)) and (w / 2, 2 (w % 2) + 1) of the
+// full 64 x 64 product; the column sums come from the transform (each thread's 8 channels,
+// summed over its rows, then over the threads of those channels at the chunk end).
+template <int K, int NCOLS, int EPI, bool MASK, bool SBIAS, bool C8 = false, bool GRAM = false>
 __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, int64_t rows_per_chunk) {
   typedef FsGeo<K, NCOLS, MASK, C8> F;
   static_assert(!C8 || EPI == PCS_EPI_BNRELU, "fp8 output: the BN+ReLU epilogue (a5)");
+  static_assert(!GRAM || (K == 64 && NCOLS == 64 && EPI == PCS_EPI_FWD && !MASK && !SBIAS && !C8 && F::ILV),
+                "Gram of the operand: conv3 only");
   constexpr int NB = F::NB, MS = F::MS, NST = F::NST, CT = F::CT, RT = F::RT, KS = F::KS;
   constexpr int ROWB = F::ROWB, SPR = F::SPR;
   constexpr int NCB = NCOLS / NB;
@@ -293,8 +304,9 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
     }
   };
 
+  float gsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // GRAM: column sums of channels 8 tc ..
   // ---- in-place BN + ReLU (+ dropout) of a landed stage: each element once
-  auto transform_pass = [&](int sidx, int p) {
+  auto transform_pass = [&](int sidx, int p, int rem) {
     char *st = lds + sidx * F::STAGE;
     {
       const int r = trow + p * (THREADS / SPR);
@@ -309,12 +321,21 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
         const u32x4 m = *reinterpret_cast<const u32x4 *>(lds + F::OFF_LUT + byte * 16);
         out = mk_u32x4(out[0] & m[0], out[1] & m[1], out[2] & m[2], out[3] & m[3]);
       }
+      if constexpr (GRAM) {   // rows past the slice (clamped copies of its last row) out of the Gram
+        if (r >= rem) out = mk_u32x4(0, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gsum[2 * e] += bf2f(out[e] & 0xffffu);
+          gsum[2 * e + 1] += bf2f(out[e] >> 16);
+        }
+      }
       *q = out;
     }
   };
-  auto transform = [&](int sidx) {
+  auto step_rem = [&](int s) { return (int)pcs_min64(hi - (lo + (int64_t)s * MS), MS); };
+  auto transform = [&](int sidx, int rem) {
 #pragma unroll
-    for (int p = 0; p < F::TPASS; ++p) transform_pass(sidx, p);
+    for (int p = 0; p < F::TPASS; ++p) transform_pass(sidx, p, rem);
   };
 
   // ---- output through one buffer descriptor for the slice's rows (columns n0 .. of the block):
@@ -366,8 +387,25 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
   // step 0 landed: newer are the SPS stores after it and NST-2 (DMA, stores) groups
   wait_vm<F::SPS + (NST - 2) * (F::LPS + F::SPS)>();
   barrier_lds();
-  transform(0);
+  transform(0, step_rem(0));
   barrier_lds();
+
+  // GRAM: fragment offsets (within a stage) of k-step ks, row quad h: lane 4 q + p of group g
+  // reads row 32 ks + 8 g + 4 h + q, columns 16 blk + 4 p .. + 3 (8 B at logical slot
+  // 2 blk + p / 2, half p % 2, of the permuted 128-B row)
+  auto gfrag = [&](const char *st, int ks, int blk) __attribute__((always_inline)) {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int r0 = 32 * ks + 8 * g + q, r1 = r0 + 4;
+    const int sl = 2 * blk + (p >> 1);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4 *)(st + r0 * ROWB + ((sl ^ fsw<K>(r0)) << 4) + 8 * (p & 1)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4 *)(st + r1 * ROWB + ((sl ^ fsw<K>(r1)) << 4) + 8 * (p & 1)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  const int gbi = wid >> 1, gbj = 2 * (wid & 1);
+  f32x4 gacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
   int sc = 0;
   uint32_t o_out = o_st;
@@ -405,8 +443,20 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
         constexpr int PER = KS / F::TPASS;   // MFMA k-steps per transform pass
         if ((kk + 1) % PER == 0 && more) {
           __builtin_amdgcn_sched_barrier(0);
-          transform_pass(sn, kk / PER);
+          transform_pass(sn, kk / PER, step_rem(t + 1));
           __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    if constexpr (GRAM) {
+#pragma unroll
+      for (int ks = 0; ks < MS / 32; ++ks) {
+        const bf16x8 fa = gfrag(st, ks, gbi);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 fb = gfrag(st, ks, gbj + j);
+          gacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, gacc[j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);   // (one pair of fragments live at a time)
         }
       }
     }
@@ -537,7 +587,7 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       o_stg += MS * NCOLS * 2;
     }
     if constexpr (!F::ILV) {
-      if (more) transform(sn);
+      if (more) transform(sn, step_rem(t + 1));
     }
     barrier_lds();
     sc = sc + 1 == NST ? 0 : sc + 1;
@@ -583,6 +633,32 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       const int64_t o = (int64_t)chunk * NCOLS + n0 + c;
       *reinterpret_cast<float2 *>(a.stats + o * 2) =
           EPI == PCS_EPI_BNRELU ? make_float2(p.x, 0.f) : make_float2(p.y, p.z);
+    }
+  }
+  if constexpr (GRAM) {   // the chunk's [64 x 64 | 64] record: G[16 bi + 4 g + r][16 bj + l16]
+    float *gr = a.gram + (int64_t)chunk * (K * K + K);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gr[(16 * gbi + 4 * g + r) * K + 16 * (gbj + j) + l16] = gacc[j][r];
+    // column sums: the 8 lanes of a wave that share tc (lane % 8), then the 8 waves via LDS
+    // (the statistics merge above is done with the red area)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) gsum[e] += __shfl_xor(gsum[e], o);
+    float *gs = reinterpret_cast<float *>(lds + F::OFF_RED);
+    __syncthreads();
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gs[wid * 64 + 8 * lane + e] = gsum[e];
+    }
+    __syncthreads();
+    if (tid < K) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += gs[w * 64 + tid];
+      gr[K * K + tid] = v;
     }
   }
 }
@@ -651,7 +727,11 @@ int pcs_fwd_stream_launch(const pcs_gemm_args &a, int64_t rows_per_chunk, hipStr
   } else if (FsShape<64, 128>::is(a)) {
     PCS_FS(64, 128, PCS_EPI_FWD, false, false);
   } else if (FsShape<64, 64>::is(a)) {
-    PCS_FS(64, 64, PCS_EPI_FWD, false, false);
+    if (a.gram)
+      hipLaunchKernelGGL((fwd_stream_kernel<64, 64, PCS_EPI_FWD, false, false, false, true>), dim3(nb), dim3(THREADS), 0,
+                         s, a, rows_per_chunk);
+    else
+      PCS_FS(64, 64, PCS_EPI_FWD, false, false);
   } else {
     return pcs_set_einval("pcs_gemm", "streaming forward: unsupported shape");
   }

@@ -661,6 +661,10 @@ extern "C" int pcs_gemm(const pcs_gemm_args *ap, pcs_stream_t stream) {
   const int64_t rpc = pcs_gemm_geometry(&a);
   if (rpc < 0) return (int)rpc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a.gram && !(a.K == 64 && a.Ncols == 64 && a.epilogue == PCS_EPI_FWD && !a.a_mask && !a.scene_bias &&
+                  pcs_fwd_stream_applicable(a)))
+    return pcs_set_einval("pcs_gemm", "gram (the operand's Gram) needs bf16 PRO_BNRELU + EPI_FWD, K = Ncols = 64, "
+                                      "no dropout bits, on the streaming kernel");
   if (pcs_fwd_stream_applicable(a)) return pcs_fwd_stream_launch(a, rpc, s);
   if (wide_class(a) && pcs_gemm_wres_applicable(a)) return pcs_gemm_wres_launch(a, rpc, s);
   if (wide_class(a) && pcs_gemm_glds_applicable(a)) {

@@ -147,6 +147,7 @@ class Saved:
     logits: torch.Tensor = None
     wc: dict = None                               # cast weights used by this pass
     gram4: tuple = None                           # (G, S) of a4 when the forward computed it
+    gram2: object = None                          # conv3's per-chunk [G | S] records of a2 (fused seg12)
     a5_colsum: torch.Tensor = None                # bf16: per-chunk column sums of a5 (conv5 epilogue)
     mask_bufs: tuple = None                       # dropout keep bits drawn on the side stream
     gram5: tuple = None                           # bf16/fp8: (G, per-scene S, workspace) of a5, from the forward
@@ -454,7 +455,15 @@ class Engine:
 
         tkw = {"dtype": L.F32} if trunk32 else {}
         layer("conv2", "conv1", "bn1", 64, 64, "bn2", P["conv2.bias"], **tkw)
-        layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"], **tkw)
+        # the fused seg_conv1 + seg_conv2 forward takes bn_seg1's statistics from the Gram of a2,
+        # which conv3's streaming pass forms from the operand it already has in LDS
+        fused12 = train and self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC) and self.fused_seg12
+        gkw = {}
+        if fused12:
+            cps3, _ = self.geometry(B, N, 64, 64)
+            sv.gram2 = torch.empty(B * cps3, 64 * 64 + 64, dtype=torch.float32, device=dev)
+            gkw = {"gram": sv.gram2}
+        layer("conv3", "conv2", "bn2", 64, 64, "bn3", P["conv3.bias"], **tkw, **gkw)
         layer("conv4", "conv3", "bn3", 64, 128, "bn4", P["conv4.bias"], **tkw)
 
         def bridge(conv, bn, K, split):
@@ -574,7 +583,6 @@ class Engine:
         L.call("pcs_scene_gemv", L.ptr(sv.g), B, 1024, L.ptr(Ws1), Ws1.shape[1], 64,
                L.ptr(P["seg_conv1.bias"]), 512, L.ptr(sbias), L.ptr(soff), s)
         sv.sbias_s1 = sbias   # the stored Y'_seg1 = a2 W_l^T + sbias[b] (the folded backward)
-        fused12 = train and self.dt == L.BF16 and not (self.flags & L.FLAG_GENERIC) and self.fused_seg12
         if fused12:
             pass   # with seg_conv2 below (pcs_fwd_seg12)
         elif trunk32:
@@ -631,11 +639,15 @@ class Engine:
         dev = sv.x.device
         s = self._stream()
         c2 = sv.bn["bn2"]
-        G2, _, gws = self._gram(sv.ys["conv2"], c2.scale, c2.shift, B, N, 64, tag="fwd_stats:seg_conv1")
-        sps = ct.c_int32(0)
-        L.load().pcs_gram_workspace(B, N, 64, self.dt, ct.byref(sps))
-        Sb = torch.empty(B, 64, dtype=torch.float32, device=dev)
-        L.call("pcs_reduce_partials_grouped", L.ptr(gws[B * sps.value * 64 * 64:]), B, sps.value, 64, 1.0, L.ptr(Sb), s)
+        # conv3's per-chunk [G | S] records of a2 -> per scene, then G2 over the scenes
+        rec = 64 * 64 + 64
+        cps3 = sv.gram2.shape[0] // B
+        per_scene = torch.empty(B, rec, dtype=torch.float32, device=dev)
+        L.call("pcs_reduce_partials_grouped", L.ptr(sv.gram2), B, cps3, rec, 1.0, L.ptr(per_scene), s)
+        tot = torch.empty(rec, dtype=torch.float32, device=dev)
+        L.call("pcs_reduce_partials", L.ptr(per_scene), B, rec, 1.0, L.ptr(tot), 1, rec, s)
+        G2 = tot[:64 * 64]
+        Sb = per_scene[:, 64 * 64:].contiguous()
         Ws1 = P["seg_conv1.weight"]
         Ws1_r = self._rounded(Ws1)
         st1 = torch.empty(B, 512, 2, dtype=torch.float32, device=dev)

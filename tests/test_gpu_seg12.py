@@ -157,3 +157,46 @@ def test_train_step_fused_vs_two_passes():
     for n in bt:
         e = float((bf[n] - bt[n]).norm() / bt[n].norm())
         assert e < 1e-3, (n, e)
+
+
+@pytest.mark.parametrize("B,N", [(2, 3000), (3, 4097), (1, 100)])
+def test_conv3_forward_gram_of_its_operand(B, N):
+    """conv3's streaming forward with the gram record (the Gram of a2 = relu(bn2(y2)) that
+    bn_seg1's statistics use): y3 bit-identical to the pass without it, and the per-chunk
+    [G | S] records sum to the fp64 Gram and per-scene column sums of the bf16 a2 (rows past
+    each chunk's slice excluded: ragged N, one chunk smaller than a step)."""
+    import pcs_amd._lib as L
+    g = torch.Generator(device="cpu").manual_seed(B * 31 + N)
+    M = B * N
+    y2 = torch.randn(M, 64, generator=g).to(torch.bfloat16).to(DEV)
+    s2, t2 = (torch.randn(64, generator=g) * 0.5 + 1.0).to(DEV), (torch.randn(64, generator=g) * 0.3).to(DEV)
+    W3 = (torch.randn(64, 64, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    outs = []
+    for with_gram in (False, True):
+        y3 = torch.empty(M, 64, dtype=torch.bfloat16, device=DEV)
+        a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=64, dtype=L.BF16, prologue=L.PRO_BNRELU,
+                       epilogue=L.EPI_FWD, chunks_per_scene=0, A=y2.data_ptr(), W=W3.data_ptr(), C=y3.data_ptr(),
+                       pa=s2.data_ptr(), pb=t2.data_ptr(), a_keep_scale=1.0, c_keep_scale=1.0)
+        L.load().pcs_gemm_geometry(ct.byref(a))
+        cps = a.chunks_per_scene
+        st = torch.empty(B * cps, 64, 2, device=DEV)
+        a.stats = st.data_ptr()
+        gr = torch.full((B * cps, 64 * 64 + 64), float("nan"), device=DEV)
+        if with_gram:
+            a.gram = gr.data_ptr()
+        L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((y3, st, gr, cps))
+    (y3a, sta, _, _), (y3b, stb, gr, cps) = outs
+    assert torch.equal(y3a.view(torch.int16), y3b.view(torch.int16))
+    assert torch.equal(sta, stb)
+    assert not torch.isnan(gr).any()
+    a2 = torch.relu(y2.float() * s2 + t2).to(torch.bfloat16).double()
+    G = gr[:, :4096].double().sum(0).view(64, 64)
+    Gref = a2.T @ a2
+    err = float((G - Gref).abs().max() / Gref.abs().max())
+    S = gr[:, 4096:].double().view(B, cps, 64).sum(1)
+    Sref = a2.view(B, N, 64).sum(1)
+    serr = float((S - Sref).abs().max() / Sref.abs().max())
+    print(f"B={B} N={N}: Gram rel err {err:.2e}, column sums {serr:.2e}")
+    assert err < 1e-4 and serr < 1e-4
