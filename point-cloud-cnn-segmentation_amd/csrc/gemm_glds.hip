@@ -510,22 +510,21 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
           // path) run on few tiles.
           const float *cur4 = lcur + wm * BN + wn * 64 + 4 * lg;
           const float *sgn4 = lsgn + wn * 64 + 4 * lg;
-          uint32_t beat = 0;   // bit j: this lane beats a running max in tile column block j
+          uint32_t beat = 0;   // bit 4 j + r: this lane beats the running max of column (j, r)
           if (signed_w && tile_full) {
             // PCS_FLAG_POOL_SIGNED_W: acc = sgn * y, 4 max3/max per column and a compare
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float4 c4 = *reinterpret_cast<const float4 *>(cur4 + j * 16);
               const float cc[4] = {c4.x, c4.y, c4.z, c4.w};
-              bool bj = false;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float t0 = max3f(acc[0][j][r], acc[1][j][r], acc[2][j][r]);
                 const float t1 = max3f(acc[3][j][r], acc[4][j][r], acc[5][j][r]);
                 const float t2 = max3f(acc[6][j][r], acc[7][j][r], t0);
-                bj |= max2f(t1, t2) >= cc[r];   // >=: an equal value may sit on an earlier row
+                // >=: an equal value may sit on an earlier row
+                beat |= (uint32_t)(max2f(t1, t2) >= cc[r]) << (4 * j + r);
               }
-              beat |= (uint32_t)bj << j;
             }
           } else {
 #pragma unroll
@@ -535,21 +534,19 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
               const float cc[4] = {c4.x, c4.y, c4.z, c4.w};
               const float gg[4] = {signed_w ? 1.f : g4.x, signed_w ? 1.f : g4.y, signed_w ? 1.f : g4.z,
                                    signed_w ? 1.f : g4.w};
-              bool bj = false;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 float mx = -__builtin_huge_valf();
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                   if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, gg[r] * acc[i][j][r]);
-                bj |= mx >= cc[r];
+                beat |= (uint32_t)(mx >= cc[r]) << (4 * j + r);
               }
-              beat |= (uint32_t)bj << j;
             }
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if (__builtin_amdgcn_ballot_w64((beat >> j) & 1u) == 0) continue;   // uniform
+            if (__builtin_amdgcn_ballot_w64((beat >> (4 * j)) & 0xFu) == 0) continue;   // uniform
             const float4 q = runp[cme];
             const float sgl = lsgn[cme - wm * BN];
             const float cur = sgl > 0.f ? q.x : -q.z;
@@ -559,6 +556,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               sg[r] = signed_w ? 1.f : sgn4[j * 16 + r];
+              vx[r] = -__builtin_huge_valf();
+              // only the columns some lane beats (late in a chunk usually one of the four)
+              if (__builtin_amdgcn_ballot_w64((beat >> (4 * j + r)) & 1u) == 0) continue;   // uniform
               float mx = -__builtin_huge_valf();
 #pragma unroll
               for (int i = 0; i < 8; ++i)
