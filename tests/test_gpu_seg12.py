@@ -67,7 +67,8 @@ def _fused(L, B, N, y2, s2, t2, W1, sbias, s1, t1, bits, W2, ks):
     return y1, out, st, rpc
 
 
-@pytest.mark.parametrize("B,N,mask", [(2, 3000, True), (3, 4097, True), (1, 100, False), (4, 2 ** 16, True)])
+@pytest.mark.parametrize("B,N,mask", [(2, 3000, True), (3, 4097, True), (1, 100, False), (4, 2 ** 16, True),
+                                      (1, 20, True), (2, 33, True)])
 def test_fused_matches_two_passes(B, N, mask):
     import pcs_amd._lib as L
     ops = list(_ops(B, N, seed=B * 7 + N))
@@ -159,7 +160,7 @@ def test_train_step_fused_vs_two_passes():
         assert e < 1e-3, (n, e)
 
 
-@pytest.mark.parametrize("B,N", [(2, 3000), (3, 4097), (1, 100)])
+@pytest.mark.parametrize("B,N", [(2, 3000), (3, 4097), (1, 100), (1, 20), (2, 65)])
 def test_conv3_forward_gram_of_its_operand(B, N):
     """conv3's streaming forward with the gram record (the Gram of a2 = relu(bn2(y2)) that
     bn_seg1's statistics use): y3 bit-identical to the pass without it, and the per-chunk
