@@ -356,8 +356,9 @@ int pcs_head(const pcs_head_args *args, pcs_stream_t stream);
 int pcs_ce_weight_sum(const int64_t *labels, int64_t M, const float *class_weight,
                       int32_t C, int64_t *counts_ws, float *out, pcs_stream_t stream);
 
-/* Dropout(p) keep bits (P:96, P:124, P:126): Philox4x32-7(seed, offset + element),
- * keep = u >= p, 8 bits per byte along the channel dimension; bits[M, C/8]. */
+/* Dropout(p) keep bits (P:96, P:124, P:126): Philox4x32-7 keyed by seed, counter (call index,
+ * offset), one call per 16 elements; 16-bit uniforms u, keep = u >= round(p * 65536) (p within
+ * 2^-17 of 1 keeps nothing); 8 bits per byte along the channel dimension; bits[M, C/8]. */
 int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
                      uint8_t *bits, pcs_stream_t stream);
 /* The same bits from at most max_workgroups 256-thread workgroups (<= 0: as many as the words

@@ -1007,6 +1007,9 @@ __global__ void ce_wsum_kernel(const unsigned long long *counts, const float *w,
 
 // Philox4x32-7 (Salmon et al. 2011: 7 rounds already pass BigCrush; the 10-round default's
 // margin cost 0.5 ms per step in dropout_bits, which is ALU-bound)
+PCS_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // a ^ b ^ c in one v_bitop3_b32
+}
 PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
@@ -1014,23 +1017,36 @@ PCS_DEV void philox(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr[2];
     const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
     const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
-    const uint32_t n0 = h1 ^ ctr[1] ^ k0, n2 = h0 ^ ctr[3] ^ k1;
+    const uint32_t n0 = xor3(h1, ctr[1], k0), n2 = xor3(h0, ctr[3], k1);
     ctr[0] = n0; ctr[1] = l1; ctr[2] = n2; ctr[3] = l0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
 }
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// per 16-bit half of x: 1 where the half is below thr (dropped), at bits 0 and 16
+// (one2 = {1, 1} passed opaque: with a known 1 hipcc folds min(sat_sub(.), 1) back into a
+// compare + select per half)
+PCS_DEV uint32_t drop2(uint32_t x, uint32_t thr2, u16x2 one2) {
+  const u16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, thr2), __builtin_bit_cast(u16x2, x));
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, one2));
+}
 __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbytes, uint32_t thr,
                                     uint8_t *bits) {
-  // bytes 2k and 2k+1 (elements 16k .. 16k+15) come from one Philox call (counter k): its 16
-  // random bytes r0..r15 give element e of the pair the 16-bit uniform (r_e << 8) | r_(e^1), so
-  // every element still keeps with probability exactly 1 - thr / 65536 (two independent bytes),
-  // and two paired elements depend on each other only through the low byte, i.e. only when one
-  // high byte equals thr >> 8.  Per 16-bit half x of an output word: element 2h+1 reads x
-  // itself, element 2h its byte swap.  Half the Philox calls of one call per byte (the kernel is
-  // ALU-bound on the 64-bit multiplies).  A thread makes 4 consecutive bytes (2 calls) and
-  // stores them as one word; a grid smaller than the words (pcs_dropout_bits_bounded) strides
-  // over them: the bits depend on j only
+  const uint32_t thr2 = thr | (thr << 16);   // (thr <= 65535: host)
+  u16x2 one2 = {1, 1};
+  asm volatile("" : "+v"(one2));
+  // A thread makes 4 consecutive keep bytes (elements 32 w .. 32 w + 31 of word w) from two
+  // Philox calls (counters 2 w, 2 w + 1) and stores them as one word.  Call q's 16 random bytes
+  // r0..r15 give 16 elements the 16-bit uniforms (r_e << 8) | r_(e^1): every element keeps with
+  // probability exactly 1 - thr / 65536 (two independent bytes), and the two elements that share
+  // a byte pair depend on each other only through the low byte (only when one high byte equals
+  // thr >> 8).  Random word i's half h (natural, v = 1) and its byte swap (v = 0) go to bit
+  // 16 h + 8 q + 2 i + v: the two elements of a pair are adjacent (2k, 2k + 1).  Each
+  // v_pk_sub_u16 (clamped) + v_pk_min_u16 turns two uniforms into two drop bits.  Half the
+  // Philox calls of one call per byte (the kernel is ALU-bound on the 64-bit multiplies); a grid
+  // smaller than the words (pcs_dropout_bits_bounded) strides over them: the bits depend on
+  // w only
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; j0 < nbytes; j0 += stride) {
   uint32_t word = 0;
@@ -1039,20 +1055,15 @@ __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbyt
     const int64_t k = (j0 >> 1) + q;
     uint32_t ctr[4] = {(uint32_t)k, (uint32_t)((uint64_t)k >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
     philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-    uint32_t b = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint32_t x = ctr[i];
       const uint32_t sw = __builtin_amdgcn_perm(0u, x, 0x02030001u);   // both halves byte-swapped
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t nat = (x >> (16 * h)) & 0xffffu, swp = (sw >> (16 * h)) & 0xffffu;
-        b |= (swp >= thr ? 1u : 0u) << (4 * i + 2 * h);
-        b |= (nat >= thr ? 1u : 0u) << (4 * i + 2 * h + 1);
-      }
+      word |= drop2(sw, thr2, one2) << (8 * q + 2 * i);
+      word |= drop2(x, thr2, one2) << (8 * q + 2 * i + 1);
     }
-    word |= b << (16 * q);
   }
+  word = ~word;   // keep = not dropped
   if (j0 + 4 <= nbytes && ((reinterpret_cast<uintptr_t>(bits) & 3) == 0)) {
     *reinterpret_cast<uint32_t *>(bits + j0) = word;
   } else {
@@ -1396,6 +1407,10 @@ extern "C" int pcs_dropout_bits_bounded(uint64_t seed, uint64_t offset, int64_t 
   const int64_t nbytes = M * (C / 8);
   if (nbytes <= 0) return 0;
   const uint32_t thr = (uint32_t)(p * 65536.0f + 0.5f);
+  if (thr > 65535u) {   // every 16-bit uniform is below 65536: nothing kept
+    const hipError_t e = hipMemsetAsync(bits, 0, (size_t)nbytes, reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : pcs_set_error(e, "pcs_dropout_bits");
+  }
   int64_t nb = blocks_for((nbytes + 3) / 4, 256);
   if (max_workgroups > 0 && nb > max_workgroups) nb = max_workgroups;
   hipLaunchKernelGGL(dropout_bits_kernel, dim3((unsigned)nb), dim3(256), 0,

@@ -198,9 +198,9 @@ def test_dropout_bits_statistics_and_determinism():
     assert torch.equal(a, b) and not torch.equal(a, c)
     # channels are independent: per-channel keep rates all near 0.7
     assert np.abs(bits.mean(0) - 0.7).max() < 0.02
-    # elements 2i and 2i+1 of a 16-element group share one byte of their 16-bit uniforms (the
-    # high byte of one is the low byte of the other, csrc/small.hip dropout_bits_kernel): their
-    # joint keep rate is the exact enumeration over the two bytes, ~0.49 = 0.7^2
+    # elements 2k and 2k+1 share one byte pair of their 16-bit uniforms (the high byte of one is
+    # the low byte of the other, csrc/small.hip dropout_bits_kernel): their joint keep rate is
+    # the exact enumeration over the two bytes, ~0.49 = 0.7^2
     thr = int(0.3 * 65536.0 + 0.5)
     r = np.arange(256)
     u_a = (r[:, None] << 8) | r[None, :]
@@ -216,6 +216,12 @@ def test_dropout_bits_statistics_and_determinism():
         d = torch.zeros(M - 3, C // 8, dtype=torch.uint8, device=DEV)
         L.call("pcs_dropout_bits_bounded", 123, 0, M - 3, C, 0.3, L.ptr(d), wg, L.stream_ptr())
         assert torch.equal(d, a[:M - 3])
+    # the ends of p: 0 keeps everything; within 2^-17 of 1 (threshold 65536) keeps nothing
+    e = torch.zeros(257, C // 8, dtype=torch.uint8, device=DEV)
+    L.call("pcs_dropout_bits", 123, 0, 257, C, 0.0, L.ptr(e), L.stream_ptr())
+    assert bool((e == 255).all())
+    L.call("pcs_dropout_bits", 123, 0, 257, C, 1.0 - 2.0 ** -20, L.ptr(e), L.stream_ptr())
+    assert bool((e == 0).all())
 
 
 def test_train_mode_random_dropout_runs_and_differs():
