@@ -398,8 +398,9 @@ class Engine:
             m2.record_stream(side)
             sv.mask_bufs = (m1, m2)
         # bf16 (stored-a5 Gram): draw beside the Gram of a5, MFMA-bound at 214 VGPRs x 2 waves per
-        # SIMD, with two 256-thread workgroups per CU (24 VGPRs a wave: they fit beside it and use
-        # its idle VALU issue); otherwise at the start of the forward with a full grid
+        # SIMD, with three 256-thread workgroups per CU (24 VGPRs a wave: they fit beside it and
+        # use its idle VALU issue; 0.77 ms per call against 0.83 with two, the Gram and the step
+        # unchanged, tools/draw_wg.py); otherwise at the start of the forward with a full grid
         draw_beside_gram = train and masks is None and self._raw_gram() and not self.fp8 and self.draw_beside_gram
         if train and masks is None and not draw_beside_gram:
             draw_masks()
@@ -528,7 +529,7 @@ class Engine:
                 raise L.PcsError(L.load().pcs_last_error().decode())
             gws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
             if draw_beside_gram:
-                draw_masks(2 * torch.cuda.get_device_properties(dev).multi_processor_count)
+                draw_masks(3 * torch.cuda.get_device_properties(dev).multi_processor_count)
             self._launch("wgrad:global_feat", "pcs_gram_raw", L.ptr(a5), M, 1024, self.a5_dt, L.ptr(gws), nbytes,
                          L.ptr(G5), s)
             # per-scene column sums of a5 from conv5's per-chunk partials (chunks are scene-aligned)
