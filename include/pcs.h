@@ -654,11 +654,12 @@ int pcs_gather_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_
  *   transposed = 0:  Y[o] = b + sum_t W_t X[o s - p + t]                  Do = (Di + 2p - k) / s + 1
  *   transposed = 1:  Y[o] = b + sum_t W_t X[(o + p - t) / s] (exact only)  Do = (Di - 1) s - 2p + k + op
  * (op = torch's output_padding, 0 <= op < s, taken from the Do / Ho / Wo given).
- * k in 1..3, s in {1, 2}, 0 <= p < k.  pcs_conv3d: Cin % 32 == 0, Cout % 64 == 0 (the Python
- * layer zero-pads other channel counts to multiples of 64).  The input gradient of either form is
+ * k in 1..3, s in {1, 2}, 0 <= p < k.  pcs_conv3d: Cin % 32 == 0, Cout % 32 == 0 (64-channel
+ * tiles, 32-channel tiles where a count is an odd multiple of 32; the Python layer zero-pads other
+ * channel counts to multiples of 32).  The input gradient of either form is
  * the other form applied to dY with pcs_conv3d_weight_t(W) and the grids swapped (a strided
  * convolution's skipped trailing input planes come back as the transposed form's op).  pcs_conv3d_wgrad: dW [Cout, k, k, k, Cin] f32 = sum_o dY[o] (x) X[in(o, t)]
- * over the forward's index map, db [Cout] f32 = sum_o dY[o] (may be NULL); Cin, Cout % 64 == 0;
+ * over the forward's index map, db [Cout] f32 = sum_o dY[o] (may be NULL); Cin, Cout % 32 == 0;
  * fp32 partials summed in a fixed order (deterministic).
  */
 typedef struct {

@@ -111,19 +111,21 @@ PCS_DEV void decode_class(const PClass &q, int64_t u, int &b, int &z, int &y, in
   b = (int)(u / q.nz);
 }
 
-// BMT = 64 or 128 output voxels per tile (4 waves as 2 x 2: wave tile BMT/2 x 32); KST = 32 or
-// 64 input channels per k-step (64: whole 128-B voxel rows per load, 2x the MFMAs per barrier)
-template <int BMT, int KST, bool OUT_BF16>
+// BMT = 64 or 128 output voxels per tile (4 waves as 2 x 2: wave tile BMT/2 x BNT/2); KST = 32 or
+// 64 input channels per k-step (64: whole 128-B voxel rows per load, 2x the MFMAs per barrier);
+// BNT = 64 or 32 output channels per tile (32: a 32-channel U-Net level without zero channels)
+template <int BMT, int KST, bool OUT_BF16, int BNT = BN>
 __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                          const bf16_t *__restrict__ W, const float *__restrict__ bias,
                                                          void *__restrict__ Y, int64_t M) {
   constexpr int RB = KST * 2;          // LDS row bytes
   constexpr int CPR = KST / 8;         // 16-B chunks per row
   constexpr int RPP = THREADS / CPR;   // rows staged per pass
-  constexpr int HA = BMT / RPP, HB = BN / RPP;
+  constexpr int HA = BMT / RPP, HB = (BNT + RPP - 1) / RPP;   // (BNT < RPP: the first BNT rows' threads)
   constexpr int TI = BMT / 32;         // 16-row MFMA tiles per wave
+  constexpr int TJ = BNT / 32;         // 16-channel MFMA tiles per wave
   constexpr int KK = KST / 32;         // MFMA k-steps per k-step
-  __shared__ __attribute__((aligned(16))) char lds[2][(BMT + BN) * RB];   // per buffer: A | B
+  __shared__ __attribute__((aligned(16))) char lds[2][(BMT + BNT) * RB];   // per buffer: A | B
   auto swzf = [](int row, int slot) { return KST == 32 ? cswz(row, slot) : (slot ^ ((row >> 1) & 7)); };
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
     m0 = (int64_t)(blockIdx.x >> 3) * BMT;
     if (m0 >= Mrows) return;   // uniform: this class has fewer tiles than the largest
   }
-  const int n0 = blockIdx.y * BN;
+  const int n0 = blockIdx.y * BNT;
   const int srow = tid / CPR, q = tid % CPR;   // staging: chunk q of rows srow + RPP h
   bool rv[HA];
   int vb[HA], vz[HA], vy[HA], vx[HA];
@@ -176,7 +178,8 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
       ra[h] = iv >= 0 ? *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + c0 + q * 8) : mk_u32x4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int h = 0; h < HB; ++h) rb[h] = *reinterpret_cast<const u32x4 *>(wrow + h * wstep + (int64_t)t * g.Cin + c0);
+    for (int h = 0; h < HB; ++h)
+      if (srow + RPP * h < BNT) rb[h] = *reinterpret_cast<const u32x4 *>(wrow + h * wstep + (int64_t)t * g.Cin + c0);
   };
   auto stage = [&](int buf) {
     char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
@@ -188,15 +191,15 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
 #pragma unroll
     for (int h = 0; h < HB; ++h) {
       const int r = srow + RPP * h;
-      *reinterpret_cast<u32x4 *>(tB + r * RB + swzf(r, q) * 16) = rb[h];
+      if (r < BNT) *reinterpret_cast<u32x4 *>(tB + r * RB + swzf(r, q) * 16) = rb[h];
     }
   };
 
-  f32x4 acc[TI][2];
+  f32x4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (nks > 0) {
     load(0);
     stage(0);
@@ -208,22 +211,22 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
     const char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      bf16x8 af[TI], bw[2];
+      bf16x8 af[TI], bw[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int r = wr * (BMT / 2) + i * 16 + lr;
         af[i] = *reinterpret_cast<const bf16x8 *>(tA + r * RB + swzf(r, kk * 4 + lg) * 16);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wc * 32 + j * 16 + lr;
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wc * (BNT / 2) + j * 16 + lr;
         bw[j] = *reinterpret_cast<const bf16x8 *>(tB + r * RB + swzf(r, kk * 4 + lg) * 16);
       }
       // W rows as the MFMA A operand: each lane ends with 4 consecutive output channels of one voxel
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (ks + 1 < nks) stage(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
     __syncthreads();
@@ -239,8 +242,8 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
       uo = (((int64_t)ob * g.Do + oz) * g.Ho + oy) * g.Wo + ox;
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int co = n0 + wc * 32 + j * 16 + 4 * lg;
+    for (int j = 0; j < TJ; ++j) {
+      const int co = n0 + wc * (BNT / 2) + j * 16 + 4 * lg;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (bias) {
         const float4 bb = *reinterpret_cast<const float4 *>(bias + co);
@@ -257,9 +260,11 @@ __global__ __launch_bounds__(THREADS) void conv3d_kernel(pcs_conv3d_geom g, cons
 }
 
 // ---- 3x3x3 stride-1 stencil (both forms) with the input block's halo staged in LDS once per
-// 64-channel slice: a 4 x 4 x 8 block of output voxels reads its 6 x 6 x 10 input halo (360
-// voxel rows) from L2 once and every tap's A operand from LDS at a shifted row, instead of
-// 27 gathers; the 27 taps' 64 x 64 weight tiles stream through a double buffer.
+// CS-channel slice (CS = 64, or 32 for a 32-channel level): a 4 x 4 x 8 block of output voxels
+// reads its 6 x 6 x 10 input halo (360 voxel rows) from L2 once and every tap's A operand from
+// LDS at a shifted row, instead of 27 gathers; the 27 taps' NT x CS weight tiles (NT = 64 or 32
+// output channels) stream through a double buffer.  The LDS images keep 128-B rows whatever CS
+// (a 32-channel slice fills the first four swizzled slots of a row).
 constexpr int SZ = 4, SY = 4, SX = 8;                      // output block: 128 voxels
 constexpr int GZ = SZ + 2, GY = SY + 2, GX = SX + 2;
 constexpr int HROWS = GZ * GY * GX;                        // 360 halo voxels
@@ -267,7 +272,7 @@ constexpr int HIMG = HROWS * 128, WTILE = 64 * 128;        // halo image (64 ch)
 
 PCS_DEV int swz8(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
-template <bool OUT_BF16>
+template <int CS, int NT, bool OUT_BF16>
 __global__ __launch_bounds__(THREADS) void stencil3_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                            const bf16_t *__restrict__ W, const float *__restrict__ bias,
                                                            void *__restrict__ Y) {
@@ -286,39 +291,43 @@ __global__ __launch_bounds__(THREADS) void stencil3_kernel(pcs_conv3d_geom g, co
   // first halo voxel: conv reads o - p + t, the transposed form o + p - t (t = 0..2)
   const int hz0 = tr ? oz0 + g.p - 2 : oz0 - g.p, hy0 = tr ? oy0 + g.p - 2 : oy0 - g.p,
             hx0 = tr ? ox0 + g.p - 2 : ox0 - g.p;
-  const int n0 = blockIdx.y * 64, Cin = g.Cin, cps = Cin / 64;
-  // wave tile: output rows wr*64 .. +64 (4 MFMA tiles), channels wc*32 .. +32; row r = (rz, ry, rx)
+  constexpr int CCH = CS / 8;                 // 16-B chunks per staged row
+  constexpr int WCH = NT * CCH;               // W tile chunks
+  constexpr int HW = (WCH + THREADS - 1) / THREADS;
+  constexpr int TJ = NT / 32, KK = CS / 32;
+  const int n0 = blockIdx.y * NT, Cin = g.Cin, cps = Cin / CS;
+  // wave tile: output rows wr*64 .. +64 (4 MFMA tiles), channels wc*NT/2 ..; row r = (rz, ry, rx)
   int hrow[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = wr * 64 + i * 16 + lr;
     hrow[i] = ((r >> 5) * GY + ((r >> 3) & 3)) * GX + (r & 7);
   }
-  u32x4 rw[2];   // W staging: 64 rows x 8 chunks, two per thread
+  u32x4 rw[HW];   // W staging: NT rows x CCH chunks
   auto loadw = [&](int t, int c0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = tid + THREADS * h, row = c >> 3, ch = c & 7;
-      rw[h] = *reinterpret_cast<const u32x4 *>(W + ((int64_t)(n0 + row) * 27 + t) * Cin + c0 + ch * 8);
+    for (int h = 0; h < HW; ++h) {
+      const int c = tid + THREADS * h, row = c / CCH, ch = c % CCH;
+      if (c < WCH) rw[h] = *reinterpret_cast<const u32x4 *>(W + ((int64_t)(n0 + row) * 27 + t) * Cin + c0 + ch * 8);
     }
   };
   auto stagew = [&](int buf) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = tid + THREADS * h, row = c >> 3, ch = c & 7;
-      *reinterpret_cast<u32x4 *>(wt + buf * WTILE + row * 128 + swz8(row, ch) * 16) = rw[h];
+    for (int h = 0; h < HW; ++h) {
+      const int c = tid + THREADS * h, row = c / CCH, ch = c % CCH;
+      if (c < WCH) *reinterpret_cast<u32x4 *>(wt + buf * WTILE + row * 128 + swz8(row, ch) * 16) = rw[h];
     }
   };
-  f32x4 acc[4][2];
+  f32x4 acc[4][TJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int cs = 0; cs < cps; ++cs) {
-    const int c0 = cs * 64;
+    const int c0 = cs * CS;
     __syncthreads();   // the previous slice's halo and W reads are done
-    for (int c = tid; c < HROWS * 8; c += THREADS) {
-      const int hr = c >> 3, ch = c & 7;
+    for (int c = tid; c < HROWS * CCH; c += THREADS) {
+      const int hr = c / CCH, ch = c % CCH;
       const int hx = hr % GX, hy = (hr / GX) % GY, hz = hr / (GX * GY);
       const int iz = hz0 + hz, iy = hy0 + hy, ix = hx0 + hx;
       u32x4 v = mk_u32x4(0, 0, 0, 0);
@@ -335,22 +344,22 @@ __global__ __launch_bounds__(THREADS) void stencil3_kernel(pcs_conv3d_geom g, co
       const int dz = t / 9, dy = (t / 3) % 3, dx = t % 3;
       const int hoff = tr ? ((2 - dz) * GY + (2 - dy)) * GX + (2 - dx) : (dz * GY + dy) * GX + dx;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[4], bw[2];
+      for (int kk = 0; kk < KK; ++kk) {
+        bf16x8 af[4], bw[TJ];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int h = hrow[i] + hoff;
           af[i] = *reinterpret_cast<const bf16x8 *>(halo + h * 128 + swz8(h, kk * 4 + lg) * 16);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int r = wc * 32 + j * 16 + lr;
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wc * (NT / 2) + j * 16 + lr;
           bw[j] = *reinterpret_cast<const bf16x8 *>(wt + buf * WTILE + r * 128 + swz8(r, kk * 4 + lg) * 16);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
       }
       if (t + 1 < 27) stagew(buf ^ 1);   // buf ^ 1 was last read before the previous barrier
       __syncthreads();
@@ -363,8 +372,8 @@ __global__ __launch_bounds__(THREADS) void stencil3_kernel(pcs_conv3d_geom g, co
     if (oz >= g.Do || oy >= g.Ho || ox >= g.Wo) continue;
     const int64_t uo = (((int64_t)b * g.Do + oz) * g.Ho + oy) * g.Wo + ox;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int co = n0 + wc * 32 + j * 16 + 4 * lg;
+    for (int j = 0; j < TJ; ++j) {
+      const int co = n0 + wc * (NT / 2) + j * 16 + 4 * lg;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (bias) {
         const float4 bb = *reinterpret_cast<const float4 *>(bias + co);
@@ -410,14 +419,17 @@ PCS_DEV bf16x8 wfrag(const char *img, int cb, int lane) {
 // in class mode, where the dx taps meet different voxel sets)
 constexpr int TG = 3;
 
+// COT x CIT = the workgroup's (co, ci) tile, 64 or 32 each (a 32-channel level stages half rows)
+template <int COT, int CIT>
 __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                                const bf16_t *__restrict__ dY, float *__restrict__ ws,
                                                                int64_t M, int64_t vps) {
   __shared__ __attribute__((aligned(16))) char lds[2][(1 + TG) * WIMG];   // per buffer: dY | X per dx tap
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
-  const int nco = g.Cout / 64;
-  const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
+  constexpr int NI = COT / 32, NJ = CIT / 32;   // 16-channel MFMA tiles per wave (co, ci)
+  const int nco = g.Cout / COT;
+  const int co0 = (blockIdx.x % nco) * COT, ci0 = (blockIdx.x / nco) * CIT;
   const int split = blockIdx.z;
   const int k = g.k, taps = k * k * k;
   // transposed, stride 2: tap t only meets the output voxels of parity class (t + p) mod 2, so
@@ -440,13 +452,13 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
   const int64_t lo = (int64_t)split * vs, hi = pcs_min64(lo + vs, Mv);
   const int sv = tid >> 3, q8 = tid & 7;   // staging: voxel row sv, 16-B chunk q8 (channels 8 q8 ..)
 
-  f32x4 acc[TG][2][2];
+  f32x4 acc[TG][NI][NJ];
 #pragma unroll
   for (int a = 0; a < TG; ++a)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // the next k-step's rows are loaded into registers while this one's MFMAs run
   u32x4 rd, rx[TG];
   auto load = [&](int64_t v0) {
@@ -463,12 +475,12 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
       } else {
         decode(g, u, b, z, y, x);
       }
-      rd = *reinterpret_cast<const u32x4 *>(dY + uo * g.Cout + co0 + q8 * 8);
+      if (q8 < COT / 8) rd = *reinterpret_cast<const u32x4 *>(dY + uo * g.Cout + co0 + q8 * 8);
 #pragma unroll
       for (int a = 0; a < TG; ++a) {
         if (a < ntg) {
           const int64_t iv = in_voxel(g, b, z, y, x, dz, dy, dx0 + a);
-          if (iv >= 0) rx[a] = *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + ci0 + q8 * 8);
+          if (iv >= 0 && q8 < CIT / 8) rx[a] = *reinterpret_cast<const u32x4 *>(X + iv * g.Cin + ci0 + q8 * 8);
         }
       }
     }
@@ -488,20 +500,20 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
   for (int ks = 0; ks < nks; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nks) load(lo + (int64_t)(ks + 1) * WV);
-    bf16x8 fd[2];
+    bf16x8 fd[NI];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) fd[i] = wfrag(lds[buf], wr * 32 + i * 16, lane);
+    for (int i = 0; i < NI; ++i) fd[i] = wfrag(lds[buf], wr * (COT / 2) + i * 16, lane);
 #pragma unroll
     for (int a = 0; a < TG; ++a) {
       if (a < ntg) {   // uniform
-        bf16x8 fx[2];
+        bf16x8 fx[NJ];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fx[j] = wfrag(lds[buf] + (1 + a) * WIMG, wc * 32 + j * 16, lane);
+        for (int j = 0; j < NJ; ++j) fx[j] = wfrag(lds[buf] + (1 + a) * WIMG, wc * (CIT / 2) + j * 16, lane);
         // lane: dW rows co = 4 lg + v of tile i, column ci = lr of tile j
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[a][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[a][i][j], 0, 0, 0);
       }
     }
@@ -514,13 +526,13 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
     if (a >= ntg) continue;
     const int t = (dz * k + dy) * k + dx0 + a;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ci = ci0 + wc * 32 + j * 16 + lr;
+      for (int j = 0; j < NJ; ++j) {
+        const int ci = ci0 + wc * (CIT / 2) + j * 16 + lr;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+          const int co = co0 + wr * (COT / 2) + i * 16 + 4 * lg + v;
           out[((int64_t)co * taps + t) * g.Cin + ci] = acc[a][i][j][v];
         }
       }
@@ -534,6 +546,7 @@ __global__ __launch_bounds__(THREADS) void conv3d_wgrad_kernel(pcs_conv3d_geom g
 // rows read transposed (k over the block's voxels)
 constexpr int XPL = SZ * GY * GX;   // 240 halo rows of one dz
 
+template <int COT, int CIT>   // the (co, ci) tile: 64 or 32 each
 __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom g, const bf16_t *__restrict__ X,
                                                                  const bf16_t *__restrict__ dY, float *__restrict__ ws,
                                                                  int64_t nblk, int64_t bps) {
@@ -541,8 +554,9 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
   char *dimg = lds, *ximg = lds + 128 * 128;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
-  const int nco = g.Cout / 64;
-  const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
+  constexpr int NI = COT / 32, NJ = CIT / 32;   // 16-channel MFMA tiles per wave (co, ci)
+  const int nco = g.Cout / COT;
+  const int co0 = (blockIdx.x % nco) * COT, ci0 = (blockIdx.x / nco) * CIT;
   const int dz = blockIdx.y, split = blockIdx.z;
   const bool tr = g.transposed;
   const int zoff = tr ? 2 - dz : dz;
@@ -564,13 +578,13 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
     const s16x8 v = {part[0][0], part[0][1], part[0][2], part[0][3], part[1][0], part[1][1], part[1][2], part[1][3]};
     return __builtin_bit_cast(bf16x8, v);
   };
-  f32x4 acc[9][2][2];
+  f32x4 acc[9][NI][NJ];
 #pragma unroll
   for (int a = 0; a < 9; ++a)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[a][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int64_t blk = b0; blk < b1; ++blk) {
     uint32_t q = (uint32_t)blk;
     const int bx = (int)(q % nbx); q /= nbx;
@@ -581,16 +595,16 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
     const int hz0 = (tr ? oz0 + g.p - 2 : oz0 - g.p) + zoff, hy0 = tr ? oy0 + g.p - 2 : oy0 - g.p,
               hx0 = tr ? ox0 + g.p - 2 : ox0 - g.p;
     __syncthreads();   // the previous block's reads are done
-    for (int c = tid; c < 128 * 8; c += THREADS) {   // dY rows of the block (zero outside the grid)
-      const int r = c >> 3, ch = c & 7;
+    for (int c = tid; c < 128 * (COT / 8); c += THREADS) {   // dY rows of the block (zero outside the grid)
+      const int r = c / (COT / 8), ch = c % (COT / 8);
       const int oz = oz0 + (r >> 5), oy = oy0 + ((r >> 3) & 3), ox = ox0 + (r & 7);
       u32x4 v = mk_u32x4(0, 0, 0, 0);
       if (oz < g.Do && oy < g.Ho && ox < g.Wo)
         v = *reinterpret_cast<const u32x4 *>(dY + ((((int64_t)b * g.Do + oz) * g.Ho + oy) * g.Wo + ox) * g.Cout + co0 + ch * 8);
       *reinterpret_cast<u32x4 *>(dimg + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4)) = v;
     }
-    for (int c = tid; c < XPL * 8; c += THREADS) {   // the 4 halo planes of this dz
-      const int hr = c >> 3, ch = c & 7;
+    for (int c = tid; c < XPL * (CIT / 8); c += THREADS) {   // the 4 halo planes of this dz
+      const int hr = c / (CIT / 8), ch = c % (CIT / 8);
       const int hx = hr % GX, hy = (hr / GX) % GY, hz = hr / (GX * GY);
       const int iz = hz0 + hz, iy = hy0 + hy, ix = hx0 + hx;
       u32x4 v = mk_u32x4(0, 0, 0, 0);
@@ -601,20 +615,20 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
     __syncthreads();
 #pragma unroll 1
     for (int kb = 0; kb < 128; kb += 32) {   // 32 block voxels per MFMA k-step
-      bf16x8 fd[2];
+      bf16x8 fd[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fd[i] = trfrag(dimg, wr * 32 + i * 16, kb, 0, 0, false);
+      for (int i = 0; i < NI; ++i) fd[i] = trfrag(dimg, wr * (COT / 2) + i * 16, kb, 0, 0, false);
 #pragma unroll
       for (int a = 0; a < 9; ++a) {
         const int ty = a / 3, tx = a % 3;
         const int dyo = tr ? 2 - ty : ty, dxo = tr ? 2 - tx : tx;
-        bf16x8 fx[2];
+        bf16x8 fx[NJ];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fx[j] = trfrag(ximg, wc * 32 + j * 16, kb, dyo, dxo, true);
+        for (int j = 0; j < NJ; ++j) fx[j] = trfrag(ximg, wc * (CIT / 2) + j * 16, kb, dyo, dxo, true);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[a][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[a][i][j], 0, 0, 0);
       }
     }
@@ -624,13 +638,13 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
   for (int a = 0; a < 9; ++a) {
     const int t = dz * 9 + a;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ci = ci0 + wc * 32 + j * 16 + lr;
+      for (int j = 0; j < NJ; ++j) {
+        const int ci = ci0 + wc * (CIT / 2) + j * 16 + lr;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+          const int co = co0 + wr * (COT / 2) + i * 16 + 4 * lg + v;
           out[((int64_t)co * 27 + t) * g.Cin + ci] = acc[a][i][j][v];
         }
       }
@@ -639,6 +653,7 @@ __global__ __launch_bounds__(THREADS) void stencil3_wgrad_kernel(pcs_conv3d_geom
 
 // db partials: column sums of dY over one voxel slice, [split][Cout]; a thread sums 8 channels
 // (one 16-B chunk) of every 32nd row, then the 32 row groups are added in LDS in a fixed order
+// (64 channels per workgroup; the last one of a 32-channel multiple runs half)
 __global__ __launch_bounds__(THREADS) void conv3d_bgrad_kernel(const bf16_t *__restrict__ dY, int Cout, int64_t M,
                                                                int64_t vps, float *__restrict__ wsb) {
   __shared__ float red[32][64];
@@ -646,7 +661,8 @@ __global__ __launch_bounds__(THREADS) void conv3d_bgrad_kernel(const bf16_t *__r
   const int c0 = blockIdx.x * 64;
   const int64_t lo = (int64_t)blockIdx.y * vps, hi = pcs_min64(lo + vps, M);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t u = lo + rg; u < hi; u += 32) {
+  const bool cv = c0 + ch * 8 < Cout;
+  for (int64_t u = cv ? lo + rg : hi; u < hi; u += 32) {
     float v[8];
     unpack_chunk(*reinterpret_cast<const u32x4 *>(dY + u * Cout + c0 + ch * 8), v);
 #pragma unroll
@@ -655,7 +671,7 @@ __global__ __launch_bounds__(THREADS) void conv3d_bgrad_kernel(const bf16_t *__r
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[rg][ch * 8 + e] = s[e];
   __syncthreads();
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64 && c0 + (int)threadIdx.x < Cout) {
     float t = 0.f;
     for (int r = 0; r < 32; ++r) t += red[r][threadIdx.x];
     wsb[(int64_t)blockIdx.y * Cout + c0 + threadIdx.x] = t;
@@ -953,6 +969,8 @@ bool geom_ok(const pcs_conv3d_geom *g, const char **why) {
 int64_t out_voxels(const pcs_conv3d_geom &g) { return g.B * g.Do * g.Ho * g.Wo; }
 
 bool stencil3(const pcs_conv3d_geom &g) { return g.k == 3 && g.s == 1; }
+// channel tile of a layer: 64, or 32 where the count is an odd multiple of 32 (a 32-channel level)
+int ctile(int c) { return c % 64 == 0 ? 64 : 32; }
 
 int64_t stencil_blocks(const pcs_conv3d_geom &g) {
   return g.B * ((g.Do + SZ - 1) / SZ) * ((g.Ho + SY - 1) / SY) * ((g.Wo + SX - 1) / SX);
@@ -961,11 +979,12 @@ int64_t stencil_blocks(const pcs_conv3d_geom &g) {
 int64_t wgrad_splits(const pcs_conv3d_geom &g) {
   const int64_t M = out_voxels(g);
   if (stencil3(g)) {   // halo-tile kernel: 3 dz workgroups per (co, ci) tile and block range
-    const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * 3;
+    const int64_t tiles = (int64_t)(g.Cout / ctile(g.Cout)) * (g.Cin / ctile(g.Cin)) * 3;
     const int64_t sp = (1024 + tiles - 1) / tiles, nb = stencil_blocks(g);
     return sp > nb ? nb : sp;
   }
-  const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64) * (g.transposed && g.s == 2 ? g.k * g.k * g.k : g.k * g.k);
+  const int64_t tiles = (int64_t)(g.Cout / ctile(g.Cout)) * (g.Cin / ctile(g.Cin)) *
+                        (g.transposed && g.s == 2 ? g.k * g.k * g.k : g.k * g.k);
   int64_t sp = (2048 + tiles - 1) / tiles;
   const int64_t maxsp = (M + 4 * WV - 1) / (4 * WV);   // at least 4 k-steps per slice
   if (sp > maxsp) sp = maxsp;
@@ -984,35 +1003,44 @@ extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W
   const char *why = nullptr;
   if (!geom_ok(g, &why)) return pcs_set_einval("pcs_conv3d", why);
   if (!X || !W || !Y) return pcs_set_einval("pcs_conv3d", "X, W and Y are required");
-  if (g->Cin % KS != 0 || g->Cout % BN != 0 || g->Cin <= 0 || g->Cout <= 0)
-    return pcs_set_einval("pcs_conv3d", "Cin must be a multiple of 32 and Cout of 64");
+  if (g->Cin % 32 != 0 || g->Cout % 32 != 0 || g->Cin <= 0 || g->Cout <= 0)
+    return pcs_set_einval("pcs_conv3d", "Cin and Cout must be multiples of 32");
   if (ydtype != PCS_F32 && ydtype != PCS_BF16) return pcs_set_einval("pcs_conv3d", "Y dtype: PCS_F32 or PCS_BF16");
   const int64_t M = out_voxels(*g);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (g->k == 3 && g->s == 1 && g->Cin % 64 == 0) {   // halo-staged stencil (both forms)
-    const int64_t nblk = g->B * ((g->Do + SZ - 1) / SZ) * ((g->Ho + SY - 1) / SY) * ((g->Wo + SX - 1) / SX);
+  const int cs = ctile(g->Cin), nt = ctile(g->Cout);
+  if (stencil3(*g)) {   // halo-staged stencil (both forms)
+    const int64_t nblk = stencil_blocks(*g);
     if (nblk > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
-    const dim3 sg((unsigned)nblk, (unsigned)(g->Cout / BN));
+    const dim3 sg((unsigned)nblk, (unsigned)(g->Cout / nt));
     const bf16_t *Xs = static_cast<const bf16_t *>(X), *Ws = static_cast<const bf16_t *>(W);
-    if (ydtype == PCS_BF16) hipLaunchKernelGGL(stencil3_kernel<true>, sg, dim3(THREADS), 0, s, *g, Xs, Ws, bias, Y);
-    else hipLaunchKernelGGL(stencil3_kernel<false>, sg, dim3(THREADS), 0, s, *g, Xs, Ws, bias, Y);
+#define PCS_S3(CS, NT)                                                                                          \
+  do {                                                                                                          \
+    if (ydtype == PCS_BF16) hipLaunchKernelGGL((stencil3_kernel<CS, NT, true>), sg, dim3(THREADS), 0, s, *g, Xs, Ws, bias, Y); \
+    else hipLaunchKernelGGL((stencil3_kernel<CS, NT, false>), sg, dim3(THREADS), 0, s, *g, Xs, Ws, bias, Y);   \
+  } while (0)
+    if (cs == 64) { if (nt == 64) PCS_S3(64, 64); else PCS_S3(64, 32); }
+    else { if (nt == 64) PCS_S3(32, 64); else PCS_S3(32, 32); }
+#undef PCS_S3
     PCS_CHECK_LAUNCH();
     return 0;
   }
   // transposed stride 2: 8 parity classes, tiles of the largest class's sub-grid each.  128-voxel
   // tiles (8 MFMAs per wave per barrier) once there are enough of them to fill the chip
   const int64_t rows_cls = g->transposed && g->s == 2 ? g->B * ((g->Do + 1) / 2) * ((g->Ho + 1) / 2) * ((g->Wo + 1) / 2) : M;
-  const int64_t ncb = g->Cout / BN;
+  const int64_t ncb = g->Cout / nt;
   const int bmt = (rows_cls / 128) * ncb * (g->transposed && g->s == 2 ? 8 : 1) >= 2048 ? 128 : 64;
   const int64_t tiles = (rows_cls + bmt - 1) / bmt * (g->transposed && g->s == 2 ? 8 : 1);
   if (tiles <= 0 || tiles > 0x7fffffff) return pcs_set_einval("pcs_conv3d", "grid too large");
   const dim3 grid((unsigned)tiles, (unsigned)ncb);
   const bf16_t *Xb = static_cast<const bf16_t *>(X), *Wb = static_cast<const bf16_t *>(W);
-  const bool k64 = g->Cin % 64 == 0;
-#define PCS_C3(BMT, KST, OB) hipLaunchKernelGGL((conv3d_kernel<BMT, KST, OB>), grid, dim3(THREADS), 0, s, *g, Xb, Wb, bias, Y, M)
-#define PCS_C3K(BMT, OB) \
-  do {                   \
-    if (k64) PCS_C3(BMT, 64, OB); else PCS_C3(BMT, 32, OB); \
+  const bool k64 = cs == 64;
+#define PCS_C3(BMT, KST, OB, NT) \
+  hipLaunchKernelGGL((conv3d_kernel<BMT, KST, OB, NT>), grid, dim3(THREADS), 0, s, *g, Xb, Wb, bias, Y, M)
+#define PCS_C3K(BMT, OB)                                          \
+  do {                                                            \
+    if (nt == 64) { if (k64) PCS_C3(BMT, 64, OB, 64); else PCS_C3(BMT, 32, OB, 64); } \
+    else { if (k64) PCS_C3(BMT, 64, OB, 32); else PCS_C3(BMT, 32, OB, 32); }          \
   } while (0)
   if (bmt == 128) {
     if (ydtype == PCS_BF16) PCS_C3K(128, true); else PCS_C3K(128, false);
@@ -1028,8 +1056,8 @@ extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W
 extern "C" int64_t pcs_conv3d_wgrad_workspace(const pcs_conv3d_geom *g) {
   const char *why = nullptr;
   if (!geom_ok(g, &why)) return pcs_set_einval("pcs_conv3d_wgrad_workspace", why);
-  if (g->Cin % 64 != 0 || g->Cout % 64 != 0 || g->Cin <= 0 || g->Cout <= 0)
-    return pcs_set_einval("pcs_conv3d_wgrad_workspace", "Cin and Cout must be multiples of 64");
+  if (g->Cin % 32 != 0 || g->Cout % 32 != 0 || g->Cin <= 0 || g->Cout <= 0)
+    return pcs_set_einval("pcs_conv3d_wgrad_workspace", "Cin and Cout must be multiples of 32");
   const int64_t sp = wgrad_splits(*g);
   return sp * ((int64_t)g->Cout * g->k * g->k * g->k * g->Cin + g->Cout) * 4;
 }
@@ -1045,20 +1073,29 @@ extern "C" int pcs_conv3d_wgrad(const pcs_conv3d_geom *g, const void *X, const v
   const int64_t wlen = (int64_t)g->Cout * taps * g->Cin;
   float *ws = static_cast<float *>(workspace), *wsb = ws + sp * wlen;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int cot = ctile(g->Cout), cit = ctile(g->Cin);
+  const unsigned ntile = (unsigned)((g->Cout / cot) * (g->Cin / cit));
+  const bf16_t *Xb = static_cast<const bf16_t *>(X), *dYb = static_cast<const bf16_t *>(dY);
   if (stencil3(*g)) {
     const int64_t nb = stencil_blocks(*g), bps = (nb + sp - 1) / sp;
-    hipLaunchKernelGGL(stencil3_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), 3u, (unsigned)sp),
-                       dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, nb, bps);
+    const dim3 grid(ntile, 3u, (unsigned)sp);
+#define PCS_SW(CO, CI) hipLaunchKernelGGL((stencil3_wgrad_kernel<CO, CI>), grid, dim3(THREADS), 0, s, *g, Xb, dYb, ws, nb, bps)
+    if (cot == 64) { if (cit == 64) PCS_SW(64, 64); else PCS_SW(64, 32); }
+    else { if (cit == 64) PCS_SW(32, 64); else PCS_SW(32, 32); }
+#undef PCS_SW
   } else {
     const int groups = g->transposed && g->s == 2 ? taps : g->k * g->k;   // workgroups per (co, ci) tile and slice
-    hipLaunchKernelGGL(conv3d_wgrad_kernel, dim3((unsigned)((g->Cout / 64) * (g->Cin / 64)), (unsigned)groups, (unsigned)sp),
-                       dim3(THREADS), 0, s, *g, static_cast<const bf16_t *>(X), static_cast<const bf16_t *>(dY), ws, M, vps);
+    const dim3 grid(ntile, (unsigned)groups, (unsigned)sp);
+#define PCS_GW(CO, CI) hipLaunchKernelGGL((conv3d_wgrad_kernel<CO, CI>), grid, dim3(THREADS), 0, s, *g, Xb, dYb, ws, M, vps)
+    if (cot == 64) { if (cit == 64) PCS_GW(64, 64); else PCS_GW(64, 32); }
+    else { if (cit == 64) PCS_GW(32, 64); else PCS_GW(32, 32); }
+#undef PCS_GW
   }
   PCS_CHECK_LAUNCH();
   hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((wlen + 255) / 256)), dim3(256), 0, s, ws, sp, wlen, dW);
   PCS_CHECK_LAUNCH();
   if (db) {
-    hipLaunchKernelGGL(conv3d_bgrad_kernel, dim3((unsigned)(g->Cout / 64), (unsigned)sp), dim3(THREADS), 0, s,
+    hipLaunchKernelGGL(conv3d_bgrad_kernel, dim3((unsigned)((g->Cout + 63) / 64), (unsigned)sp), dim3(THREADS), 0, s,
                        static_cast<const bf16_t *>(dY), g->Cout, M, vps, wsb);
     PCS_CHECK_LAUNCH();
     hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((g->Cout + 255) / 256)), dim3(256), 0, s, wsb, sp,

@@ -135,7 +135,8 @@ def _bf16_2d(t, rows, cols):
     return out
 
 
-CH_ALIGN = 64   # channel multiple of the conv3d kernels' 64-wide tiles (forward, input and weight gradients)
+CH_ALIGN = 64   # channel multiple of the sparse conv kernels' 64-wide tiles (sparse.py)
+DENSE_CH_ALIGN = 32   # the dense conv3d kernels' tiles: 64 channels, or 32 for a 32-channel level
 
 
 def _ceil(c, m=CH_ALIGN):
@@ -154,10 +155,11 @@ def _pad_channels(t, c_to):
 class _Conv3dFn(torch.autograd.Function):
     """y = conv(x, w) + b with w in kernel layout [Cout, taps * Cin] (fp32 master).
 
-    Channel counts that are not multiples of 64 (a first layer on raw point features, a 32-channel
-    U-Net level) run on zero-padded channels: x and W^T get zero input channels, W and b zero
-    output channels, and the padded output / gradient channels are sliced off.  Zero channels
-    contribute exact zeros, so results equal the unpadded convolution's."""
+    Multiples of 32 run natively (a 32-channel U-Net level on 32-channel tiles); other channel
+    counts (a first layer on raw point features) run on zero-padded channels: x and W^T get zero
+    input channels, W and b zero output channels, and the padded output / gradient channels are
+    sliced off.  Zero channels contribute exact zeros, so results equal the unpadded
+    convolution's."""
 
     @staticmethod
     def forward(ctx, x, wk, bias, k, s, p, transposed, out_dtype, op):
@@ -169,7 +171,7 @@ class _Conv3dFn(torch.autograd.Function):
         cout, taps = wk.shape[0], k ** 3
         if wk.shape[1] != taps * cin:
             raise ValueError(f"weight has {wk.shape[1] // taps} input channels, x has {cin}")
-        cin_k, cout_k = _ceil(cin), _ceil(cout)
+        cin_k, cout_k = _ceil(cin, DENSE_CH_ALIGN), _ceil(cout, DENSE_CH_ALIGN)
         g = _geom(B, (D, H, W), cin_k, cout_k, k, s, p, transposed, op)
         xk = _pad_channels(x, cin_k)
         if (cin_k, cout_k) != (cin, cout):

@@ -35,9 +35,15 @@ CASES = [
     (2, 2, 0, False, (7, 5, 7), 64, 128),     # 2x2x2 down on an odd grid (skipped last plane)
     (3, 2, 1, True, (3, 4, 2), 64, 64, 1),    # transposed with output_padding 1
     (2, 2, 0, True, (3, 2, 4), 64, 64, (1, 0, 1)),   # 2x2x2 up with per-dimension output_padding
-    (3, 1, 1, False, (4, 3, 5), 32, 64),      # the U-Net's 32-channel level (padded to 64)
-    (3, 1, 1, False, (5, 4, 3), 4, 32),       # raw point features in, 32 channels out (padded)
+    (3, 1, 1, False, (4, 3, 5), 32, 64),      # the U-Net's 32 -> 64 step (32-channel halo slices)
+    (3, 1, 1, False, (5, 4, 3), 4, 32),       # raw point features in (padded to 32), 32 channels out
     (2, 2, 0, True, (2, 3, 2), 64, 32),       # transposed up to a 32-channel level
+    (3, 1, 1, False, (5, 6, 7), 32, 32),      # the 32-channel level's own stencil (32 x 32 tiles)
+    (3, 1, 1, True, (4, 5, 3), 64, 32),       # transposed stencil, 64-channel slices into 32-channel tiles
+    (2, 2, 0, False, (6, 4, 7), 32, 64),      # 2x2x2 down from the 32-channel level (gather, 32-deep k-steps)
+    (3, 2, 1, False, (7, 5, 7), 32, 32),      # strided gather on 32-channel tiles both ways
+    (1, 1, 0, False, (3, 5, 4), 96, 32),      # 1x1x1 channel mix, three 32-channel slices in
+    (3, 1, 1, False, (3, 4, 5), 96, 96),      # odd multiples of 32 both ways (three tiles each)
 ]
 
 
@@ -102,7 +108,8 @@ def test_forward_large_tiles(k, s, p, transposed, grid, cin, cout):
 @pytest.mark.parametrize("k,s,p,transposed,grid,cin,cout,op", [_case(c) for c in CASES])
 def test_backward_matches_torch(k, s, p, transposed, grid, cin, cout, op):
     """Every case, including even grids under a stride (the input gradient's output_padding),
-    odd grids under the 2x2x2 down layer and channel counts off the 64 multiple (padded)."""
+    odd grids under the 2x2x2 down layer, odd multiples of 32 (32-channel tiles) and counts off
+    the 32 multiple (padded)."""
     import pcs_amd.voxel as V
     x, w, b = _operands(k, transposed, grid, cin, cout, seed=1)
     xr = _ncdhw(x).requires_grad_()

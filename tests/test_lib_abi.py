@@ -89,11 +89,12 @@ def test_conv3d_argument_validation_without_gpu():
 
     ok = geom()
     assert lib.pcs_conv3d_wgrad_workspace(ct.byref(ok)) > 0
-    for bad in (geom(Cin=48), geom(Cout=32), geom(Do=7), geom(k=4), geom(s=3), geom(p=3),
+    for bad in (geom(Cin=48), geom(Cout=40), geom(Do=7), geom(k=4), geom(s=3), geom(p=3),
                 geom(transposed=1, Do=9)):
         assert lib.pcs_conv3d(ct.byref(bad), 1, 1, None, 1, L.BF16, None) == -1000
     assert lib.pcs_conv3d(ct.byref(ok), 1, 1, None, 1, L.F32 + 7, None) == -1000
-    assert lib.pcs_conv3d_wgrad_workspace(ct.byref(geom(Cin=32))) == -1000
+    assert lib.pcs_conv3d_wgrad_workspace(ct.byref(geom(Cin=40))) == -1000
+    assert lib.pcs_conv3d_wgrad_workspace(ct.byref(geom(Cin=32, Cout=96))) > 0   # 32-channel tiles
     up = geom(Di=4, Hi=4, Wi=4, k=2, s=2, p=0, transposed=1)     # 4^3 -> 8^3
     assert lib.pcs_conv3d_wgrad_workspace(ct.byref(up)) > 0
 
