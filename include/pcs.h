@@ -701,6 +701,21 @@ int pcs_conv3d_weight_t(const void *W, int32_t Cout, int32_t taps, int32_t Cin, 
  *   taps one of its rows has a neighbour at.
  * pcs_sparse_conv_wgrad: dW [Cout][taps][Cin] f32 = sum_m dY[m] (x) X[nbr[m][t]], db [Cout] (may be
  *   NULL); Cin, Cout % 64 == 0; fixed-order partial sums (deterministic).
+ *
+ * Per-tap pair lists (the same convolutions as gather-GEMM-reduce, for low occupancy where most
+ * (row, tap) entries of nbr are -1): built once per neighbour map and shared by every layer.
+ * pcs_sparse_pairs_count: tap_counts [taps] i64 (device) = valid entries per tap; workspace of
+ *   pcs_sparse_pairs_workspace bytes, kept for the build.  The caller copies tap_counts to the host
+ *   and forms tap_off [taps + 1] (exclusive prefix, P = tap_off[taps] pairs).
+ * pcs_sparse_pairs_build: pair_in / pair_out [P] i32: tap t's pairs at [tap_off[t], tap_off[t + 1]),
+ *   out rows ascending, pair_in = nbr[pair_out][t]; pair_pos [M][taps] i32 = the pair index of
+ *   (m, t) or -1.
+ * pcs_sparse_conv_pairs: pcs_sparse_conv's Y (same flip rule) from Z [P][Cout] f32 (workspace):
+ *   Z[p] = W[tw(t)] X[pair_in[p]], then Y[m] = b + sum over t in order of Z[pair_pos[m][t]];
+ *   tap_off is a HOST array.  Cin % 32 == 0, Cout % 64 == 0.
+ * pcs_sparse_conv_wgrad_pairs: pcs_sparse_conv_wgrad's dW / db over the pairs only (dW_t = sum over
+ *   tap t's pairs of dY[pair_out] (x) X[pair_in]); tap_off a host array; Cin, Cout % 64 == 0;
+ *   fixed-order partial sums (deterministic).
  */
 int pcs_voxel_keys(const float *points, const int64_t *offsets, int64_t num_scenes, int64_t T, int32_t grid,
                    float lo_x, float lo_y, float lo_z, float hi_x, float hi_y, float hi_z,
@@ -718,6 +733,20 @@ int64_t pcs_sparse_conv_wgrad_workspace(int64_t M, int32_t taps, int32_t Cin, in
 int pcs_sparse_conv_wgrad(const int32_t *nbr, int64_t M, int32_t taps, const void *X, int32_t Cin, const void *dY,
                           int32_t Cout, void *workspace, int64_t workspace_bytes, float *dW, float *db,
                           pcs_stream_t stream);
+int64_t pcs_sparse_pairs_workspace(int64_t M, int32_t taps);   /* bytes */
+int pcs_sparse_pairs_count(const int32_t *nbr, int64_t M, int32_t taps, void *workspace, int64_t *tap_counts,
+                           pcs_stream_t stream);
+int pcs_sparse_pairs_build(const int32_t *nbr, int64_t M, int32_t taps, const void *workspace,
+                           const int64_t *tap_counts, int32_t *pair_in, int32_t *pair_out, int32_t *pair_pos,
+                           pcs_stream_t stream);
+int pcs_sparse_conv_pairs(const int32_t *pair_in, const int32_t *pair_pos, const int64_t *tap_off, int32_t taps,
+                          int64_t M, const void *X, int32_t Cin, const void *W, int32_t Cout, const float *bias,
+                          float *Z, void *Y, int32_t ydtype, int32_t flip, pcs_stream_t stream);
+int64_t pcs_sparse_conv_wgrad_pairs_workspace(const int64_t *tap_off, int32_t taps, int64_t M, int32_t Cin,
+                                              int32_t Cout);   /* bytes */
+int pcs_sparse_conv_wgrad_pairs(const int32_t *pair_in, const int32_t *pair_out, const int64_t *tap_off,
+                                int32_t taps, int64_t M, const void *X, int32_t Cin, const void *dY, int32_t Cout,
+                                void *workspace, int64_t workspace_bytes, float *dW, float *db, pcs_stream_t stream);
 
 /* Build-time identification and error string. */
 int pcs_abi_version(void);

@@ -144,6 +144,14 @@ SIGNATURES = [
     ("pcs_sparse_conv", ct.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _i32, _vp]),
     ("pcs_sparse_conv_wgrad_workspace", _i64, [_i64, _i32, _i32, _i32]),
     ("pcs_sparse_conv_wgrad", ct.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _i64, _vp, _vp, _vp]),
+    ("pcs_sparse_pairs_workspace", _i64, [_i64, _i32]),
+    ("pcs_sparse_pairs_count", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    ("pcs_sparse_pairs_build", ct.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("pcs_sparse_conv_pairs", ct.c_int, [_vp, _vp, _vp, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _i32,
+                                         _vp]),
+    ("pcs_sparse_conv_wgrad_pairs_workspace", _i64, [_vp, _i32, _i64, _i32, _i32]),
+    ("pcs_sparse_conv_wgrad_pairs", ct.c_int, [_vp, _vp, _vp, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp, _vp,
+                                               _vp]),
     ("pcs_voxel_keys", ct.c_int, [_vp, _vp, _i64, _i64, _i32, _f, _f, _f, _f, _f, _f, _vp, _vp, _vp]),
     ("pcs_voxel_hash_capacity", _i64, [_i64]),
     ("pcs_voxel_hash_build", ct.c_int, [_vp, _i64, _vp, _vp, _i64, _vp]),

@@ -996,6 +996,332 @@ int64_t wgrad_vps(const pcs_conv3d_geom &g, int64_t sp) {
   return ((M + sp - 1) / sp + WV - 1) / WV * WV;
 }
 
+// ---- per-tap pair lists of a neighbour map: the sparse convolution as gather-GEMM-reduce.  The
+// gather kernel above multiplies a zero row for every row of a tile that lacks a tap the tile
+// meets; at low occupancy (1.5 occupied taps per voxel) that is most of its work.  Here each tap's
+// (out row, in row) pairs are listed once per neighbour map (rows ascending within a tap, so the
+// lists and every sum below are deterministic), the product of tap t is a GEMM over its own pairs
+// only, and each output row sums its pairs' products in tap order.
+constexpr int PT_MAX = 27;   // taps of the centred 3x3x3 map
+struct PairTaps {            // host-built, passed by value: tap t's pairs [tap_off[t], tap_off[t + 1]),
+  int64_t tap_off[PT_MAX + 1];   // its GEMM tiles [tile_off[t], tile_off[t + 1]), its weight-gradient
+  int32_t tile_off[PT_MAX + 1];  // slices [slice_off[t], slice_off[t + 1]) of slice_len pairs each
+  int32_t slice_off[PT_MAX + 1];
+  int64_t slice_len;
+  int32_t taps;
+};
+
+// a block's 256 rows of the neighbour map through LDS: coalesced loads (and, for pair_pos,
+// coalesced stores) instead of 27 strided accesses per thread; [row][tap] words, stride 27 (odd:
+// the per-tap reads are conflict-free)
+PCS_DEV int pairs_rows(const int32_t *__restrict__ nbr, int64_t M, int taps, int32_t *rb) {
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int nr = (int)pcs_min64(256, M - r0), n = nr * taps;
+  for (int i = threadIdx.x; i < n; i += 256) rb[i] = nbr[r0 * taps + i];
+  __syncthreads();
+  return nr;
+}
+
+// per-block pair counts of every tap: cnt[block][t] (one thread per row)
+__global__ __launch_bounds__(256) void pairs_count_kernel(const int32_t *__restrict__ nbr, int64_t M, int taps,
+                                                          int32_t *__restrict__ cnt) {
+  __shared__ int32_t wc[4][PT_MAX];
+  __shared__ int32_t rb[256 * PT_MAX];
+  const int tid = threadIdx.x, w = tid >> 6;
+  const int nr = pairs_rows(nbr, M, taps, rb);
+  for (int t = 0; t < taps; ++t) {
+    const bool has = tid < nr && rb[tid * taps + t] >= 0;
+    const uint64_t b = __ballot(has);
+    if ((tid & 63) == 0) wc[w][t] = __popcll(b);
+  }
+  __syncthreads();
+  if (tid < taps) cnt[(int64_t)blockIdx.x * taps + tid] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
+}
+
+// exclusive prefix of the block counts per tap (one workgroup per tap) and the tap totals
+__global__ __launch_bounds__(256) void pairs_scan_kernel(int32_t *__restrict__ cnt, int64_t nblk, int taps,
+                                                         int64_t *__restrict__ tap_counts) {
+  __shared__ int32_t ws[4];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < nblk; b0 += 256) {
+    const int64_t b = b0 + tid;
+    const int32_t v = b < nblk ? cnt[b * taps + t] : 0;
+    int32_t x = v;   // inclusive scan of the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    int32_t before = 0;
+    for (int i = 0; i < w; ++i) before += ws[i];
+    if (b < nblk) cnt[b * taps + t] = (int32_t)(carry + before + x - v);
+    const int32_t tot = ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+    carry += tot;
+  }
+  if (tid == 0) tap_counts[t] = carry;
+}
+
+// pair_in / pair_out at tap_off[t] + (block prefix) + (rank in the block), pair_pos[m][t]:
+// two ballot passes (the block's per-wave counts first, then each lane's rank)
+__global__ __launch_bounds__(256) void pairs_build_kernel(const int32_t *__restrict__ nbr, int64_t M, int taps,
+                                                          const int32_t *__restrict__ pre,
+                                                          const int64_t *__restrict__ tap_counts,
+                                                          int32_t *__restrict__ pin, int32_t *__restrict__ pout,
+                                                          int32_t *__restrict__ ppos) {
+  __shared__ int32_t wc[4][PT_MAX];
+  __shared__ int64_t toff[PT_MAX];
+  __shared__ int32_t rb[256 * PT_MAX];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t m = (int64_t)blockIdx.x * 256 + tid;
+  if (tid == 0) {
+    int64_t s = 0;
+    for (int t = 0; t < taps; ++t) { toff[t] = s; s += tap_counts[t]; }
+  }
+  const int nr = pairs_rows(nbr, M, taps, rb);
+  for (int t = 0; t < taps; ++t) {
+    const uint64_t b = __ballot(tid < nr && rb[tid * taps + t] >= 0);
+    if (lane == 0) wc[w][t] = __popcll(b);
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int t = 0; t < taps; ++t) {
+    const int32_t n = tid < nr ? rb[tid * taps + t] : -1;
+    const uint64_t b = __ballot(n >= 0);
+    int32_t q = -1;
+    if (n >= 0) {
+      int64_t pos = toff[t] + pre[(int64_t)blockIdx.x * taps + t] + __popcll(b & lt);
+      for (int i = 0; i < w; ++i) pos += wc[i][t];
+      q = (int32_t)pos;
+      pin[pos] = n;
+      pout[pos] = (int32_t)m;
+    }
+    if (tid < nr) rb[tid * taps + t] = q;   // (only this thread reads or writes its row)
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  for (int i = tid; i < nr * taps; i += 256) ppos[r0 * taps + i] = rb[i];
+}
+
+// Z[p][n0 ..] = W[tw(t)] X[pair_in[p]] for the 64 pairs of one tile of tap t (fp32 products).
+// (Reducing in the centre tap's GEMM epilogue instead of a separate pass, the centre's products
+// never stored, was slower: 26 dependent gathers per lane there against 8 threads per row here.)
+template <int KST>
+__global__ __launch_bounds__(THREADS) void pair_gemm_kernel(PairTaps pt, const int32_t *__restrict__ pin,
+                                                            const bf16_t *__restrict__ X, int Cin,
+                                                            const bf16_t *__restrict__ W, int Cout, int flip,
+                                                            float *__restrict__ Z) {
+  constexpr int BMT = 64, RB = KST * 2, CPR = KST / 8, RPP = THREADS / CPR;
+  constexpr int HA = BMT / RPP, HB = BN / RPP, KK = KST / 32;
+  __shared__ __attribute__((aligned(16))) char lds[2][(BMT + BN) * RB];
+  auto swzf = [](int row, int slot) { return KST == 32 ? cswz(row, slot) : (slot ^ ((row >> 1) & 7)); };
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int taps = pt.taps, tile = blockIdx.x;
+  int t = 0;
+  while (t + 1 < taps && pt.tile_off[t + 1] <= tile) ++t;
+  const int tw = flip ? taps - 1 - t : t;
+  const int64_t p0 = pt.tap_off[t] + (int64_t)(tile - pt.tile_off[t]) * BMT, pend = pt.tap_off[t + 1];
+  const int n0 = blockIdx.y * BN;
+  const int srow = tid / CPR, q = tid % CPR;
+  int iv[HA];
+#pragma unroll
+  for (int h = 0; h < HA; ++h) {
+    const int64_t p = p0 + srow + RPP * h;
+    iv[h] = p < pend ? pin[p] : -1;
+  }
+  const bf16_t *wrow = W + ((int64_t)(n0 + srow) * taps + tw) * Cin + q * 8;
+  const int64_t wstep = (int64_t)RPP * taps * Cin;
+  const int nks = Cin / KST;
+  u32x4 ra[HA], rb[HB];
+  auto load = [&](int ks) {
+    const int c0 = ks * KST;
+#pragma unroll
+    for (int h = 0; h < HA; ++h)
+      ra[h] = iv[h] >= 0 ? *reinterpret_cast<const u32x4 *>(X + (int64_t)iv[h] * Cin + c0 + q * 8) : mk_u32x4(0, 0, 0, 0);
+#pragma unroll
+    for (int h = 0; h < HB; ++h) rb[h] = *reinterpret_cast<const u32x4 *>(wrow + h * wstep + c0);
+  };
+  auto stage = [&](int buf) {
+    char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
+#pragma unroll
+    for (int h = 0; h < HA; ++h) {
+      const int r = srow + RPP * h;
+      *reinterpret_cast<u32x4 *>(tA + r * RB + swzf(r, q) * 16) = ra[h];
+    }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) {
+      const int r = srow + RPP * h;
+      *reinterpret_cast<u32x4 *>(tB + r * RB + swzf(r, q) * 16) = rb[h];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  stage(0);
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nks) load(ks + 1);
+    const char *tA = lds[buf], *tB = lds[buf] + BMT * RB;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 af[2], bw[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wr * 32 + i * 16 + lr;
+        af[i] = *reinterpret_cast<const bf16x8 *>(tA + r * RB + swzf(r, kk * 4 + lg) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 32 + j * 16 + lr;
+        bw[j] = *reinterpret_cast<const bf16x8 *>(tB + r * RB + swzf(r, kk * 4 + lg) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (ks + 1 < nks) stage(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t p = p0 + wr * 32 + i * 16 + lr;
+    if (p >= pend) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = n0 + wc * 32 + j * 16 + 4 * lg;
+      *reinterpret_cast<f32x4 *>(Z + p * Cout + co) = acc[i][j];
+    }
+  }
+}
+
+// Y[m][c .. c + 7] = b + sum over taps in order of Z[pair_pos[m][t]] (one thread per 8 channels)
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void pair_reduce_kernel(const int32_t *__restrict__ ppos, int64_t M, int taps,
+                                                          const float *__restrict__ Z, int Cout,
+                                                          const float *__restrict__ bias, void *__restrict__ Y) {
+  const int cpr = Cout / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * cpr) return;
+  const int64_t m = i / cpr;
+  const int c = (int)(i - m * cpr) * 8;
+  f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+    a = *reinterpret_cast<const f32x4 *>(bias + c);
+    b = *reinterpret_cast<const f32x4 *>(bias + c + 4);
+  }
+  for (int t = 0; t < taps; ++t) {
+    const int32_t q = ppos[m * taps + t];
+    if (q < 0) continue;
+    a += *reinterpret_cast<const f32x4 *>(Z + (int64_t)q * Cout + c);
+    b += *reinterpret_cast<const f32x4 *>(Z + (int64_t)q * Cout + c + 4);
+  }
+  if constexpr (OUT_BF16) {
+    *reinterpret_cast<u32x4 *>(reinterpret_cast<bf16_t *>(Y) + m * Cout + c) =
+        mk_u32x4(pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3]));
+  } else {
+    *reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(Y) + m * Cout + c) = a;
+    *reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(Y) + m * Cout + c + 4) = b;
+  }
+}
+
+// dW_t partial of one pair slice g of tap t: sum over its pairs of dY[pair_out] (x) X[pair_in] into
+// ws[g][co][ci] (the k-over-rows MFMA operands of conv3d_wgrad_kernel, gathered through the pair
+// list).  Slices are a fixed number of pairs, so a tap's slice count follows its pair count (the
+// centre tap has every row) and every workgroup has about the same work.
+__global__ __launch_bounds__(THREADS) void pair_wgrad_kernel(PairTaps pt, const int32_t *__restrict__ pin,
+                                                             const int32_t *__restrict__ pout,
+                                                             const bf16_t *__restrict__ X, int Cin,
+                                                             const bf16_t *__restrict__ dY, int Cout,
+                                                             float *__restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2 * WIMG];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, lr = lane & 15, lg = lane >> 4;
+  const int nco = Cout / 64, taps = pt.taps;
+  const int co0 = (blockIdx.x % nco) * 64, ci0 = (blockIdx.x / nco) * 64;
+  const int g = blockIdx.y;
+  int t = 0;
+  while (t + 1 < taps && pt.slice_off[t + 1] <= g) ++t;
+  const int64_t cnt = pt.tap_off[t + 1] - pt.tap_off[t], s0 = (int64_t)(g - pt.slice_off[t]) * pt.slice_len;
+  const int64_t lo = pt.tap_off[t] + pcs_min64(s0, cnt), hi = pt.tap_off[t] + pcs_min64(s0 + pt.slice_len, cnt);
+  const int sv = tid >> 3, q8 = tid & 7;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 rd, rx;
+  auto load = [&](int64_t p0) {
+    const int64_t p = p0 + sv;
+    rd = mk_u32x4(0, 0, 0, 0);
+    rx = mk_u32x4(0, 0, 0, 0);
+    if (p < hi) {
+      rd = *reinterpret_cast<const u32x4 *>(dY + (int64_t)pout[p] * Cout + co0 + q8 * 8);
+      rx = *reinterpret_cast<const u32x4 *>(X + (int64_t)pin[p] * Cin + ci0 + q8 * 8);
+    }
+  };
+  auto stage = [&](int buf) {
+    *reinterpret_cast<u32x4 *>(lds[buf] + woff(sv, q8 * 16)) = rd;
+    *reinterpret_cast<u32x4 *>(lds[buf] + WIMG + woff(sv, q8 * 16)) = rx;
+  };
+  const int nks = (int)((hi - lo + WV - 1) / WV);   // uniform; 0 for an empty slice
+  if (nks > 0) {
+    load(lo);
+    stage(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nks) load(lo + (int64_t)(ks + 1) * WV);
+    bf16x8 fd[2], fx[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fd[i] = wfrag(lds[buf], wr * 32 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fx[j] = wfrag(lds[buf] + WIMG, wc * 32 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
+    if (ks + 1 < nks) stage(buf ^ 1);
+    __syncthreads();
+  }
+  float *out = ws + (int64_t)g * Cout * Cin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = ci0 + wc * 32 + j * 16 + lr;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int co = co0 + wr * 32 + i * 16 + 4 * lg + v;
+        out[(int64_t)co * Cin + ci] = acc[i][j][v];
+      }
+    }
+}
+
+// dW[co][t][ci] = sum over tap t's slices in order of ws[g][co][ci]
+__global__ __launch_bounds__(256) void pair_wgrad_reduce_kernel(PairTaps pt, const float *__restrict__ ws, int Cin,
+                                                                int Cout, float *__restrict__ dW) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // index into dW [Cout][taps][Cin]
+  const int taps = pt.taps;
+  if (i >= (int64_t)Cout * taps * Cin) return;
+  const int ci = (int)(i % Cin);
+  const int64_t r = i / Cin;
+  const int t = (int)(r % taps), co = (int)(r / taps);
+  float s = 0.f;
+  for (int g = pt.slice_off[t]; g < pt.slice_off[t + 1]; ++g) s += ws[((int64_t)g * Cout + co) * Cin + ci];
+  dW[i] = s;
+}
+
+
 }  // namespace
 
 extern "C" int pcs_conv3d(const pcs_conv3d_geom *g, const void *X, const void *W, const float *bias, void *Y,
@@ -1187,6 +1513,157 @@ extern "C" int pcs_sparse_conv_wgrad(const int32_t *nbr, int64_t M, int32_t taps
     PCS_CHECK_LAUNCH();
     hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, wsb, sp,
                        (int64_t)Cout, db);
+    PCS_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// ---- per-tap pair lists (see pairs_count_kernel)
+extern "C" int64_t pcs_sparse_pairs_workspace(int64_t M, int32_t taps) {
+  if (M < 0 || taps < 1 || taps > PT_MAX) return pcs_set_einval("pcs_sparse_pairs_workspace", "bad arguments (1 <= taps <= 27)");
+  return ((M + 255) / 256 * taps + 1) * 4;
+}
+
+extern "C" int pcs_sparse_pairs_count(const int32_t *nbr, int64_t M, int32_t taps, void *workspace, int64_t *tap_counts,
+                                      pcs_stream_t stream) {
+  const int64_t need = pcs_sparse_pairs_workspace(M, taps);
+  if (need < 0) return (int)need;
+  if (!nbr || !workspace || !tap_counts) return pcs_set_einval("pcs_sparse_pairs_count", "nbr, workspace and tap_counts are required");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nblk = (M + 255) / 256;
+  int32_t *cnt = static_cast<int32_t *>(workspace);
+  if (nblk > 0)
+    hipLaunchKernelGGL(pairs_count_kernel, dim3((unsigned)nblk), dim3(256), 0, s, nbr, M, (int)taps, cnt);
+  hipLaunchKernelGGL(pairs_scan_kernel, dim3((unsigned)taps), dim3(256), 0, s, cnt, nblk, (int)taps, tap_counts);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int pcs_sparse_pairs_build(const int32_t *nbr, int64_t M, int32_t taps, const void *workspace,
+                                      const int64_t *tap_counts, int32_t *pair_in, int32_t *pair_out, int32_t *pair_pos,
+                                      pcs_stream_t stream) {
+  if (pcs_sparse_pairs_workspace(M, taps) < 0) return PCS_EINVAL;
+  if (!nbr || !workspace || !tap_counts || !pair_pos || ((!pair_in || !pair_out) && M > 0))
+    return pcs_set_einval("pcs_sparse_pairs_build", "nbr, workspace, tap_counts, pair_in, pair_out and pair_pos are required");
+  if (M * taps >= ((int64_t)1 << 31)) return pcs_set_einval("pcs_sparse_pairs_build", "M * taps must be < 2^31");
+  const int64_t nblk = (M + 255) / 256;
+  if (nblk > 0)
+    hipLaunchKernelGGL(pairs_build_kernel, dim3((unsigned)nblk), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), nbr, M,
+                       (int)taps, static_cast<const int32_t *>(workspace), tap_counts, pair_in, pair_out, pair_pos);
+  PCS_CHECK_LAUNCH();
+  return 0;
+}
+
+namespace {
+// the tap and tile offsets of a pair list from the host copy of its tap offsets
+const char *pair_taps(const int64_t *tap_off, int32_t taps, PairTaps *pt) {
+  if (!tap_off || taps < 1 || taps > PT_MAX) return "tap_off (host, taps + 1 entries) and 1 <= taps <= 27";
+  pt->taps = taps;
+  int64_t tiles = 0;
+  for (int t = 0; t <= taps; ++t) {
+    if (tap_off[t] < (t ? tap_off[t - 1] : 0) || (t == 0 && tap_off[0] != 0)) return "tap_off must start at 0 and not decrease";
+    pt->tap_off[t] = tap_off[t];
+    pt->tile_off[t] = (int32_t)tiles;
+    if (t < taps) tiles += (tap_off[t + 1] - tap_off[t] + 63) / 64;
+  }
+  if (tiles > 0x7fffffff || tap_off[taps] >= ((int64_t)1 << 31)) return "too many pairs";
+  return nullptr;
+}
+}  // namespace
+
+extern "C" int pcs_sparse_conv_pairs(const int32_t *pair_in, const int32_t *pair_pos, const int64_t *tap_off, int32_t taps,
+                                     int64_t M, const void *X, int32_t Cin, const void *W, int32_t Cout,
+                                     const float *bias, float *Z, void *Y, int32_t ydtype, int32_t flip,
+                                     pcs_stream_t stream) {
+  PairTaps pt;
+  const char *why = pair_taps(tap_off, taps, &pt);
+  if (why) return pcs_set_einval("pcs_sparse_conv_pairs", why);
+  if (!pair_pos || !X || !W || !Y || M < 0 || Cin <= 0 || Cout <= 0 || Cin % KS != 0 || Cout % BN != 0 ||
+      (ydtype != PCS_F32 && ydtype != PCS_BF16) || (tap_off[taps] > 0 && (!pair_in || !Z)))
+    return pcs_set_einval("pcs_sparse_conv_pairs", "bad arguments (Cin % 32 == 0, Cout % 64 == 0, Y f32 | bf16, Z [P, Cout] f32)");
+  if (flip && taps != 27 && taps != 1)
+    return pcs_set_einval("pcs_sparse_conv_pairs", "flip needs the centred 27-tap neighbour map (or taps == 1)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int tiles = pt.tile_off[taps];
+  const bf16_t *Xb = static_cast<const bf16_t *>(X), *Wb = static_cast<const bf16_t *>(W);
+  if (tiles > 0) {
+    const dim3 grid((unsigned)tiles, (unsigned)(Cout / BN));
+    if (Cin % 64 == 0) hipLaunchKernelGGL(pair_gemm_kernel<64>, grid, dim3(THREADS), 0, s, pt, pair_in, Xb, (int)Cin, Wb, (int)Cout, (int)flip, Z);
+    else hipLaunchKernelGGL(pair_gemm_kernel<32>, grid, dim3(THREADS), 0, s, pt, pair_in, Xb, (int)Cin, Wb, (int)Cout, (int)flip, Z);
+    PCS_CHECK_LAUNCH();
+  }
+  const int64_t n = M * (Cout / 8);
+  if (n > 0) {
+    const dim3 g((unsigned)((n + 255) / 256));
+    if (ydtype == PCS_BF16) hipLaunchKernelGGL(pair_reduce_kernel<true>, g, dim3(256), 0, s, pair_pos, M, (int)taps, Z, (int)Cout, bias, Y);
+    else hipLaunchKernelGGL(pair_reduce_kernel<false>, g, dim3(256), 0, s, pair_pos, M, (int)taps, Z, (int)Cout, bias, Y);
+    PCS_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+namespace {
+// weight-gradient slices: slice_len pairs each (at least 4 k-steps, about 2048 slices in all),
+// ceil(count / slice_len) per tap (at least one, so every tap's partial is written)
+void pair_wgrad_slices(PairTaps *pt) {
+  const int64_t P = pt->tap_off[pt->taps];
+  int64_t len = (P + 2047) / 2048;
+  len = (len < 4 * WV ? 4 * WV : len + WV - 1) / WV * WV;
+  pt->slice_len = len;
+  int64_t g = 0;
+  for (int t = 0; t <= pt->taps; ++t) {
+    pt->slice_off[t] = (int32_t)g;
+    if (t < pt->taps) {
+      const int64_t c = pt->tap_off[t + 1] - pt->tap_off[t];
+      g += c > 0 ? (c + len - 1) / len : 1;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int64_t pcs_sparse_conv_wgrad_pairs_workspace(const int64_t *tap_off, int32_t taps, int64_t M, int32_t Cin,
+                                                         int32_t Cout) {
+  PairTaps pt;
+  const char *why = pair_taps(tap_off, taps, &pt);
+  if (why) return pcs_set_einval("pcs_sparse_conv_wgrad_pairs_workspace", why);
+  if (M < 0 || Cin <= 0 || Cout <= 0 || Cin % 64 != 0 || Cout % 64 != 0)
+    return pcs_set_einval("pcs_sparse_conv_wgrad_pairs_workspace", "bad arguments (Cin, Cout multiples of 64)");
+  pair_wgrad_slices(&pt);
+  const int64_t spb = sparse_wgrad_splits(M, 1, 64, Cout);
+  return ((int64_t)pt.slice_off[taps] * Cout * Cin + spb * Cout) * 4;
+}
+
+extern "C" int pcs_sparse_conv_wgrad_pairs(const int32_t *pair_in, const int32_t *pair_out, const int64_t *tap_off,
+                                           int32_t taps, int64_t M, const void *X, int32_t Cin, const void *dY,
+                                           int32_t Cout, void *workspace, int64_t workspace_bytes, float *dW, float *db,
+                                           pcs_stream_t stream) {
+  const int64_t need = pcs_sparse_conv_wgrad_pairs_workspace(tap_off, taps, M, Cin, Cout);
+  if (need < 0) return (int)need;
+  if (!X || !dY || !dW || !workspace || workspace_bytes < need || (tap_off[taps] > 0 && (!pair_in || !pair_out)))
+    return pcs_set_einval("pcs_sparse_conv_wgrad_pairs", "pairs, X, dY, dW and a workspace of pcs_sparse_conv_wgrad_pairs_workspace bytes");
+  PairTaps pt;
+  pair_taps(tap_off, taps, &pt);
+  pair_wgrad_slices(&pt);
+  const int64_t ns = pt.slice_off[taps], wlen = (int64_t)Cout * taps * Cin;
+  float *ws = static_cast<float *>(workspace), *wsb = ws + ns * Cout * Cin;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(pair_wgrad_kernel, dim3((unsigned)((Cout / 64) * (Cin / 64)), (unsigned)ns), dim3(THREADS), 0, s,
+                     pt, pair_in, pair_out, static_cast<const bf16_t *>(X), (int)Cin, static_cast<const bf16_t *>(dY), (int)Cout, ws);
+  PCS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pair_wgrad_reduce_kernel, dim3((unsigned)((wlen + 255) / 256)), dim3(256), 0, s, pt, ws, (int)Cin, (int)Cout, dW);
+  PCS_CHECK_LAUNCH();
+  if (db) {
+    const int64_t spb = sparse_wgrad_splits(M, 1, 64, Cout);
+    const int64_t vps = ((M + spb - 1) / spb + WV - 1) / WV * WV;
+    if (M > 0) {
+      hipLaunchKernelGGL(conv3d_bgrad_kernel, dim3((unsigned)((Cout + 63) / 64), (unsigned)spb), dim3(THREADS), 0, s,
+                         static_cast<const bf16_t *>(dY), (int)Cout, M, vps, wsb);
+    } else {
+      const hipError_t e = hipMemsetAsync(wsb, 0, spb * Cout * 4, s);
+      if (e != hipSuccess) return pcs_set_error(e, "pcs_sparse_conv_wgrad_pairs");
+    }
+    PCS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(conv3d_reduce_kernel, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, wsb, spb, (int64_t)Cout, db);
     PCS_CHECK_LAUNCH();
   }
   return 0;

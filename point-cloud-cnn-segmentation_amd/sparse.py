@@ -17,7 +17,7 @@ the transposed, tap-flipped weight).
 from __future__ import annotations
 
 import ctypes as ct
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 
@@ -26,6 +26,10 @@ from .data import RaggedBatch
 from .voxel import CH_ALIGN, VoxelBatch, _box, _bf16_2d, _ceil, _pad_channels
 
 TAPS = 27
+# pair lists (gather-GEMM-reduce) when the map has at most this many occupied taps per voxel;
+# above it the tile-gather kernels, whose zero rows are then few and which need no per-pair
+# products in memory (profiles/bench_sparse_pairs_r05.txt)
+PAIR_TAPS_MAX = 3.0
 
 
 @dataclass
@@ -35,10 +39,37 @@ class SparseVoxels:
     table_vals: torch.Tensor   # int32 [cap]
     nbr: torch.Tensor          # int32 [V, 27]
     grid: int
+    _pairs: tuple = field(default=None, repr=False)   # (pair_in, pair_out, pair_pos, tap_off host array, P)
 
     @property
     def num_voxels(self) -> int:
         return self.keys.numel()
+
+    def pairs(self):
+        """Per-tap pair lists of the neighbour map, built once (pcs_sparse_pairs_*; one host read of
+        the 27 tap counts): (pair_in, pair_out, pair_pos, tap_off, P) with tap_off a host int64
+        array of 28 entries."""
+        if self._pairs is None:
+            V, dev = self.num_voxels, self.nbr.device
+            st = L.stream_ptr(dev)
+            nb = int(L.load().pcs_sparse_pairs_workspace(V, TAPS))
+            if nb < 0:
+                raise L.PcsError(L.load().pcs_last_error().decode())
+            ws = torch.empty(max(nb // 4, 1), dtype=torch.int32, device=dev)
+            counts = torch.empty(TAPS, dtype=torch.int64, device=dev)
+            L.call("pcs_sparse_pairs_count", L.ptr(self.nbr), V, TAPS, L.ptr(ws), L.ptr(counts), st)
+            tap_off = (ct.c_int64 * (TAPS + 1))(0, *torch.cumsum(counts, 0).tolist())
+            P = int(tap_off[TAPS])
+            pin = torch.empty(max(P, 1), dtype=torch.int32, device=dev)
+            pout = torch.empty(max(P, 1), dtype=torch.int32, device=dev)
+            ppos = torch.empty(V, TAPS, dtype=torch.int32, device=dev)
+            L.call("pcs_sparse_pairs_build", L.ptr(self.nbr), V, TAPS, L.ptr(ws), L.ptr(counts), L.ptr(pin), L.ptr(pout),
+                   L.ptr(ppos), st)
+            self._pairs = (pin, pout, ppos, tap_off, P)
+        return self._pairs
+
+    def use_pairs(self) -> bool:
+        return self.num_voxels > 0 and self.pairs()[4] <= PAIR_TAPS_MAX * self.num_voxels
 
     def find(self, keys: torch.Tensor) -> torch.Tensor:
         """int32 rows of the voxels with these keys (-1: unoccupied), one device lookup each."""
@@ -84,12 +115,22 @@ def sparse_voxels(rb: RaggedBatch, vb: VoxelBatch, lo=(-1.0, -1.0, -1.0), hi=(1.
     return sparse_from_keys(keys, vb.grid)
 
 
+def _conv_pairs(sv, x, cin, w, cout, bias, y, ydt, flip):
+    """y = the submanifold convolution of x through the pair lists (Z = per-pair products, fp32)."""
+    pin, _, ppos, tap_off, P = sv.pairs()
+    z = torch.empty(max(P, 1), cout, dtype=torch.float32, device=x.device)
+    L.call("pcs_sparse_conv_pairs", L.ptr(pin), L.ptr(ppos), ct.addressof(tap_off), TAPS, sv.num_voxels, L.ptr(x), cin,
+           L.ptr(w), cout, L.ptr(bias) if bias is not None else None, L.ptr(z), L.ptr(y), ydt, flip,
+           L.stream_ptr(x.device))
+
+
 class _SubMConvFn(torch.autograd.Function):
     """y = b + sum_t W_t x[nbr[:, t]] with w in kernel layout [Cout, 27 * Cin] (fp32 master);
     channel counts off the 64 multiple run zero-padded (exact, as voxel._Conv3dFn)."""
 
     @staticmethod
-    def forward(ctx, x, wk, bias, nbr, out_dtype):
+    def forward(ctx, x, wk, bias, sv, out_dtype):
+        nbr = sv.nbr
         if not x.is_cuda:
             raise RuntimeError("pcs_amd sparse conv runs on a HIP device only (no CPU fallback)")
         if x.dtype != torch.bfloat16 or x.dim() != 2 or nbr.shape != (x.shape[0], TAPS):
@@ -109,10 +150,15 @@ class _SubMConvFn(torch.autograd.Function):
         if bias is not None:
             bk = bias.float().contiguous() if cout_k == cout else _pad_channels(bias.float(), cout_k)
         y = torch.empty(V, cout_k, dtype=out_dtype, device=x.device)
-        L.call("pcs_sparse_conv", L.ptr(nbr), V, TAPS, L.ptr(xk), cin_k, L.ptr(wb), cout_k,
-               L.ptr(bk) if bk is not None else None, L.ptr(y), L.BF16 if out_dtype == torch.bfloat16 else L.F32, 0,
-               L.stream_ptr(x.device))
+        ydt = L.BF16 if out_dtype == torch.bfloat16 else L.F32
+        pairs = sv.use_pairs()
+        if pairs:
+            _conv_pairs(sv, xk, cin_k, wb, cout_k, bk, y, ydt, 0)
+        else:
+            L.call("pcs_sparse_conv", L.ptr(nbr), V, TAPS, L.ptr(xk), cin_k, L.ptr(wb), cout_k,
+                   L.ptr(bk) if bk is not None else None, L.ptr(y), ydt, 0, L.stream_ptr(x.device))
         ctx.save_for_backward(xk, wb, nbr)
+        ctx.sv, ctx.pairs = sv, pairs
         ctx.cfg = (bias is not None, cin, cout)
         return y if cout_k == cout else y[:, :cout].contiguous()
 
@@ -129,19 +175,31 @@ class _SubMConvFn(torch.autograd.Function):
             wt = torch.empty(cin_k, TAPS * cout_k, dtype=torch.bfloat16, device=dev)
             L.call("pcs_conv3d_weight_t", L.ptr(wb), cout_k, TAPS, cin_k, L.ptr(wt), st)
             dx = torch.empty(V, cin_k, dtype=torch.bfloat16, device=dev)
-            L.call("pcs_sparse_conv", L.ptr(nbr), V, TAPS, L.ptr(dyb), cout_k, L.ptr(wt), cin_k, None, L.ptr(dx),
-                   L.BF16, 1, st)
+            if ctx.pairs:
+                _conv_pairs(ctx.sv, dyb, cout_k, wt, cin_k, None, dx, L.BF16, 1)
+            else:
+                L.call("pcs_sparse_conv", L.ptr(nbr), V, TAPS, L.ptr(dyb), cout_k, L.ptr(wt), cin_k, None, L.ptr(dx),
+                       L.BF16, 1, st)
             if cin_k != cin:
                 dx = dx[:, :cin].contiguous()
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            nbytes = int(L.load().pcs_sparse_conv_wgrad_workspace(V, TAPS, cin_k, cout_k))
+            if ctx.pairs:
+                pin, pout, _, tap_off, _ = ctx.sv.pairs()
+                nbytes = int(L.load().pcs_sparse_conv_wgrad_pairs_workspace(ct.addressof(tap_off), TAPS, V, cin_k,
+                                                                            cout_k))
+            else:
+                nbytes = int(L.load().pcs_sparse_conv_wgrad_workspace(V, TAPS, cin_k, cout_k))
             if nbytes < 0:
                 raise L.PcsError(L.load().pcs_last_error().decode())
             ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
             dwk = torch.empty(cout_k, TAPS * cin_k, dtype=torch.float32, device=dev)
             db = torch.empty(cout_k, dtype=torch.float32, device=dev) if has_bias else None
-            L.call("pcs_sparse_conv_wgrad", L.ptr(nbr), V, TAPS, L.ptr(xk), cin_k, L.ptr(dyb), cout_k, L.ptr(ws),
-                   nbytes, L.ptr(dwk), L.ptr(db), st)
+            if ctx.pairs:
+                L.call("pcs_sparse_conv_wgrad_pairs", L.ptr(pin), L.ptr(pout), ct.addressof(tap_off), TAPS, V, L.ptr(xk),
+                       cin_k, L.ptr(dyb), cout_k, L.ptr(ws), nbytes, L.ptr(dwk), L.ptr(db), st)
+            else:
+                L.call("pcs_sparse_conv_wgrad", L.ptr(nbr), V, TAPS, L.ptr(xk), cin_k, L.ptr(dyb), cout_k, L.ptr(ws),
+                       nbytes, L.ptr(dwk), L.ptr(db), st)
             if (cin_k, cout_k) != (cin, cout):
                 dwk = dwk.reshape(cout_k, TAPS, cin_k)[:cout, :, :cin].reshape(cout, TAPS * cin)
                 db = db[:cout] if db is not None else None
@@ -155,7 +213,7 @@ def submanifold_conv3d(x, weight, sv: SparseVoxels, bias=None, out_dtype=torch.b
     if k != 3 or tuple(weight.shape[2:]) != (3, 3, 3):
         raise ValueError("submanifold_conv3d is the 3x3x3 form")
     wk = weight.permute(0, 2, 3, 4, 1).reshape(cout, TAPS * cin)
-    return _SubMConvFn.apply(x, wk, bias, sv.nbr, out_dtype)
+    return _SubMConvFn.apply(x, wk, bias, sv, out_dtype)
 
 
 class SubMConv3d(torch.nn.Module):

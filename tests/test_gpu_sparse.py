@@ -69,9 +69,18 @@ def _dense(x, keys, grid, B):
     return d, (s, ix, iy, iz)
 
 
+@pytest.fixture(params=["gather", "pairs"])
+def conv_path(request, monkeypatch):
+    """Both forms of the submanifold convolution: the tile-gather kernel and the per-tap pair lists
+    (sparse.PAIR_TAPS_MAX picks between them by occupied taps per voxel)."""
+    import pcs_amd.sparse as S
+    monkeypatch.setattr(S, "PAIR_TAPS_MAX", 0.0 if request.param == "gather" else 27.0)
+    return request.param
+
+
 @pytest.mark.parametrize("grid,occupancy,cin,cout", [(16, 0.3, 64, 64), (32, 0.05, 64, 128),
                                                     (16, 0.2, 4, 32), (24, 0.1, 32, 64)])
-def test_submanifold_conv_matches_dense_conv3d(grid, occupancy, cin, cout):
+def test_submanifold_conv_matches_dense_conv3d(grid, occupancy, cin, cout, conv_path):
     from pcs_amd.sparse import submanifold_conv3d
     rb = _batch(5 + cin + grid, 2, grid, occupancy)
     _, sv = _sparse(rb, grid)
@@ -103,9 +112,32 @@ def test_submanifold_conv_matches_dense_conv3d(grid, occupancy, cin, cout):
     # and the numpy restatement on the neighbour map
     assert rel(y, torch.from_numpy(so.submanifold_conv(x.double().numpy(), w.numpy(), b.numpy(),
                                                        sv.nbr.cpu().numpy()))) < 1e-5
+    assert sv.use_pairs() == (conv_path == "pairs")
 
 
-def test_isolated_voxels_run_only_the_centre_tap():
+def test_pair_lists_match_the_neighbour_map():
+    """Per-tap pair lists: tap t's pairs are exactly the rows m with nbr[m][t] >= 0, ascending,
+    pair_in = nbr[pair_out][t], and pair_pos indexes them back (-1 elsewhere); the same lists on a
+    rebuild (deterministic)."""
+    from pcs_amd.sparse import TAPS, sparse_from_keys
+    rb = _batch(3, 3, 20, 0.07)
+    _, sv = _sparse(rb, 20)
+    pin, pout, ppos, tap_off, P = sv.pairs()
+    nbr = sv.nbr.cpu().numpy()
+    pin, pout, ppos = pin.cpu().numpy()[:P], pout.cpu().numpy()[:P], ppos.cpu().numpy()
+    assert P == int((nbr >= 0).sum())
+    for t in range(TAPS):
+        rows = np.nonzero(nbr[:, t] >= 0)[0]
+        a, b = tap_off[t], tap_off[t + 1]
+        assert np.array_equal(pout[a:b], rows)
+        assert np.array_equal(pin[a:b], nbr[rows, t])
+        assert np.array_equal(ppos[rows, t], np.arange(a, b))
+    assert (ppos[nbr < 0] == -1).all()
+    sv2 = sparse_from_keys(sv.keys, 20)
+    assert all(torch.equal(u[:P].cpu(), v[:P].cpu()) for u, v in zip(sv.pairs()[:3], sv2.pairs()[:3]))
+
+
+def test_isolated_voxels_run_only_the_centre_tap(conv_path):
     """Voxels with no occupied neighbour: every tile's tap mask is the centre tap alone, and the
     output is the 1x1 channel mix of the centre weight."""
     from pcs_amd.sparse import sparse_from_keys, submanifold_conv3d

@@ -1,7 +1,8 @@
 """Occupied-voxel path at BASELINE configs[2]'s scale: a 256^3 effective grid, jittered clouds
 occupying ~2 % of it (pcs_amd.data.jittered_clouds), 4 scenes.  Times the sparse index (voxel keys,
 hash table, 27-neighbour map) and one 64 -> 64 submanifold 3x3x3 convolution forward, input
-gradient and weight gradient; prints voxels/s and the useful TF/s (taps with a neighbour only).
+gradient and weight gradient, in the tile-gather form and through per-tap pair lists; prints
+voxels/s and the useful TF/s (taps with a neighbour only).
     python tools/bench_sparse.py [reps] [occupancy]"""
 import os
 import sys
@@ -63,6 +64,25 @@ def main():
         print(f"submanifold 3x3x3 {C}->{C} {name}: {ms:.3f} ms = {V / ms / 1e3:.1f} M voxels/s, "
               f"{useful / ms * 1e3:.1f} useful TF/s", flush=True)
     print(f"fwd + bwd: {tot:.3f} ms = {V / tot / 1e3:.1f} M voxels/s", flush=True)
+    # the per-tap pair-list form of the same three convolutions (pairs built once per map)
+    import ctypes as ct
+    ms_pairs = timeit(lambda: (setattr(sv, "_pairs", None), sv.pairs()), 1)
+    pin, pout, ppos, tap_off, P = sv.pairs()
+    z = torch.empty(max(P, 1), C, device=dev)
+    ta = ct.addressof(tap_off)
+    pfwd = lambda: L.call("pcs_sparse_conv_pairs", L.ptr(pin), L.ptr(ppos), ta, TAPS, V, L.ptr(x), C, L.ptr(w), C, None, L.ptr(z), L.ptr(y), L.BF16, 0, st)  # noqa: E731
+    pdgr = lambda: L.call("pcs_sparse_conv_pairs", L.ptr(pin), L.ptr(ppos), ta, TAPS, V, L.ptr(y), C, L.ptr(wt), C, None, L.ptr(z), L.ptr(x), L.BF16, 1, st)  # noqa: E731
+    nbp = int(L.load().pcs_sparse_conv_wgrad_pairs_workspace(ta, TAPS, V, C, C))
+    wsp = torch.empty(nbp // 4, device=dev)
+    pwgr = lambda: L.call("pcs_sparse_conv_wgrad_pairs", L.ptr(pin), L.ptr(pout), ta, TAPS, V, L.ptr(x), C, L.ptr(y), C, L.ptr(wsp), nbp, L.ptr(dw), L.ptr(db), st)  # noqa: E731
+    print(f"pair lists (build, once per neighbour map): {ms_pairs:.3f} ms", flush=True)
+    tot = 0.0
+    for name, fn in [("forward", pfwd), ("input gradient", pdgr), ("weight gradient", pwgr)]:
+        ms = timeit(fn, reps)
+        tot += ms
+        print(f"pairs: submanifold 3x3x3 {C}->{C} {name}: {ms:.3f} ms = {V / ms / 1e3:.1f} M voxels/s, "
+              f"{useful / ms * 1e3:.1f} useful TF/s", flush=True)
+    print(f"pairs: fwd + bwd: {tot:.3f} ms = {V / tot / 1e3:.1f} M voxels/s", flush=True)
 
 
 if __name__ == "__main__":
