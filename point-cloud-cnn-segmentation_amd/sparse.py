@@ -26,10 +26,12 @@ from .data import RaggedBatch
 from .voxel import CH_ALIGN, VoxelBatch, _box, _bf16_2d, _ceil, _pad_channels
 
 TAPS = 27
-# pair lists (gather-GEMM-reduce) when the map has at most this many occupied taps per voxel;
-# above it the tile-gather kernels, whose zero rows are then few and which need no per-pair
-# products in memory (profiles/bench_sparse_pairs_r05.txt)
+# forward / input gradient through the pair lists (gather-GEMM-reduce) when the map has at most
+# this many occupied taps per voxel; above it the tile-gather kernel, whose zero rows are then few
+# and which keeps no per-pair products in memory.  The weight gradient takes the pair lists at
+# every occupancy (PAIR_WGRAD).  profiles/bench_sparse_pairs_r05.txt
 PAIR_TAPS_MAX = 3.0
+PAIR_WGRAD = True
 
 
 @dataclass
@@ -69,6 +71,7 @@ class SparseVoxels:
         return self._pairs
 
     def use_pairs(self) -> bool:
+        """The forward / input gradient form for this map (the pair lists or the tile gather)."""
         return self.num_voxels > 0 and self.pairs()[4] <= PAIR_TAPS_MAX * self.num_voxels
 
     def find(self, keys: torch.Tensor) -> torch.Tensor:
@@ -158,7 +161,7 @@ class _SubMConvFn(torch.autograd.Function):
             L.call("pcs_sparse_conv", L.ptr(nbr), V, TAPS, L.ptr(xk), cin_k, L.ptr(wb), cout_k,
                    L.ptr(bk) if bk is not None else None, L.ptr(y), ydt, 0, L.stream_ptr(x.device))
         ctx.save_for_backward(xk, wb, nbr)
-        ctx.sv, ctx.pairs = sv, pairs
+        ctx.sv, ctx.pairs, ctx.wpairs = sv, pairs, PAIR_WGRAD and V > 0
         ctx.cfg = (bias is not None, cin, cout)
         return y if cout_k == cout else y[:, :cout].contiguous()
 
@@ -183,7 +186,7 @@ class _SubMConvFn(torch.autograd.Function):
             if cin_k != cin:
                 dx = dx[:, :cin].contiguous()
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            if ctx.pairs:
+            if ctx.wpairs:
                 pin, pout, _, tap_off, _ = ctx.sv.pairs()
                 nbytes = int(L.load().pcs_sparse_conv_wgrad_pairs_workspace(ct.addressof(tap_off), TAPS, V, cin_k,
                                                                             cout_k))
@@ -194,7 +197,7 @@ class _SubMConvFn(torch.autograd.Function):
             ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=dev)
             dwk = torch.empty(cout_k, TAPS * cin_k, dtype=torch.float32, device=dev)
             db = torch.empty(cout_k, dtype=torch.float32, device=dev) if has_bias else None
-            if ctx.pairs:
+            if ctx.wpairs:
                 L.call("pcs_sparse_conv_wgrad_pairs", L.ptr(pin), L.ptr(pout), ct.addressof(tap_off), TAPS, V, L.ptr(xk),
                        cin_k, L.ptr(dyb), cout_k, L.ptr(ws), nbytes, L.ptr(dwk), L.ptr(db), st)
             else:

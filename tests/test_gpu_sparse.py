@@ -75,6 +75,7 @@ def conv_path(request, monkeypatch):
     (sparse.PAIR_TAPS_MAX picks between them by occupied taps per voxel)."""
     import pcs_amd.sparse as S
     monkeypatch.setattr(S, "PAIR_TAPS_MAX", 0.0 if request.param == "gather" else 27.0)
+    monkeypatch.setattr(S, "PAIR_WGRAD", request.param == "pairs")
     return request.param
 
 
