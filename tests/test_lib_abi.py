@@ -113,3 +113,25 @@ def test_seg_backward_geometry_without_gpu():
             cps = a.chunks_per_scene
             assert nbytes == 4 * cps * cout * cin * 4
             assert cps * 4 * nblk >= 256 and cps * 4 * nblk < 2 * 256   # about one workgroup per CU
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
+def test_sparse_pairs_argument_validation_without_gpu():
+    """The pair-list entry points reject bad tap offsets and channel counts on the host, before
+    any launch, and size their workspaces from the host tap offsets (no GPU needed)."""
+    import pcs_amd._lib as L
+    lib = L.load()
+    assert lib.pcs_sparse_pairs_workspace(1000, 27) == ((1000 + 255) // 256 * 27 + 1) * 4
+    assert lib.pcs_sparse_pairs_workspace(-1, 27) == -1000
+    assert lib.pcs_sparse_pairs_workspace(10, 28) == -1000
+    good = (ct.c_int64 * 28)(*([0] * 13 + [100] * 15))       # only the centre tap: 100 rows
+    ta = ct.addressof(good)
+    assert lib.pcs_sparse_conv_wgrad_pairs_workspace(ta, 27, 100, 64, 64) > 0
+    assert lib.pcs_sparse_conv_wgrad_pairs_workspace(ta, 27, 100, 32, 64) == -1000   # Cin % 64
+    bad = (ct.c_int64 * 28)(*([0] * 13 + [100] * 14 + [50]))   # decreasing
+    assert lib.pcs_sparse_conv_wgrad_pairs_workspace(ct.addressof(bad), 27, 100, 64, 64) == -1000
+    start = (ct.c_int64 * 28)(*([5] + [100] * 27))             # not starting at 0
+    assert lib.pcs_sparse_conv_pairs(1, 1, ct.addressof(start), 27, 100, 1, 64, 1, 64, None, 1, 1, L.BF16, 0,
+                                     None) == -1000
+    assert lib.pcs_sparse_conv_pairs(1, 1, ta, 27, 100, 1, 64, 1, 48, None, 1, 1, L.BF16, 0, None) == -1000   # Cout
+    assert lib.pcs_sparse_conv_pairs(1, 1, ta, 27, 100, 1, 64, 1, 64, None, None, 1, L.BF16, 0, None) == -1000   # no Z
