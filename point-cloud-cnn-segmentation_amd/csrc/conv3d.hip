@@ -1529,6 +1529,7 @@ extern "C" int pcs_sparse_pairs_count(const int32_t *nbr, int64_t M, int32_t tap
   const int64_t need = pcs_sparse_pairs_workspace(M, taps);
   if (need < 0) return (int)need;
   if (!nbr || !workspace || !tap_counts) return pcs_set_einval("pcs_sparse_pairs_count", "nbr, workspace and tap_counts are required");
+  if (M * taps >= ((int64_t)1 << 31)) return pcs_set_einval("pcs_sparse_pairs_count", "M * taps must be < 2^31");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t nblk = (M + 255) / 256;
   int32_t *cnt = static_cast<int32_t *>(workspace);
