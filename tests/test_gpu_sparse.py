@@ -69,13 +69,15 @@ def _dense(x, keys, grid, B):
     return d, (s, ix, iy, iz)
 
 
-@pytest.fixture(params=["gather", "pairs"])
+@pytest.fixture(params=["gather", "pairs", "default"])
 def conv_path(request, monkeypatch):
     """Both forms of the submanifold convolution: the tile-gather kernel and the per-tap pair lists
-    (sparse.PAIR_TAPS_MAX picks between them by occupied taps per voxel)."""
+    (sparse.PAIR_TAPS_MAX picks between them by occupied taps per voxel), and the module's own mix
+    (the weight gradient always on the pair lists)."""
     import pcs_amd.sparse as S
-    monkeypatch.setattr(S, "PAIR_TAPS_MAX", 0.0 if request.param == "gather" else 27.0)
-    monkeypatch.setattr(S, "PAIR_WGRAD", request.param == "pairs")
+    if request.param != "default":
+        monkeypatch.setattr(S, "PAIR_TAPS_MAX", 0.0 if request.param == "gather" else 27.0)
+        monkeypatch.setattr(S, "PAIR_WGRAD", request.param == "pairs")
     return request.param
 
 
@@ -113,7 +115,8 @@ def test_submanifold_conv_matches_dense_conv3d(grid, occupancy, cin, cout, conv_
     # and the numpy restatement on the neighbour map
     assert rel(y, torch.from_numpy(so.submanifold_conv(x.double().numpy(), w.numpy(), b.numpy(),
                                                        sv.nbr.cpu().numpy()))) < 1e-5
-    assert sv.use_pairs() == (conv_path == "pairs")
+    if conv_path != "default":
+        assert sv.use_pairs() == (conv_path == "pairs")
 
 
 def test_pair_lists_match_the_neighbour_map():
