@@ -748,7 +748,11 @@ int pcs_sparse_conv_wgrad_pairs(const int32_t *pair_in, const int32_t *pair_out,
                                 int32_t taps, int64_t M, const void *X, int32_t Cin, const void *dY, int32_t Cout,
                                 void *workspace, int64_t workspace_bytes, float *dW, float *db, pcs_stream_t stream);
 
-/* Build-time identification and error string. */
+/* Build-time identification and error string.  pcs_abi_version() returns PCS_ABI_VERSION,
+ * bumped with every change to an argument struct's layout or an entry point's signature
+ * (2: pcs_gemm_args gained `gram`, the w4 entry points were removed); a binding checks it
+ * before its first call. */
+#define PCS_ABI_VERSION 2
 int pcs_abi_version(void);
 const char *pcs_last_error(void);
 

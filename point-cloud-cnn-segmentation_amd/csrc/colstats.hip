@@ -44,8 +44,8 @@ __global__ __launch_bounds__(THREADS) void colstats_kernel(const T *__restrict__
       m2[e] = fmaf(d, v[e] - mean[e], m2[e]);
       if constexpr (POOL) {
         const int g = (int)(scene * N + r);
-        if (v[e] > mx[e]) { mx[e] = v[e]; mxi[e] = g; }   // rows ascend: first max kept
-        if (v[e] < mn[e]) { mn[e] = v[e]; mni[e] = g; }
+        if (pool_max_step(v[e], mx[e], mxi[e])) { mx[e] = v[e]; mxi[e] = g; }   // rows ascend: first max kept
+        if (pool_min_step(v[e], mn[e], mni[e])) { mn[e] = v[e]; mni[e] = g; }
       }
     }
   }
@@ -73,8 +73,8 @@ __global__ __launch_bounds__(THREADS) void colstats_kernel(const T *__restrict__
         for (int j = 0; j < rpp; ++j) {
           const float4 p = red[j * cpr + cc];
           const int pi = __float_as_int(p.y), pj = __float_as_int(p.w);
-          if (p.x > a || (p.x == a && pi < ai)) { a = p.x; ai = pi; }
-          if (p.z < b || (p.z == b && pj < bi)) { b = p.z; bi = pj; }
+          if (pool_max_wins(p.x, pi, a, ai)) { a = p.x; ai = pi; }
+          if (pool_min_wins(p.z, pj, b, bi)) { b = p.z; bi = pj; }
         }
         *reinterpret_cast<float4 *>(pool + ((int64_t)chunk * C + cc * EPC + e) * 4) =
             make_float4(a, __int_as_float(ai), b, __int_as_float(bi));

@@ -134,6 +134,34 @@ PCS_DEV void chan_merge(float &n, float &mean, float &m2, float nb, float meanb,
   n = nn;
 }
 
+// ReLU as torch.relu: a NaN propagates.  __builtin_elementwise_maximum (IEEE 754-2019 maximum)
+// lowers to v_maximum3_f32 on gfx950, issued at the v_max_f32 rate (4.6 against 4.5 cycles per
+// wave-instruction, tools/probes/probe_maximum3.hip); fmaxf's maxNum would turn a NaN into 0, so a
+// diverged run would report a finite loss where the reference reports NaN
+PCS_DEV float relu(float x) { return __builtin_elementwise_maximum(x, 0.f); }
+
+// Max-pool candidate order of torch.max / torch.min over a dim (P:114): a NaN beats every
+// number (torch propagates it), and among equal values -- or among NaNs -- the smaller row
+// wins (the first one in row order).  (v, vi) is the candidate, (cur, ci) the running pick.
+// (Bitwise on bools, so the selects stay branch-free: an ordered compare with a NaN operand
+// is false, so the last two terms only ever hold between two numbers.)
+PCS_DEV bool pool_max_wins(float v, int vi, float cur, int ci) {
+  return ((v != v) & ((cur == cur) | (vi < ci))) | (v > cur) | ((v == cur) & (vi < ci));
+}
+PCS_DEV bool pool_min_wins(float v, int vi, float cur, int ci) {
+  return ((v != v) & ((cur == cur) | (vi < ci))) | (v < cur) | ((v == cur) & (vi < ci));
+}
+// per-element running pick over ascending rows: a later row replaces the pick only when it is
+// strictly greater (smaller) or the first NaN; the first row always makes a pick (ci is the
+// 0x7fffffff "none yet" sentinel until then), so a column of -inf still gets its first row
+constexpr int PCS_POOL_NONE = 0x7fffffff;
+PCS_DEV bool pool_max_step(float v, float cur, int ci) {
+  return (v > cur) | ((v != v) & (cur == cur)) | (ci == PCS_POOL_NONE);
+}
+PCS_DEV bool pool_min_step(float v, float cur, int ci) {
+  return (v < cur) | ((v != v) & (cur == cur)) | (ci == PCS_POOL_NONE);
+}
+
 // row-tile geometry of one scene-aware chunk (rows never straddle scenes)
 struct ChunkGeo {
   int64_t scene_rows;   // N: rows per scene (padded cloud length)

@@ -17,4 +17,6 @@ int pcs_set_einval(const char *where, const char *msg) {
 }
 
 extern "C" const char *pcs_last_error(void) { return g_err; }
-extern "C" int pcs_abi_version(void) { return 1; }
+// PCS_ABI_VERSION (include/pcs.h): bumped whenever an argument struct's layout or an entry
+// point's signature changes; _lib.load() refuses a library whose number differs
+extern "C" int pcs_abi_version(void) { return PCS_ABI_VERSION; }

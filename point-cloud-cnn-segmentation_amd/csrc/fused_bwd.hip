@@ -164,7 +164,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
     lds_vec8(cf + CS + xc * 8, xs); lds_vec8(cf + CS + CIN + xc * 8, xt);
     unpack_chunk(rx, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(v[e], xs[e], xt[e]));
     u32x4 out = pack_chunk(v);
     if (m0 + xr >= hi) out = mk_u32x4(0, 0, 0, 0);
     if constexpr (FOLDED) {   // the sums of the stored (bf16) x, as the contractions see it
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
       unpack_chunk(rp[i], v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float x = fmaxf(fmaf(v[e], s8[e], t8[e]), 0.f);
+        float x = relu(fmaf(v[e], s8[e], t8[e]));
         if constexpr (MASK) x = ((rm[i] >> e) & 1u) ? x * ks : 0.f;
         v[e] = x;
       }

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(THREADS) void c5_dgrad_kernel(pcs_gemm_args a, int6
     lds_vec8(cft + NC * 4, NC * 2, sh);
     unpack_chunk(*reinterpret_cast<const u32x4 *>(lds + sidx * STAGE + o_ty), v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(v[e], sc[e], sh[e]));
     u32x4 out = pack_chunk(v);
     if (rem < MS && trow >= rem) out = mk_u32x4(0, 0, 0, 0);
     *reinterpret_cast<u32x4 *>(lds + o_ta) = out;

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(THREADS) void seg_bwd_kernel(pcs_gemm_args a, float
     lds_vec8(cfx + CB * 4, CB * 2, xt);
     unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o_ypx), v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(v[e], xs[e], xt[e]));
     u32x4 out = pack_chunk(v);
     if constexpr (MASK) {   // dropout: AND with the byte's masks (one LDS read for 8 values)
       const u32x4 m = *reinterpret_cast<const u32x4 *>(lds + F::OFF_LUT + (uint32_t)(uint8_t)st[o_mkx] * 16);

@@ -424,7 +424,7 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
         const int kb = __builtin_amdgcn_sbfe((int)wb, 16 * (ct & 1) + l16, 1);
         const int keep = (MASK || 4 * g + r < rem) ? kb : 0;
         const float z = fmaf(y, esk[ct], etk[ct]);
-        xv[r] = __int_as_float(__float_as_int(fmaxf(z, 0.f)) & keep);
+        xv[r] = __int_as_float(__float_as_int(relu(z)) & keep);
         v[r] = xv[r] > 0.f ? dacc[ct][r] * ks : 0.f;
         s1[ct] += v[r];
         s2[ct] = fmaf(v[r], y, s2[ct]);

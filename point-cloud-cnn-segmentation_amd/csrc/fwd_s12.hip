@@ -190,10 +190,10 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
     const f32x4 s2 = *reinterpret_cast<const f32x4 *>(lds + OFF_S2 + (8 * ls + 4 * hf) * 4);
     const f32x4 t2 = *reinterpret_cast<const f32x4 *>(lds + OFF_T2 + (8 * ls + 4 * hf) * 4);
     const uint2 u = *q;
-    const float v0 = fmaxf(fmaf(bf2f(u.x & 0xffffu), s2[0], t2[0]), 0.f);
-    const float v1 = fmaxf(fmaf(bf2f(u.x >> 16), s2[1], t2[1]), 0.f);
-    const float v2 = fmaxf(fmaf(bf2f(u.y & 0xffffu), s2[2], t2[2]), 0.f);
-    const float v3 = fmaxf(fmaf(bf2f(u.y >> 16), s2[3], t2[3]), 0.f);
+    const float v0 = relu(fmaf(bf2f(u.x & 0xffffu), s2[0], t2[0]));
+    const float v1 = relu(fmaf(bf2f(u.x >> 16), s2[1], t2[1]));
+    const float v2 = relu(fmaf(bf2f(u.y & 0xffffu), s2[2], t2[2]));
+    const float v3 = relu(fmaf(bf2f(u.y >> 16), s2[3], t2[3]));
     *q = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
   };
 
@@ -235,10 +235,10 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
       const int R = 16 * rt + l16;
       pk[rt][0] = pack2bf(acc1[rt][0] + sb[0], acc1[rt][1] + sb[1]);
       pk[rt][1] = pack2bf(acc1[rt][2] + sb[2], acc1[rt][3] + sb[3]);
-      const float x0 = fmaxf(fmaf(bf2f(pk[rt][0] & 0xffffu), sc1[0], tc1[0]), 0.f);
-      const float x1 = fmaxf(fmaf(bf2f(pk[rt][0] >> 16), sc1[1], tc1[1]), 0.f);
-      const float x2 = fmaxf(fmaf(bf2f(pk[rt][1] & 0xffffu), sc1[2], tc1[2]), 0.f);
-      const float x3 = fmaxf(fmaf(bf2f(pk[rt][1] >> 16), sc1[3], tc1[3]), 0.f);
+      const float x0 = relu(fmaf(bf2f(pk[rt][0] & 0xffffu), sc1[0], tc1[0]));
+      const float x1 = relu(fmaf(bf2f(pk[rt][0] >> 16), sc1[1], tc1[1]));
+      const float x2 = relu(fmaf(bf2f(pk[rt][1] & 0xffffu), sc1[2], tc1[2]));
+      const float x3 = relu(fmaf(bf2f(pk[rt][1] >> 16), sc1[3], tc1[3]));
       uint2 xo = make_uint2(pack2bf(x0, x1), pack2bf(x2, x3));
       if constexpr (MASK) {   // columns c0 .. c0 + 3: keep byte c0 / 8 of row R, bits 4 (g % 2) ..
         const uint32_t byte = *reinterpret_cast<const uint8_t *>(st + XB1 + R * MROW + 8 * w + 2 * ct + (g >> 1));
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
     const float Q = reinterpret_cast<const float *>(lds + OFF_SQ)[tid];
     const float d1 = S / n;
     *reinterpret_cast<float2 *>(a.stats + ((int64_t)chunk * N2 + tid) * 2) =
-        make_float2(reinterpret_cast<const float *>(lds + OFF_SH)[tid] + d1, fmaxf(Q - S * d1, 0.f));
+        make_float2(reinterpret_cast<const float *>(lds + OFF_SH)[tid] + d1, relu(Q - S * d1));
   }
 }
 

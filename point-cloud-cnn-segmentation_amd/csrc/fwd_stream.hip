@@ -314,7 +314,7 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
       float v[8];
       unpack_chunk(*q, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], ts[e], tt[e]), 0.f);
+      for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(v[e], ts[e], tt[e]));
       u32x4 out = pack_chunk(v);
       if constexpr (MASK) {
         const uint32_t byte = (uint8_t)st[F::XB + r * (K / 8) + tc];
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if constexpr (EPI == PCS_EPI_BNRELU) v[r] = fmaxf(fmaf(acc[ct][rt][r], es[ct][r], eb[ct][r]), 0.f);
+          if constexpr (EPI == PCS_EPI_BNRELU) v[r] = relu(fmaf(acc[ct][rt][r], es[ct][r], eb[ct][r]));
           else v[r] = acc[ct][rt][r] + eb[ct][r];
         }
         float d[4];   // the stored values
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(THREADS) void fwd_stream_kernel(pcs_gemm_args a, in
         if (n > 0.f) {
           const float d1 = s1[ct][r] / n;
           mean = sh[ct][r] + d1;
-          m2 = fmaxf(s2[ct][r] - s1[ct][r] * d1, 0.f);
+          m2 = relu(s2[ct][r] - s1[ct][r] * d1);
         }
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {

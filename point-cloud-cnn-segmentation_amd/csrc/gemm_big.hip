@@ -183,7 +183,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
       if constexpr (PRO == PCS_PRO_BNRELU) {
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
-          float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+          float x = relu(fmaf(v[e], c0[e], c1[e]));
           if constexpr (AMASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
           v[e] = x;
         }
@@ -310,10 +310,10 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
         const float4 t4 = *reinterpret_cast<const float4 *>(a.et + n0 + wn * 64 + j * 16 + lcol);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          acc[i][j][0] = fmaxf(fmaf(acc[i][j][0], s4.x, t4.x), 0.f);
-          acc[i][j][1] = fmaxf(fmaf(acc[i][j][1], s4.y, t4.y), 0.f);
-          acc[i][j][2] = fmaxf(fmaf(acc[i][j][2], s4.z, t4.z), 0.f);
-          acc[i][j][3] = fmaxf(fmaf(acc[i][j][3], s4.w, t4.w), 0.f);
+          acc[i][j][0] = relu(fmaf(acc[i][j][0], s4.x, t4.x));
+          acc[i][j][1] = relu(fmaf(acc[i][j][1], s4.y, t4.y));
+          acc[i][j][2] = relu(fmaf(acc[i][j][2], s4.z, t4.z));
+          acc[i][j][3] = relu(fmaf(acc[i][j][3], s4.w, t4.w));
         }
       }
     }
@@ -375,8 +375,8 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
               const int grow = (int)(row_base + rr);
 #pragma unroll
               for (int e = 0; e < EPC; ++e) {
-                if (v[e] > pmx[e]) { pmx[e] = v[e]; pmxi[e] = grow; }
-                if (v[e] < pmn[e]) { pmn[e] = v[e]; pmni[e] = grow; }
+                if (pool_max_step(v[e], pmx[e], pmxi[e])) { pmx[e] = v[e]; pmxi[e] = grow; }
+                if (pool_min_step(v[e], pmn[e], pmni[e])) { pmn[e] = v[e]; pmni[e] = grow; }
               }
             }
           }
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
             }
             const float nt = (float)valid, d1 = s1 / nt;
             float n = run_n, mean = run[c], m2 = run[BN + c];
-            chan_merge(n, mean, m2, nt, kc + d1, fmaxf(s2 - s1 * d1, 0.f));
+            chan_merge(n, mean, m2, nt, kc + d1, relu(s2 - s1 * d1));
             run[c] = mean; run[BN + c] = m2;
           } else {
             float s1 = run[c], s2 = run[BN + c];
@@ -509,8 +509,8 @@ __global__ __launch_bounds__(THREADS) void gemm_big_kernel(pcs_gemm_args a, int 
           for (int j = 0; j < RPP; ++j) {
             const float4 q = pp[j * BN + c];
             const int qi = __float_as_int(q.y), qj = __float_as_int(q.w);
-            if (q.x > mx || (q.x == mx && qi < mxi)) { mx = q.x; mxi = qi; }
-            if (q.z < mn || (q.z == mn && qj < mni)) { mn = q.z; mni = qj; }
+            if (pool_max_wins(q.x, qi, mx, mxi)) { mx = q.x; mxi = qi; }
+            if (pool_min_wins(q.z, qj, mn, mni)) { mn = q.z; mni = qj; }
           }
           run[2 * BN + c] = mx; run[3 * BN + c] = __int_as_float(mxi);
           run[4 * BN + c] = mn; run[5 * BN + c] = __int_as_float(mni);

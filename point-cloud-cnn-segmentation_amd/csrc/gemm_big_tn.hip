@@ -123,7 +123,7 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_
         for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
       } else if constexpr (DYMODE == PCS_PRO_BNRELU) {   // Gram: (beta, gamma) slots hold (s, t)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(y[e], cb[e], cg[e]), 0.f);
+        for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(y[e], cb[e], cg[e]));
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -148,7 +148,7 @@ PCS_DEV void tn_store(const pcs_wgrad_args &a, char *tA, const float *cf, int64_
     unpack_chunk(rx[i], w);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float x = fmaxf(fmaf(w[e], xs[e], xt[e]), 0.f);
+      float x = relu(fmaf(w[e], xs[e], xt[e]));
       if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.x_keep_scale : 0.f;
       w[e] = x;
     }

@@ -96,7 +96,7 @@ PCS_DEV float row_sum(float v) {
   v += dppf<0xB1>(v); v += dppf<0x4E>(v); v += dppf<0x141>(v);
   return v + dppf<0x140>(v);
 }
-PCS_DEV float row_max(float v) {
+PCS_DEV float row_max(float v) {   // maxNum: only for NaN-free operands
   v = fmaxf(v, dppf<0xB1>(v)); v = fmaxf(v, dppf<0x4E>(v)); v = fmaxf(v, dppf<0x141>(v));
   return fmaxf(v, dppf<0x140>(v));
 }
@@ -104,18 +104,21 @@ PCS_DEV float row_min(float v) {
   v = fminf(v, dppf<0xB1>(v)); v = fminf(v, dppf<0x4E>(v)); v = fminf(v, dppf<0x141>(v));
   return fminf(v, dppf<0x140>(v));
 }
-// v_max3_f32 / v_max_f32 as single instructions: on MFMA results hipcc otherwise inserts a
-// canonicalising v_max before each fmaxf (MI355X_MICROARCH 'Per-instruction cycle constants')
+// The pool's maxima propagate NaN, as torch.max does (P:114): v_maximum3_f32 (IEEE 754-2019
+// maximum, gfx950) rather than v_max3_f32, whose maxNum drops a NaN operand.  Single
+// instructions in asm: on MFMA results hipcc otherwise inserts a canonicalising v_max before
+// each fmaxf (MI355X_MICROARCH 'Per-instruction cycle constants')
 PCS_DEV float max3f(float a, float b, float c) {
   float r;
-  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm volatile("v_maximum3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 PCS_DEV float max2f(float a, float b) {
   float r;
-  asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  asm volatile("v_maximum3_f32 %0, %1, %2, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+PCS_DEV float maxp(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 // 0 / 1 per 16-bit half: bf16 x > 0 <=> x > 0 as a signed 16-bit integer (-0 = 0x8000 is not)
 PCS_DEV uint32_t pos01(uint32_t x, uint32_t one2) {
   uint32_t r;
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
           }
           const float nt = (float)nvw, d1 = S1 / nt;
           float n = run_n, mean = run[cme].x, m2 = run[cme].y;
-          chan_merge(n, mean, m2, nt, SH + d1, fmaxf(S2 - S1 * d1, 0.f));
+          chan_merge(n, mean, m2, nt, SH + d1, relu(S2 - S1 * d1));
           run[cme] = make_float2(mean, m2);
         }
         if (do_pool) {
@@ -522,8 +525,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                 const float t0 = max3f(acc[0][j][r], acc[1][j][r], acc[2][j][r]);
                 const float t1 = max3f(acc[3][j][r], acc[4][j][r], acc[5][j][r]);
                 const float t2 = max3f(acc[6][j][r], acc[7][j][r], t0);
-                // >=: an equal value may sit on an earlier row
-                beat |= (uint32_t)(max2f(t1, t2) >= cc[r]) << (4 * j + r);
+                // not <: an equal value may sit on an earlier row, and a NaN always beats
+                beat |= (uint32_t)!(max2f(t1, t2) < cc[r]) << (4 * j + r);
               }
             }
           } else {
@@ -539,8 +542,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
                 float mx = -__builtin_huge_valf();
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                  if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, gg[r] * acc[i][j][r]);
-                beat |= (uint32_t)(mx >= cc[r]) << (4 * j + r);
+                  if (tile_full || ((rowok >> i) & 1u)) mx = maxp(mx, gg[r] * acc[i][j][r]);
+                beat |= (uint32_t)!(mx < cc[r]) << (4 * j + r);
               }
             }
           }
@@ -562,7 +565,26 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
               float mx = -__builtin_huge_valf();
 #pragma unroll
               for (int i = 0; i < 8; ++i)
-                if (tile_full || ((rowok >> i) & 1u)) mx = fmaxf(mx, sg[r] * acc[i][j][r]);
+                if (tile_full || ((rowok >> i) & 1u)) mx = maxp(mx, sg[r] * acc[i][j][r]);
+              if (__builtin_amdgcn_ballot_w64(mx != mx) != 0) {   // uniform; rare (a diverged input)
+                // a NaN in this column of the tile: torch.max's pick is the first NaN row; it
+                // replaces a running number, or a running NaN on a later row (the tiles are not
+                // visited in row order).  The running NaN makes every later tile take this slow
+                // path, where a number never replaces it (mine >= NaN is false below).
+                int ix = 0x7fffffff;
+#pragma unroll
+                for (int i = 7; i >= 0; --i)
+                  if (((rowok >> i) & 1u) && acc[i][j][r] != acc[i][j][r]) ix = (int)(rb + wm * 128 + i * 16 + lr);
+                ix = row_mini(ix);
+                if (lr == j * 4 + r && (cur == cur || ix < curix)) {
+                  float4 u = q;
+                  if (sgl > 0.f) { u.x = __builtin_nanf(""); u.y = __int_as_float(ix); }
+                  else { u.z = __builtin_nanf(""); u.w = __int_as_float(ix); }
+                  runp[cme] = u;
+                  lcur[cme] = __builtin_nanf("");
+                }
+                continue;
+              }
               vx[r] = row_max(mx);
               if (lr == j * 4 + r) mine = vx[r];
             }
@@ -684,8 +706,8 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       const float4 q = runp[BN + tid];
       const int pi = __float_as_int(p.y), qi = __float_as_int(q.y);
       const int pj = __float_as_int(p.w), qj = __float_as_int(q.w);
-      if (q.x > p.x || (q.x == p.x && qi < pi)) { p.x = q.x; p.y = q.y; }
-      if (q.z < p.z || (q.z == p.z && qj < pj)) { p.z = q.z; p.w = q.w; }
+      if (pool_max_wins(q.x, qi, p.x, pi)) { p.x = q.x; p.y = q.y; }
+      if (pool_min_wins(q.z, qj, p.z, pj)) { p.z = q.z; p.w = q.w; }
       *reinterpret_cast<float4 *>(a.pool + o * 4) = p;
     }
   }
@@ -801,8 +823,11 @@ __global__ __launch_bounds__(256) void pool_rows_add_kernel(T *__restrict__ dz, 
       if (q >= p1) break;
       v = fmaf(cf[u], wv[u], v);
       if (q + 1 == p1 || srow_at(q + 1) != srow_at(q)) {   // last pair of this row: apply
-        const int64_t o = (int64_t)srow_at(q) * Ncols + n;
-        if (load_elem(Yp, o) > 0.f) {
+        const int64_t m = (int64_t)srow_at(q);
+        const int64_t o = m * Ncols + n;
+        // rows outside scene b are skipped (pcs_pool_finalize emits none; a caller's index array
+        // may): the row is a memory address here
+        if (m >= (int64_t)b * N && m < (int64_t)(b + 1) * N && load_elem(Yp, o) > 0.f) {
           const float d = load_elem(dz, o) + v;
           if constexpr (sizeof(T) == 2) dz[o] = (T)(pack2bf(d, 0.f) & 0xffffu);
           else dz[o] = d;

@@ -139,14 +139,14 @@ PCS_DEV void nt_store(const pcs_gemm_args &a, char *tA, const float *cf, int64_t
     if constexpr (PRO == PCS_PRO_BNRELU) {
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
-        float x = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+        float x = relu(fmaf(v[e], c0[e], c1[e]));
         if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.a_keep_scale : 0.f;
         v[e] = x;
       }
     } else if constexpr (PRO == PCS_PRO_CAT) {
       if (cat2) {
 #pragma unroll
-        for (int e = 0; e < EPC; ++e) v[e] = fmaxf(fmaf(v[e], c0[e], c1[e]), 0.f);
+        for (int e = 0; e < EPC; ++e) v[e] = relu(fmaf(v[e], c0[e], c1[e]));
       }
     } else if constexpr (PRO == PCS_PRO_BWD) {
       float y[EPC];
@@ -348,8 +348,8 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
           if constexpr (EPI == PCS_EPI_BNRELU) {   // this layer's BN + ReLU on the way out
             const float4 s4 = *reinterpret_cast<const float4 *>(a.es + n0 + n);
             const float4 t4 = *reinterpret_cast<const float4 *>(a.et + n0 + n);
-            v0 = fmaxf(fmaf(v0, s4.x, t4.x), 0.f); v1 = fmaxf(fmaf(v1, s4.y, t4.y), 0.f);
-            v2 = fmaxf(fmaf(v2, s4.z, t4.z), 0.f); v3 = fmaxf(fmaf(v3, s4.w, t4.w), 0.f);
+            v0 = relu(fmaf(v0, s4.x, t4.x)); v1 = relu(fmaf(v1, s4.y, t4.y));
+            v2 = relu(fmaf(v2, s4.z, t4.z)); v3 = relu(fmaf(v3, s4.w, t4.w));
           }
           char *dst = lds + m * CROW + n * SZ;
           if constexpr (SZ == 4) {
@@ -414,8 +414,8 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
               if constexpr (POOL) {
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) {
-                  if (v[e] > pmax[e]) { pmax[e] = v[e]; pmaxi[e] = (int)grow; }
-                  if (v[e] < pmin[e]) { pmin[e] = v[e]; pmini[e] = (int)grow; }
+                  if (pool_max_step(v[e], pmax[e], pmaxi[e])) { pmax[e] = v[e]; pmaxi[e] = (int)grow; }
+                  if (pool_min_step(v[e], pmin[e], pmini[e])) { pmin[e] = v[e]; pmini[e] = (int)grow; }
                 }
               }
             } else if constexpr (EPI == PCS_EPI_DGRAD) {
@@ -499,8 +499,8 @@ __global__ __launch_bounds__(THREADS, 2) void gemm_nt_kernel(pcs_gemm_args a, in
       for (int j = 0; j < RPP; ++j) {
         const float4 q = red[j * BN + c];
         const int qi = __float_as_int(q.y), qj = __float_as_int(q.w);
-        if (q.x > mx || (q.x == mx && qi < mxi)) { mx = q.x; mxi = qi; }
-        if (q.z < mn || (q.z == mn && qj < mni)) { mn = q.z; mni = qj; }
+        if (pool_max_wins(q.x, qi, mx, mxi)) { mx = q.x; mxi = qi; }
+        if (pool_min_wins(q.z, qj, mn, mni)) { mn = q.z; mni = qj; }
       }
       *reinterpret_cast<float4 *>(a.pool + (chunk_id * Ncols + n0 + c) * 4) =
           make_float4(mx, __int_as_float(mxi), mn, __int_as_float(mni));

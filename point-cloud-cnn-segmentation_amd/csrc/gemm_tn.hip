@@ -146,7 +146,7 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
         for (int e = 0; e < EPC; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
       } else if constexpr (DYMODE == PCS_PRO_BNRELU) {
 #pragma unroll
-        for (int e = 0; e < EPC; ++e) v[e] = fmaxf(fmaf(y[e], cb[e], cg[e]), 0.f);
+        for (int e = 0; e < EPC; ++e) v[e] = relu(fmaf(y[e], cb[e], cg[e]));
       } else {
         const int grow = (int)(scene * N + r);
 #pragma unroll
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(pcs_wgrad_args a, int
         unpack_chunk(rx[i], v);
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
-          float x = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+          float x = relu(fmaf(v[e], xs[e], xt[e]));
           if constexpr (MASK) x *= ((mk[i] >> e) & 1u) ? a.x_keep_scale : 0.f;
           v[e] = x;
         }

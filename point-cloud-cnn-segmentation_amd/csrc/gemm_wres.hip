@@ -196,7 +196,7 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
       float v[8];
       unpack_chunk(*p, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], ts[e], tt[e]), 0.f);
+      for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(v[e], ts[e], tt[e]));
       *p = pack_chunk(v);
     }
   };
@@ -309,8 +309,8 @@ __global__ __launch_bounds__(THREADS) void wres_bnrelu_kernel(pcs_gemm_args a, i
         for (int h = 0; h < 2; ++h) {
           const f32x2 x = {acc[i][j][2 * h], acc[i][j][2 * h + 1]};
           v2[h] = __builtin_elementwise_fma(x, es2[j][h], et2[j][h]);
-          v2[h][0] = fmaxf(v2[h][0], 0.f);
-          v2[h][1] = fmaxf(v2[h][1], 0.f);
+          v2[h][0] = relu(v2[h][0]);
+          v2[h][1] = relu(v2[h][1]);
         }
         f32x2 d[2];   // the stored values, decoded
         if constexpr (C8) {

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(THREADS) void gram_wgrad_kernel(
 #pragma unroll
       for (int j = 0; j < RR; ++j) {
         const int k = k0 + tx * RR + j;
-        o[j] = fmaf(w, fmaxf(fmaf(load_elem(Y, m * Cin + k), s[k], t[k]), 0.f), o[j]);
+        o[j] = fmaf(w, relu(fmaf(load_elem(Y, m * Cin + k), s[k], t[k])), o[j]);
       }
     }
 #pragma unroll
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void bn_stats_gram_kernel(const float *__restr
     __syncthreads();
   }
   if (tid < B) {
-    const double mean = sh[0][0] / n, m2 = sh[0][1] > 0.0 ? sh[0][1] : 0.0;
+    const double mean = sh[0][0] / n, m2 = sh[0][1] < 0.0 ? 0.0 : sh[0][1];   // clamp; a NaN stays
     *reinterpret_cast<float2 *>(stats + ((int64_t)tid * C + c) * 2) = make_float2((float)mean, (float)(m2 / B));
   }
 }
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void bn_stats_scenes_kernel(const double *__re
     const double mean = s / n;
     for (int b = 0; b < B; ++b) between += nb * (d[b] / nb - mean) * (d[b] / nb - mean);
     double m2b = (q - s * s / n - between) / B;
-    m2b = m2b > 0.0 ? m2b : 0.0;
+    m2b = m2b < 0.0 ? 0.0 : m2b;   // clamp the rounding; a NaN (a diverged a5) stays NaN, as torch's var
     for (int b = 0; b < B; ++b)
       *reinterpret_cast<float2 *>(stats + ((int64_t)b * C + c) * 2) = make_float2((float)(d[b] / nb), (float)m2b);
   }

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(THREADS, (C <= 2 ? HS_WPS : 1)) void head_stream_ke
       float y[8], av[8];
       unpack_chunk(yv, y);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) av[e] = fmaxf(fmaf(y[e], s[e], t[e]), 0.f);
+      for (int e = 0; e < 8; ++e) av[e] = relu(fmaf(y[e], s[e], t[e]));
       float lg[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) {

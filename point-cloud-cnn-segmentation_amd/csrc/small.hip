@@ -291,16 +291,19 @@ __global__ void pool_finalize_kernel(const float *pool, int64_t B, int64_t N, in
   for (int j = 0; j < cps; ++j) {
     const float4 q = *reinterpret_cast<const float4 *>(pool + (((int64_t)b * cps + j) * C + c) * 4);
     const int qi = __float_as_int(q.y), qj = __float_as_int(q.w);
-    if (q.x > mx || (q.x == mx && qi < mxi)) { mx = q.x; mxi = qi; }
-    if (q.z < mn || (q.z == mn && qj < mni)) { mn = q.z; mni = qj; }
+    if (pool_max_wins(q.x, qi, mx, mxi)) { mx = q.x; mxi = qi; }
+    if (pool_min_wins(q.z, qj, mn, mni)) { mn = q.z; mni = qj; }
   }
   const float sc = s[c];
   float y; int idx;
   if (sc > 0.f) { y = mx; idx = mxi; }
   else if (sc < 0.f) { y = mn; idx = mni; }
-  else { y = mx; idx = (int)(b * N); }  // constant z: torch's first index
+  else { y = mx; idx = (int)(b * N); }  // constant z (or a NaN scale): torch's first index
+  // never hand on the "no candidate" sentinel (or any row outside the scene) as a row index:
+  // the backward's pool kernels read the row it names
+  if ((int64_t)idx < b * N || (int64_t)idx >= (b + 1) * N) idx = (int)(b * N);
   const float z = fmaf(y, sc, t[c]);
-  g[i] = fmaxf(z, 0.f);
+  g[i] = (z > 0.f || z != z) ? z : 0.f;   // ReLU that keeps a NaN, as torch.relu does
   am[i] = idx;
   ysel[i] = y;
 }
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(THREADS) void head_kernel(pcs_head_args a, int tile
         if constexpr (MODE != PCS_HEAD_FWD) { load_vec<EPC>(a.mean, ch0 + c, mu); load_vec<EPC>(a.rstd, ch0 + c, rs); }
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
-          av[r * HEAD_LD + ch0 + c + e] = fmaxf(fmaf(y[e], s[e], t[e]), 0.f);
+          av[r * HEAD_LD + ch0 + c + e] = relu(fmaf(y[e], s[e], t[e]));
           if constexpr (MODE != PCS_HEAD_FWD) xh[r * HEAD_LD + ch0 + c + e] = (y[e] - mu[e]) * rs[e];
         }
       }
@@ -661,7 +664,7 @@ __global__ __launch_bounds__(THREADS) void head_wide_kernel(pcs_head_args a, int
         if constexpr (MODE != PCS_HEAD_FWD) { load_vec<EPC>(a.mean, ch0 + c, mu); load_vec<EPC>(a.rstd, ch0 + c, rs); }
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
-          ar[c + e] = fmaxf(fmaf(y[e], sv[e], tv[e]), 0.f);
+          ar[c + e] = relu(fmaf(y[e], sv[e], tv[e]));
           if constexpr (MODE != PCS_HEAD_FWD) xr[c + e] = (y[e] - mu[e]) * rs[e];
         }
       }
@@ -880,7 +883,7 @@ __global__ __launch_bounds__(THREADS) void head_small_kernel(pcs_head_args a, in
         for (int e = 0; e < EPC; ++e) y[k * EPC + e] = tmp[e];
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) av[e] = fmaxf(fmaf(y[e], s[e], t[e]), 0.f);
+      for (int e = 0; e < 8; ++e) av[e] = relu(fmaf(y[e], s[e], t[e]));
       float lg[C];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -1532,7 +1535,7 @@ __global__ __launch_bounds__(256) void bnrelu_bf16_kernel(const float *__restric
     float hi[8], lo[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float a = fmaxf(fmaf(yv[e], s[k + e], t[k + e]), 0.f);
+      const float a = relu(fmaf(yv[e], s[k + e], t[k + e]));
       hi[e] = bf2f(pack2bf(a, 0.f) & 0xffffu);
       lo[e] = a - hi[e];   // exact in fp32
     }

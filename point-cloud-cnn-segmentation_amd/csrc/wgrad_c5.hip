@@ -166,7 +166,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
     float v[8];
     unpack_chunk(*reinterpret_cast<const u32x4 *>(lds + sidx * STAGE + o_yx), v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = relu(fmaf(v[e], xs[e], xt[e]));
     u32x4 out = pack_chunk(v);
     if (xrr >= rem) out = mk_u32x4(0, 0, 0, 0);
     *reinterpret_cast<u32x4 *>(lds + OFF_X + (s & 1) * XB + o_xw) = out;
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(THREADS) void gram128_kernel(pcs_wgrad_args a, int6
       float v[8];
       unpack_chunk(*pc, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = r < rem ? fmaxf(fmaf(v[e], xs[e], xt[e]), 0.f) : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = r < rem ? relu(fmaf(v[e], xs[e], xt[e])) : 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += v[e];   // column sums in fp32 (as the tiled kernel)
       *pc = pack_chunk(v);

@@ -198,7 +198,9 @@ class Engine:
         # capture (a dict) receives the operands and outputs of global_feat's input gradient and
         # conv5's backward kernels; perturb = {"dz5": (c0, c1, scale)} scales columns c0..c1 of
         # dz5 after global_feat's input gradient (a simulated kernel error, the negative
-        # control).  Never set on the product path.
+        # control); {"a5": (rows, cols, value)} writes value into a5[rows, cols] after conv5's
+        # forward (a diverged activation: NaN through the max-pool, tests/test_gpu_pool_nan.py).
+        # Never set on the product path.
         self.capture = None
         self.perturb = None
         # bf16 / fp8 training forward: seg_conv1's local half and seg_conv2 in one streaming pass
@@ -509,6 +511,12 @@ class Engine:
             self._gemm(B, N, 128, 1024, L.PRO_BNRELU, L.EPI_BNRELU, sv.ys["conv4"], wc["conv5"][0], a5,
                        es=c5.scale, et=c5.shift, stats=sv.a5_colsum, tag="fwd:conv5",
                        extra_flags=L.FLAG_C_FP8 if self.fp8 else 0, **bnrelu("bn4"))
+        if self.perturb is not None and "a5" in self.perturb:
+            rows, cols, value = self.perturb["a5"]
+            if self.fp8:   # e4m3 bytes: 0x7f is its NaN
+                a5[rows, cols] = 0x7f if value != value else int(torch.tensor(value).to(torch.float8_e4m3fn).view(torch.uint8))
+            else:
+                a5[rows, cols] = value
         sv.ys["a5"] = a5
 
         # global_feat (P:113-114): a5 W^T with max-pool partials (and, on the fp32 / generic

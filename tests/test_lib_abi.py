@@ -30,7 +30,11 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
     lib.pcs_abi_version.restype = ct.c_int
-    assert lib.pcs_abi_version() == 1
+    hdr = open(os.path.join(REPO, "include", "pcs.h")).read()
+    want = int(re.search(r"#define PCS_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.pcs_abi_version() == want == 2
+    import pcs_amd._lib as L
+    assert L.ABI_VERSION == want
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libpcs.so not built")
