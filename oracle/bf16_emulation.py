@@ -312,8 +312,10 @@ _TRUNK = ("conv1", "conv2", "conv3", "conv4")
 def eval_sites(trunk="bf16"):
     """bf16 rounding sites of the HIP eval forward.  Names: W<l> (GEMM weight), Y<l> (stored
     pre-BN output), A<l> (relu(bn(Y_l)) as the next GEMM's operand; "Aconv2s" is seg_conv1's
-    copy of a2), "a5" (stored relu(bn5(y5))).  trunk="fp32": conv1..conv4 stored and computed
-    in fp32, seg_conv1 fed a bf16 a2, conv5 fed a 16-bit split of a4 (treated as exact)."""
+    copy of a2), "a5" (stored relu(bn5(y5))), "Asplit4" (conv5's operand as the 16-bit split
+    [hi | lo] of pcs_bnrelu_bf16: hi = bf16(a4), lo = bf16(a4 - hi), so conv5 sees hi + lo).
+    trunk="fp32": conv1..conv4 stored and computed in fp32, seg_conv1 fed a bf16 a2, conv5 fed
+    the split of a4."""
     s = {"a5", "Wglobal_feat", "Wconv5", "Aconv2s"}
     for l in EVAL_LAYERS:
         s |= {f"Y{l}", f"A{l}"}
@@ -322,14 +324,19 @@ def eval_sites(trunk="bf16"):
     s.discard("Aseg_conv3")           # the head reads bn_seg3's output in fp32
     if trunk == "fp32":
         s -= {f"{k}{l}" for l in _TRUNK for k in "YAW"}
+        s.add("Asplit4")
     return frozenset(s)
 
 
-def eval_logits(sd, x, sites, fp8=False):
+def eval_logits(sd, x, sites, fp8=False, sums="f32"):
     """float32 eval forward with the bf16 rounding ``sites`` (eval_sites); logits [B, N, C].
     Stored pre-BN outputs omit the conv bias as the HIP path's do (seg_conv1's per-scene bias
     centred over the scenes).  fp8=True: a5 in e4m3 and global_feat's weight as e4m3 rows with
-    one power-of-two scale each (the compute dtype "fp8"), whatever ``sites`` holds for them."""
+    one power-of-two scale each (the compute dtype "fp8"), whatever ``sites`` holds for them.
+    relu(bn(y)) = max(fma(y, s, t), 0) with one rounding, as the kernels' fmaf.
+    ``sums``: "f32" sums every GEMM in float32 (BLAS order), "f64" in float64 rounded once to
+    float32 -- another valid order of the same arithmetic, whose distance from the "f32" result
+    is the rounding-order noise floor a device-vs-emulation comparison cannot go below."""
     def R(a, site):
         if fp8 and site == "a5":
             return round_e4m3(a)
@@ -348,12 +355,17 @@ def eval_logits(sd, x, sites, fp8=False):
         sc = g / np.sqrt(sd[f"{bn}.running_var"].astype(np.float64) + BN_EPS)
         return sc.astype(F32), (sd[f"{bn}.bias"].astype(np.float64) - (rm - off) * sc).astype(F32)
 
+    def mm(A, Wt):   # A @ Wt.T
+        if sums == "f64":
+            return (np.asarray(A, np.float64) @ np.asarray(Wt, np.float64).T).astype(F32)
+        return A @ Wt.T
+
     def layer(A, conv, bn, Wt):
-        Y = R(A @ Wt.T, f"Y{conv}")
+        Y = R(mm(A, Wt), f"Y{conv}")
         return Y, *coefs(bn, sd[f"{conv}.bias"].astype(np.float64))
 
-    def relu_bn(Y, s, t):
-        return np.maximum(Y * s + t, F32(0))
+    def relu_bn(Y, s, t):   # fma: the product and sum of two float32 are exact in float64
+        return np.maximum((Y.astype(np.float64) * s + t).astype(F32), F32(0))
 
     Y, s, t = layer(X, "conv1", "bn1", W["conv1"])
     Y, s, t = layer(R(relu_bn(Y, s, t), "Aconv1"), "conv2", "bn2", R(W["conv2"], "Wconv2"))
@@ -361,18 +373,21 @@ def eval_logits(sd, x, sites, fp8=False):
     Y, s, t = layer(R(A2, "Aconv2"), "conv3", "bn3", R(W["conv3"], "Wconv3"))
     Y, s, t = layer(R(relu_bn(Y, s, t), "Aconv3"), "conv4", "bn4", R(W["conv4"], "Wconv4"))
     A4 = R(relu_bn(Y, s, t), "Aconv4")
+    if "Asplit4" in sites:   # engine.Engine.forward's bridge("conv4", "bn4", 128, True)
+        hi = round_bf16(A4)
+        A4 = hi + round_bf16(A4 - hi)   # exact in fp32 (16 significant bits)
     s5, t5 = coefs("bn5", sd["conv5.bias"].astype(np.float64))
-    a5 = R(relu_bn(A4 @ R(W["conv5"], "Wconv5").T, s5, t5), "a5")          # fp32 accumulators
+    a5 = R(relu_bn(mm(A4, R(W["conv5"], "Wconv5")), s5, t5), "a5")          # fp32 accumulators
     sg, tg = coefs("bn_global", sd["global_feat.bias"].astype(np.float64))
-    zg = ((a5 @ R(W["global_feat"], "Wglobal_feat").T) * sg + tg).reshape(B, N, -1)
+    zg = (mm(a5, R(W["global_feat"], "Wglobal_feat")).astype(np.float64) * sg + tg).astype(F32).reshape(B, N, -1)
     g = np.maximum(zg.max(axis=1), 0).astype(np.float64)                   # P:114
     del zg
     sb = g @ W["seg_conv1"][:, 64:].T.astype(np.float64) + sd["seg_conv1.bias"]   # [B, 512]
     soff = sb.mean(axis=0)
     a2s = R(A2, "Aconv2" if "Aconv2" in sites else "Aconv2s")
-    Ys1 = R((a2s @ R(W["seg_conv1"][:, :64], "Wseg_conv1").T).reshape(B, N, -1)
+    Ys1 = R(mm(a2s, R(W["seg_conv1"][:, :64], "Wseg_conv1")).reshape(B, N, -1)
             + (sb - soff)[:, None, :].astype(F32), "Yseg_conv1").reshape(M, -1)
     s, t = coefs("bn_seg1", soff)
     Y, s, t = layer(R(relu_bn(Ys1, s, t), "Aseg_conv1"), "seg_conv2", "bn_seg2", R(W["seg_conv2"], "Wseg_conv2"))
     Y, s, t = layer(R(relu_bn(Y, s, t), "Aseg_conv2"), "seg_conv3", "bn_seg3", R(W["seg_conv3"], "Wseg_conv3"))
-    return (relu_bn(Y, s, t) @ W["seg_conv4"].T + sd["seg_conv4.bias"].astype(F32)).reshape(B, N, -1)
+    return (mm(relu_bn(Y, s, t), W["seg_conv4"]) + sd["seg_conv4.bias"].astype(F32)).reshape(B, N, -1)

@@ -64,5 +64,10 @@ def test_eval_logits_without_rounding_is_the_reference_eval():
     # the site sets: the fp32 trunk drops exactly conv1..conv4's sites, bf16 storage is lossy
     b, f = emu.eval_sites("bf16"), emu.eval_sites("fp32")
     assert b - f == {f"{k}conv{i}" for k in "YA" for i in (1, 2, 3, 4)} | {"Wconv2", "Wconv3", "Wconv4"}
+    assert f - b == {"Asplit4"}   # conv5 fed pcs_bnrelu_bf16's [hi | lo] of a4
+    a = np.random.default_rng(0).standard_normal(4096).astype(np.float32)
+    hi = emu.round_bf16(a)
+    lo = emu.round_bf16(a - hi)
+    assert np.all(np.abs(a - (hi + lo)) <= np.abs(a) * 2.0 ** -16) and np.any(hi + lo != a)
     lb = emu.eval_logits(sd, pts, b)
     assert 0 < np.abs(lb - l64).max() <= 0.1 * scale

@@ -128,8 +128,16 @@ def test_storage_eval_is_its_emulation(trained, dtype):
     fp8 a5 / global_feat weight rows for "fp8") and as shipped (eval_trunk="fp32") against the
     numpy restatement of exactly that storage (oracle/bf16_emulation.eval_logits): their logit
     margins agree to within 1/8 of what the storage itself costs, so a mIoU miss of the
-    storage path is a property of its number format, not of a kernel.  The misses are
-    reported, not bounded (fp8: ~100 flipped points either way, see the print)."""
+    storage path is a property of its number format, not of a kernel.  Each path is held to
+    its OWN format cost (the shipped fp32 trunk's is ~7x smaller than the all-bf16 one's); the
+    emulation restates the shipped path's 16-bit split of a4 ("Asplit4") and the kernels'
+    single-rounding fmaf, so the typical point agrees to fp32 rounding (p50 <= 1e-6; r06:
+    2.4e-7 on both trunks).  The p99.9 tail is set by bf16 rounding-boundary flips that depend
+    on the order of fp32 sums, and the emulation in float64 sums ("f64", another valid order)
+    sits 7.7e-3 from the float32-sum emulation on the fp32 trunk, above that trunk's cost/8
+    (4.8e-3): no implementation can be held below that floor, so the tail bound is the larger
+    of cost/8 and 1.5x the floor (device 5.5e-3, r06).  The misses are reported, not bounded
+    (fp8: ~100 flipped points either way, see the print)."""
     from bf16_emulation import eval_logits, eval_sites
     C, sd, pts, lab, logits = _val_case(trained)
     pred = logits.argmax(-1).reshape(-1)
@@ -137,15 +145,18 @@ def test_storage_eval_is_its_emulation(trained, dtype):
     ref = _sk_miou(pred, lab.reshape(-1))
     p = lambda a: float(np.quantile(a, 0.999))   # noqa: E731
     fp8 = dtype == "fp8"
-    cost = None
     for trunk in ("bf16", "fp32"):
         got, dpred, dlog = _device_eval(sd, pts, lab, C, dtype, eval_trunk=trunk)
         emu = eval_logits(sd, pts, eval_sites(trunk), fp8=fp8)
+        emu64 = eval_logits(sd, pts, eval_sites(trunk), fp8=fp8, sums="f64")
         err = np.abs(_margin(emu) - _margin(logits))[v]        # what the storage costs
-        cost = p(err) if cost is None else cost                # yardstick: the all-storage path
+        cost = p(err)                                          # yardstick: this path's own format
         diff = np.abs(_margin(dlog) - _margin(emu))[v]         # device vs its restatement
+        noise = np.abs(_margin(emu64) - _margin(emu))[v]       # the restatement in another sum order
+        q = lambda a: f"p50 {np.median(a):.2e} p99 {np.quantile(a, 0.99):.2e} p99.9 {p(a):.2e}"   # noqa: E731
         print(f"{dtype} eval_trunk={trunk}: mIoU {got:.6f} vs oracle {ref:.6f} (diff {got - ref:+.2e}, "
               f"emulation {_sk_miou(emu.argmax(-1).reshape(-1), lab.reshape(-1)) - ref:+.2e}), flipped "
-              f"{int(((dpred != pred) & v).sum())}; margin error p99.9: format {p(err):.3e}, device vs "
-              f"emulation {p(diff):.3e} (p50 {np.median(diff):.2e})")
-        assert p(diff) <= cost / 8
+              f"{int(((dpred != pred) & v).sum())}; margin error: format {q(err)}; device vs emulation "
+              f"{q(diff)}; emulation f64 sums vs f32 sums {q(noise)}; bound {max(cost / 8, 1.5 * p(noise)):.3e}")
+        assert np.median(diff) <= 1e-6
+        assert p(diff) <= max(cost / 8, 1.5 * p(noise))
