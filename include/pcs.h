@@ -45,9 +45,7 @@ enum {
                            W's rows (pcs_sign_rows) and bias by sign(es), so the pool keeps the
                            plain column max of acc (no multiply); es still names the sign.
                            Needs pool and es, no statistics (they would be of the signed y)  */
-  PCS_FLAG_SEG8 = 64    /* pcs_dgrad_wgrad_bn of seg_conv2 / seg_conv3: the 8-wave 128-column
-                           kernel (fused_seg.hip) instead of the 4-wave 256-column one
-                           (fused_seg4.hip), for A/B timing and cross-checks                 */
+  /* 64: unused since ABI 2 (was the 8-wave seg_conv2/3 backward, an A/B-only kernel)        */
 };
 
 /* prologue applied to an operand element A[m,k] as it is staged into LDS */
@@ -366,6 +364,12 @@ int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float
  * (the training step draws beside the Gram of a5) occupies few wave slots for longer. */
 int pcs_dropout_bits_bounded(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
                              uint8_t *bits, int32_t max_workgroups, pcs_stream_t stream);
+/* Opt-in for parity runs: the same keep rule with every element's 16-bit uniform from its own
+ * two Philox bytes (i.i.d. Bernoulli, as nn.Dropout; pcs_dropout_bits lets elements 2k and
+ * 2k + 1 share a byte pair: joint keep 0.490463 against 0.49 at p = 0.3), one call per 8
+ * elements (twice pcs_dropout_bits's calls).  A different stream of bits from the same seed. */
+int pcs_dropout_bits_independent(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                                 uint8_t *bits, pcs_stream_t stream);
 
 /*
  * Gram of the BN+ReLU activations a = relu(Y * s + t) (Y [M, C] scene-major rows), or of Y

@@ -47,7 +47,6 @@ FLAG_NO_GLDS = 2
 FLAG_AW_FP8 = 4
 FLAG_C_FP8 = 8
 FLAG_POOL_SIGNED_W = 16
-FLAG_SEG8 = 64
 
 
 class WgradArgs(ct.Structure):
@@ -128,6 +127,7 @@ SIGNATURES = [
     ("pcs_ce_weight_sum", ct.c_int, [_vp, _i64, _vp, _i32, _vp, _vp, _vp]),
     ("pcs_dropout_bits", ct.c_int, [ct.c_uint64, ct.c_uint64, _i64, _i32, _f, _vp, _vp]),
     ("pcs_dropout_bits_bounded", ct.c_int, [ct.c_uint64, ct.c_uint64, _i64, _i32, _f, _vp, _i32, _vp]),
+    ("pcs_dropout_bits_independent", ct.c_int, [ct.c_uint64, ct.c_uint64, _i64, _i32, _f, _vp, _vp]),
     ("pcs_reduce_partials", ct.c_int, [_vp, _i64, _i64, _f, _vp, _i64, _i64, _vp]),
     ("pcs_reduce_partials_grouped", ct.c_int, [_vp, _i64, _i64, _i64, _f, _vp, _vp]),
     ("pcs_cast_weight", ct.c_int, [_vp, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),

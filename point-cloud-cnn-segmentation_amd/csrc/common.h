@@ -199,13 +199,10 @@ bool pcs_gemm_wres_applicable(const pcs_gemm_args &a);
 int pcs_gemm_wres_launch(const pcs_gemm_args &g, int64_t rows_per_chunk, hipStream_t s);
 int pcs_gemm_glds_launch(const pcs_gemm_args &a, int tiles_per_scene, int tiles_per_chunk,
                          hipStream_t s);
-// fused seg_conv2 / seg_conv3 input + weight gradient (fused_seg.hip)
+// fused seg_conv2 / seg_conv3 input + weight gradient (fused_seg4.hip)
 bool pcs_seg4_applicable(const pcs_gemm_args &a);
 int64_t pcs_seg4_geometry(pcs_gemm_args *a);
 int pcs_seg4_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);
-bool pcs_seg_bwd_applicable(const pcs_gemm_args &a);
-int64_t pcs_seg_bwd_geometry(pcs_gemm_args *a);
-int pcs_seg_bwd_launch(const pcs_gemm_args &a, float *wpart, hipStream_t s);
 // conv5's folded input gradient as one LDS-DMA stream (fused_c5.hip)
 bool pcs_c5_dgrad_class(const pcs_gemm_args &a);
 bool pcs_c5_dgrad_applicable(const pcs_gemm_args &a);

@@ -1604,11 +1604,16 @@ extern "C" int pcs_sparse_conv_pairs(const int32_t *pair_in, const int32_t *pair
 }
 
 namespace {
-// weight-gradient slices: slice_len pairs each (at least 4 k-steps, about 2048 slices in all),
-// ceil(count / slice_len) per tap (at least one, so every tap's partial is written)
-void pair_wgrad_slices(PairTaps *pt) {
+// weight-gradient slices: slice_len pairs each (at least 4 k-steps), ceil(count / slice_len) per
+// tap (at least one, so every tap's partial is written), about 2048 workgroups over the slices
+// and the 64 x 64 channel tiles together (as sparse_wgrad_splits): each slice holds a full
+// Cout x Cin fp32 partial, so the workspace stays near 2048 tiles' worth (34 MB at 64 -> 64, 40 MB
+// at 256 -> 256, where a fixed 2048 slices took 544 MB) instead of growing with the channel product
+void pair_wgrad_slices(PairTaps *pt, int Cin, int Cout) {
   const int64_t P = pt->tap_off[pt->taps];
-  int64_t len = (P + 2047) / 2048;
+  const int64_t tiles = (int64_t)(Cout / 64) * (Cin / 64);
+  const int64_t target = (2048 + tiles - 1) / tiles;
+  int64_t len = (P + target - 1) / target;
   len = (len < 4 * WV ? 4 * WV : len + WV - 1) / WV * WV;
   pt->slice_len = len;
   int64_t g = 0;
@@ -1629,7 +1634,7 @@ extern "C" int64_t pcs_sparse_conv_wgrad_pairs_workspace(const int64_t *tap_off,
   if (why) return pcs_set_einval("pcs_sparse_conv_wgrad_pairs_workspace", why);
   if (M < 0 || Cin <= 0 || Cout <= 0 || Cin % 64 != 0 || Cout % 64 != 0)
     return pcs_set_einval("pcs_sparse_conv_wgrad_pairs_workspace", "bad arguments (Cin, Cout multiples of 64)");
-  pair_wgrad_slices(&pt);
+  pair_wgrad_slices(&pt, Cin, Cout);
   const int64_t spb = sparse_wgrad_splits(M, 1, 64, Cout);
   return ((int64_t)pt.slice_off[taps] * Cout * Cin + spb * Cout) * 4;
 }
@@ -1644,7 +1649,7 @@ extern "C" int pcs_sparse_conv_wgrad_pairs(const int32_t *pair_in, const int32_t
     return pcs_set_einval("pcs_sparse_conv_wgrad_pairs", "pairs, X, dY, dW and a workspace of pcs_sparse_conv_wgrad_pairs_workspace bytes");
   PairTaps pt;
   pair_taps(tap_off, taps, &pt);
-  pair_wgrad_slices(&pt);
+  pair_wgrad_slices(&pt, Cin, Cout);
   const int64_t ns = pt.slice_off[taps], wlen = (int64_t)Cout * taps * Cin;
   float *ws = static_cast<float *>(workspace), *wsb = ws + ns * Cout * Cin;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

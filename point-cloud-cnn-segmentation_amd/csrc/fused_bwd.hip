@@ -748,7 +748,7 @@ int launch_bn(const pcs_gemm_args &a, float *wpart, int64_t rps, hipStream_t s) 
 // 4.96 vs 4.73 ms, seg_conv2 12.8 vs 12.6 ms: 2 TB/s, latency-bound at one workgroup per
 // CU with the dy slab staged once per column block), so they stay on the pair.
 struct BnShape { int cout, cin, cb, ms; };
-// (seg_conv2 and seg_conv3 now go to the LDS-DMA stream of fused_seg.hip instead)
+// (seg_conv2 and seg_conv3 go to the LDS-DMA stream of fused_seg4.hip instead)
 constexpr BnShape kBnShapes[] = {{64, 64, 64, 64}, {128, 64, 64, 64}};
 
 const BnShape *bn_shape(int K, int Ncols) {
@@ -763,10 +763,6 @@ extern "C" int64_t pcs_dgrad_wgrad_bn_workspace(pcs_gemm_args *a) {
   if (!a || a->num_scenes <= 0 || a->scene_rows <= 0) return pcs_set_einval("pcs_dgrad_wgrad_bn_workspace", "bad geometry");
   if (pcs_seg4_applicable(*a)) {   // seg_conv2 / seg_conv3: one wave per SIMD (fused_seg4.hip)
     pcs_seg4_geometry(a);
-    return (int64_t)a->num_scenes * a->chunks_per_scene * a->K * a->Ncols * 4;
-  }
-  if (pcs_seg_bwd_applicable(*a)) {   // seg_conv2 / seg_conv3: 8-wave LDS-DMA stream (fused_seg.hip)
-    pcs_seg_bwd_geometry(a);
     return (int64_t)a->num_scenes * a->chunks_per_scene * a->K * a->Ncols * 4;
   }
   const BnShape *sh = bn_shape(a->K, a->Ncols);
@@ -798,9 +794,8 @@ extern "C" int pcs_dgrad_wgrad_bn(const pcs_gemm_args *ap, float *partial, float
     return pcs_set_einval("pcs_dgrad_wgrad_bn", "missing operand (A, A2, pa, pb, pc, W, C, Yp, es, et, emean, "
                                                 "erstd, stats)");
   if (a.scene_rows * a.num_scenes >= (int64_t)1 << 31) return pcs_set_einval("pcs_dgrad_wgrad_bn", "M must be < 2^31");
-  if (pcs_seg4_applicable(a) || pcs_seg_bwd_applicable(a)) {
-    const int rc = pcs_seg4_applicable(a) ? pcs_seg4_launch(a, partial, reinterpret_cast<hipStream_t>(stream))
-                                          : pcs_seg_bwd_launch(a, partial, reinterpret_cast<hipStream_t>(stream));
+  if (pcs_seg4_applicable(a)) {
+    const int rc = pcs_seg4_launch(a, partial, reinterpret_cast<hipStream_t>(stream));
     if (rc) return rc;
     const int nslab = (int)(a.num_scenes * a.chunks_per_scene);
     return pcs_reduce_partials(partial, nslab, (int64_t)a.K * a.Ncols, 1.0f, dW, ldw ? ldw : a.Ncols, a.Ncols, stream);

@@ -14,7 +14,7 @@
 //   this step's 72 MFMAs per wave run;
 // * relu(bn4(y4)) is formed once per element, in LDS, one step ahead; the epilogue reads the raw
 //   y4 of the step for bn4's ReLU mask and S2.
-// dz5 rows carry the chunk permutation ftr of fused_seg.hip (conflict-free fragment reads), y4
+// dz5 rows carry the chunk permutation ftr of the r03 fused_seg.hip, now in git history (conflict-free fragment reads), y4
 // rows the (row & 15) permutation (conflict-free epilogue reads), both put on the DMA source.
 #include "common.h"
 
@@ -35,7 +35,6 @@ constexpr int BYTES = OFF_CF + 7 * NC * 4;
 static_assert(BYTES <= 160 * 1024, "LDS budget");
 constexpr int KS1 = K1 / 32, KS2 = K2 / 32;  // MFMA k-steps
 constexpr int DZP = DZB / 1024;             // 64 pieces: 8 per wave
-constexpr int VM_STEP = DZP / 8 + 1;        // + one y4 piece per wave
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 

@@ -1,12 +1,12 @@
 // Fused input + weight gradient of seg_conv2 (512 -> 256) and seg_conv3 (256 -> 128) at one
-// wave per SIMD (autograd of P:125-127 at P:254), the same operation as fused_seg.hip:
+// wave per SIMD (autograd of P:125-127 at P:254), the same operation as the r03 8-wave kernel (fused_seg.hip, removed in r06):
 //
 //   dy   = alpha * dZ + beta + gamma * Y                 ([M, COUT], bn_seg{2,3} backward)
 //   g    = dy . W                                        ([M, CIN])
 //   dz'  = (es * Yp + et > 0) * keep * ks * g             (stored; S1 = sum dz', S2 = sum dz' Yp)
 //   dW  += dy^T . x,   x = relu(es * Yp + et) * keep * ks ([COUT, CIN])
 //
-// fused_seg.hip's 8-wave workgroups own 128 CIN columns each, so the four (seg_conv2) or two
+// that kernel's 8-wave workgroups own 128 CIN columns each, so the four (seg_conv2) or two
 // (seg_conv3) workgroups of a row slice all recompute the slice's dy, and every wave reads the
 // whole dy slab for its 16 dgrad columns: vector-ALU- and LDS-bound at 3.2 TB/s.  Here four
 // waves (one per SIMD, 512 registers each) own 256 columns:
@@ -551,10 +551,10 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
 }  // namespace
 
 // Shapes served: (Cout, Cin) = K x Ncols in {256 x 512 (seg_conv2), 128 x 256 (seg_conv3)}, bf16,
-// PRO_BWD / EPI_DGRAD, no addend; PCS_FLAG_SEG8 keeps them on fused_seg.hip (A/B timing).
+// PRO_BWD / EPI_DGRAD, no addend.
 int64_t pcs_seg4_geometry(pcs_gemm_args *a);
 bool pcs_seg4_applicable(const pcs_gemm_args &a) {
-  if (!(a.dtype == PCS_BF16 && !(a.flags & (PCS_FLAG_GENERIC | PCS_FLAG_SEG8)) && !a.addend &&
+  if (!(a.dtype == PCS_BF16 && !(a.flags & PCS_FLAG_GENERIC) && !a.addend &&
         ((a.K == 256 && a.Ncols == 512) || (a.K == 128 && a.Ncols == 256))))
     return false;
   // the buffer-store range and the per-lane row offsets are 32-bit: a slice's rows (Ncols

@@ -15,7 +15,7 @@
 //
 // A workgroup (8 waves) owns a scene-aligned row slice.  Per 32-row step:
 // * LDS-DMA (dword pieces, counted waits) brings y2 (4 KB) and the step's keep bits (2 KB)
-//   through a 4-stage ring; bn2 + ReLU is applied once per element, in place;
+//   through a 3-stage ring (NST); bn2 + ReLU is applied once per element, in place;
 // * stage 1: wave w computes Y1 columns 64 w .. 64 w + 63 (W1 rows from LDS, 16 MFMAs), its
 //   epilogue adds the scene bias, rounds, stores Y1 (16-B stores after v_permlane16_swap) and
 //   writes x = bn_seg1 / ReLU / dropout of the ROUNDED values (the backward recomputes x from the
@@ -452,7 +452,8 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
   }
 }
 
-// bn_seg1's batch statistics from the Gram of a2 (one workgroup per 256 output channels): the
+// bn_seg1's batch statistics from the Gram of a2 (16 output channels per workgroup; each of the
+// C / 16 workgroups rebuilds the 64 x 64 fp64 Cw, a few microseconds, below): the
 // centred within-scene Gram Cw = G - sum_b S_b S_b^T / N (fp64, in LDS), then per channel
 // M2w = w Cw w^T and the per-scene means S_b w / N + sbias[b]; written as per-scene partials
 // (mean_b, M2w / B) whose Chan merge in pcs_bn_fwd_finalize adds the between-scene term

@@ -1075,6 +1075,38 @@ __global__ void dropout_bits_kernel(uint64_t seed, uint64_t offset, int64_t nbyt
   }
 }
 
+// The independent form (pcs_dropout_bits_independent, opt-in for parity runs): every element
+// draws its own 16-bit uniform from its own two Philox bytes, as nn.Dropout's i.i.d. Bernoulli
+// draws (P:96), at twice the Philox calls: a thread's word (32 elements) takes four calls,
+// counters 4 w .. 4 w + 3, and call q's word i half h is element 8 q + 2 i + h.
+__global__ void dropout_bits_indep_kernel(uint64_t seed, uint64_t offset, int64_t nbytes, uint32_t thr,
+                                          uint8_t *bits) {
+  const uint32_t thr2 = thr | (thr << 16);
+  u16x2 one2 = {1, 1};
+  asm volatile("" : "+v"(one2));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; j0 < nbytes; j0 += stride) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t k = j0 + q;   // = 4 w + q
+      uint32_t ctr[4] = {(uint32_t)k, (uint32_t)((uint64_t)k >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
+      philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t d = drop2(ctr[i], thr2, one2);   // bits 0 and 16: halves 0 and 1
+        word |= ((d & 1u) | ((d >> 15) & 2u)) << (8 * q + 2 * i);
+      }
+    }
+    word = ~word;
+    if (j0 + 4 <= nbytes && ((reinterpret_cast<uintptr_t>(bits) & 3) == 0)) {
+      *reinterpret_cast<uint32_t *>(bits + j0) = word;
+    } else {
+      for (int q = 0; q < 4 && j0 + q < nbytes; ++q) bits[j0 + q] = (uint8_t)(word >> (8 * q));
+    }
+  }
+}
+
 // out = scale * sum over slabs.  TPO threads share one 4-float output (slabs k = sub,
 // sub + TPO, ...) and combine with a fixed xor-shuffle tree: deterministic, and wide enough
 // for the thousand-slab reductions of the small layers' weight gradients.
@@ -1425,6 +1457,23 @@ extern "C" int pcs_dropout_bits_bounded(uint64_t seed, uint64_t offset, int64_t 
 extern "C" int pcs_dropout_bits(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
                                 uint8_t *bits, pcs_stream_t stream) {
   return pcs_dropout_bits_bounded(seed, offset, M, C, p, bits, 0, stream);
+}
+
+extern "C" int pcs_dropout_bits_independent(uint64_t seed, uint64_t offset, int64_t M, int32_t C, float p,
+                                            uint8_t *bits, pcs_stream_t stream) {
+  if (!bits || C % 8 != 0 || p < 0.f || p >= 1.f)
+    return pcs_set_einval("pcs_dropout_bits_independent", "bad arguments");
+  const int64_t nbytes = M * (C / 8);
+  if (nbytes <= 0) return 0;
+  const uint32_t thr = (uint32_t)(p * 65536.0f + 0.5f);
+  if (thr > 65535u) {
+    const hipError_t e = hipMemsetAsync(bits, 0, (size_t)nbytes, reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : pcs_set_error(e, "pcs_dropout_bits_independent");
+  }
+  hipLaunchKernelGGL(dropout_bits_indep_kernel, dim3((unsigned)blocks_for((nbytes + 3) / 4, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), seed, offset, nbytes, thr, bits);
+  PCS_CHECK_LAUNCH();
+  return 0;
 }
 
 namespace {

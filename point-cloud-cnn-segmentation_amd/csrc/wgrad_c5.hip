@@ -3,7 +3,7 @@
 //
 // The register-staged pcs_wgrad kernel (gemm_tn.hip, 128 x 128 tiles, 64-row steps, a barrier
 // and a register round trip per step) read dz5 and y4 at 4.5-4.9 TB/s (3.95-4.26 ms at cfg2).
-// Here the fused seg backward's weight-gradient half (fused_seg.hip) without its input gradient:
+// Here the fused seg backward's weight-gradient half (the r03 fused_seg.hip, now in git history) without its input gradient:
 // * a workgroup (8 waves) owns NB = 256 dz5 columns and all 128 a4 channels of a scene-aligned
 //   row slice: the [256 x 128] fp32 partial of R stays in registers (64 per lane), the slice's
 //   partial goes out once, summed over the slices by pcs_reduce_partials (fixed order);
@@ -11,7 +11,7 @@
 //   waits; relu(bn4(y4)) formed once per element into a double-buffered x tile (the 4 column
 //   blocks of a slice repeat this 128-wide transform, on one XCD, through L2);
 // * MFMA operands by ds_read_b64_tr_b16 of the row-major dz5 and x tiles (k = rows), the
-//   layouts (slot permutations, padded x rows) of fused_seg.hip: bank-conflict free.
+//   layouts (slot permutations, padded x rows) of the r03 fused_seg.hip, now in git history: bank-conflict free.
 #include "common.h"
 
 namespace {
@@ -73,7 +73,7 @@ PCS_DEV void barrier_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
-// slot permutations (fused_seg.hip): dz5 rows chunk c at c ^ ftr(r); y4 rows at c ^ (r & 15);
+// slot permutations (the r03 fused_seg.hip, now in git history): dz5 rows chunk c at c ^ ftr(r); y4 rows at c ^ (r & 15);
 // x rows permuted (bits 2 <-> 3) and padded
 PCS_DEV int ftr(int row) { return ((row & 3) << 1) | (row & 8); }
 PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(THREADS) void wgrad_c5_kernel(pcs_wgrad_args a, int
     }
   };
 
-  // transposed-read offsets (fused_seg.hip's weight-gradient half): dz5 columns 16 (2 wid + ob) +
+  // transposed-read offsets (the r03 fused_seg.hip, now in git history's weight-gradient half): dz5 columns 16 (2 wid + ob) +
   // 4 p of rows 8 g + q and 8 g + 4 + q; x columns 16 u + 4 p of the same rows
   const int g = lane >> 4, l16 = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
   const int tr0 = 8 * g + q, tr1 = 8 * g + 4 + q;

@@ -210,6 +210,10 @@ class Engine:
         # bf16 training step: draw the dropout keep bits beside the Gram of a5 (bounded grid, in
         # its idle VALU issue) instead of at the start of the forward with a full grid
         self.draw_beside_gram = True
+        # "paired" (default): pcs_dropout_bits (elements 2k, 2k + 1 share a byte pair of their
+        # uniforms); "independent": pcs_dropout_bits_independent, i.i.d. keep bits as nn.Dropout
+        # (P:96) at twice the Philox calls, drawn at the start of the forward (parity runs)
+        self.dropout_draw = "paired"
         L.load()
 
     def _launch(self, tag, name, *args):
@@ -392,8 +396,12 @@ class Engine:
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 ss = L.stream_ptr()
-                L.call("pcs_dropout_bits_bounded", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), max_wg, ss)
-                L.call("pcs_dropout_bits_bounded", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), max_wg, ss)
+                if self.dropout_draw == "independent":
+                    L.call("pcs_dropout_bits_independent", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), ss)
+                    L.call("pcs_dropout_bits_independent", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), ss)
+                else:
+                    L.call("pcs_dropout_bits_bounded", seed, 0, M, 512, DROPOUT_P, L.ptr(m1), max_wg, ss)
+                    L.call("pcs_dropout_bits_bounded", seed, 1, M, 256, DROPOUT_P, L.ptr(m2), max_wg, ss)
                 sv.mask_ready = torch.cuda.Event()
                 sv.mask_ready.record(side)
             m1.record_stream(side)
@@ -403,7 +411,8 @@ class Engine:
         # SIMD, with three 256-thread workgroups per CU (24 VGPRs a wave: they fit beside it and
         # use its idle VALU issue; 0.77 ms per call against 0.83 with two, the Gram and the step
         # unchanged, tools/draw_wg.py); otherwise at the start of the forward with a full grid
-        draw_beside_gram = train and masks is None and self._raw_gram() and not self.fp8 and self.draw_beside_gram
+        draw_beside_gram = (train and masks is None and self._raw_gram() and not self.fp8 and self.draw_beside_gram
+                            and self.dropout_draw != "independent")
         if train and masks is None and not draw_beside_gram:
             draw_masks()
         sv.wc = wc = self.cast_weights(P)

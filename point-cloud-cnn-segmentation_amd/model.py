@@ -92,9 +92,15 @@ class PointNetSegmentation(nn.Module):
     with trained weights, bf16 storage there moves mIoU by more than the north star's 1e-3
     (DESIGN.md section 4).  ``"bf16"`` keeps the eval forward on the training step's bf16
     storage.  Training always uses the compute dtype throughout.
+
+    ``dropout_draw``: ``"paired"`` (default, the bench path: elements 2k and 2k + 1 share a
+    byte pair of their 16-bit uniforms, each keep bit exactly Bernoulli(0.7), pair correlation
+    0.0022) or ``"independent"`` (i.i.d. keep bits as nn.Dropout, P:96, for parity runs; twice
+    the Philox work).
     """
 
-    def __init__(self, num_classes, input_dim=4, *, compute_dtype: str = "fp32", eval_trunk: str = "fp32"):
+    def __init__(self, num_classes, input_dim=4, *, compute_dtype: str = "fp32", eval_trunk: str = "fp32",
+                 dropout_draw: str = "paired"):
         super().__init__()
         # Point-wise MLPs for feature extraction (P:70-74)
         self.conv1 = nn.Conv1d(input_dim, 64, 1)
@@ -121,6 +127,9 @@ class PointNetSegmentation(nn.Module):
         self.input_dim = input_dim
         self.compute_dtype = compute_dtype
         self.eval_trunk = eval_trunk
+        if dropout_draw not in ("paired", "independent"):
+            raise ValueError(f"dropout_draw must be 'paired' or 'independent', got {dropout_draw!r}")
+        self.dropout_draw = dropout_draw
         check_dims(num_classes, input_dim)   # fail at construction, not at the first forward
         # created lazily (it loads libpcs.so); it holds no per-call state (only a geometry
         # cache), so DataParallel replicas may share it
@@ -133,6 +142,7 @@ class PointNetSegmentation(nn.Module):
         if (self._eng is None or self._eng.dtype != self.compute_dtype
                 or self._eng.eval_trunk != self.eval_trunk):
             self._eng = Engine(self.num_classes, self.compute_dtype, self.input_dim, self.eval_trunk)
+        self._eng.dropout_draw = self.dropout_draw
         return self._eng
 
     def _params(self):

@@ -29,9 +29,12 @@ TAPS = 27
 # forward / input gradient through the pair lists (gather-GEMM-reduce) when the map has at most
 # this many occupied taps per voxel; above it the tile-gather kernel, whose zero rows are then few
 # and which keeps no per-pair products in memory.  The weight gradient takes the pair lists at
-# every occupancy (PAIR_WGRAD).  profiles/bench_sparse_pairs_r05.txt
+# every occupancy (PAIR_WGRAD) for layers of at most PAIR_WGRAD_MAX_CH2 = Cin x Cout channel
+# pairs (64 -> 64, the shape profiles/bench_sparse_pairs_r05.txt measured); wider layers keep
+# the tile-gather weight gradient until the pair form is measured there
 PAIR_TAPS_MAX = 3.0
 PAIR_WGRAD = True
+PAIR_WGRAD_MAX_CH2 = 64 * 64
 
 
 @dataclass
@@ -161,7 +164,8 @@ class _SubMConvFn(torch.autograd.Function):
             L.call("pcs_sparse_conv", L.ptr(nbr), V, TAPS, L.ptr(xk), cin_k, L.ptr(wb), cout_k,
                    L.ptr(bk) if bk is not None else None, L.ptr(y), ydt, 0, L.stream_ptr(x.device))
         ctx.save_for_backward(xk, wb, nbr)
-        ctx.sv, ctx.pairs, ctx.wpairs = sv, pairs, PAIR_WGRAD and V > 0
+        ctx.sv, ctx.pairs = sv, pairs
+        ctx.wpairs = PAIR_WGRAD and V > 0 and cin_k * cout_k <= PAIR_WGRAD_MAX_CH2
         ctx.cfg = (bias is not None, cin, cout)
         return y if cout_k == cout else y[:, :cout].contiguous()
 

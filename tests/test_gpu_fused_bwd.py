@@ -126,15 +126,6 @@ def test_dgrad_wgrad_bn_matches_torch(cout, cin, variant, B, N):
     _check_bn(cout, cin, variant, B, N, 0)
 
 
-@pytest.mark.parametrize("cout,cin,variant,B,N", [
-    (256, 512, "mask", 2, 4096 + 33), (256, 512, "plain", 1, 70), (128, 256, "mask", 3, 1000),
-    (128, 256, "plain", 2, 64 * 40 + 5)])
-def test_seg_bwd_8wave_matches_torch(cout, cin, variant, B, N):
-    """The same checks on the 8-wave 128-column kernel (csrc/fused_seg.hip, PCS_FLAG_SEG8)."""
-    import pcs_amd._lib as L
-    _check_bn(cout, cin, variant, B, N, L.FLAG_SEG8)
-
-
 def _check_bn(cout, cin, variant, B, N, flags):
     import pcs_amd._lib as L
     g = torch.Generator(device="cpu").manual_seed(cout * 31 + cin + N)

@@ -224,6 +224,47 @@ def test_dropout_bits_statistics_and_determinism():
     assert bool((e == 0).all())
 
 
+def test_dropout_bits_independent_draw():
+    """pcs_dropout_bits_independent (opt-in, PointNetSegmentation(dropout_draw="independent")):
+    i.i.d. keep bits as nn.Dropout (P:96): marginal 0.7, adjacent elements' joint keep 0.49
+    (the paired default gives 0.490463), deterministic per (seed, offset); the model's
+    training forward draws exactly these bits."""
+    import pcs_amd._lib as L
+    from pcs_amd.model import PointNetSegmentation
+    M, C = 65536, 512
+    a, b, c, pr = (torch.empty(M, C // 8, dtype=torch.uint8, device=DEV) for _ in range(4))
+    s = L.stream_ptr()
+    L.call("pcs_dropout_bits_independent", 123, 0, M, C, 0.3, L.ptr(a), s)
+    L.call("pcs_dropout_bits_independent", 123, 0, M, C, 0.3, L.ptr(b), s)
+    L.call("pcs_dropout_bits_independent", 123, 1, M, C, 0.3, L.ptr(c), s)
+    L.call("pcs_dropout_bits", 123, 0, M, C, 0.3, L.ptr(pr), s)
+    assert torch.equal(a, b) and not torch.equal(a, c) and not torch.equal(a, pr)
+    bits = np.unpackbits(a.cpu().numpy(), axis=1, bitorder="little")
+    keep = 1.0 - int(0.3 * 65536.0 + 0.5) / 65536.0
+    assert abs(bits.mean() - keep) < 2e-3
+    assert np.abs(bits.mean(0) - keep).max() < 0.02
+    for lag in (1, 2, 8, 16):   # adjacent, same Philox word, same call, next call
+        both = float((bits[:, :-lag] & bits[:, lag:]).mean())
+        assert abs(both - keep * keep) < 2e-3, (lag, both)
+    e = torch.zeros(257, C // 8, dtype=torch.uint8, device=DEV)
+    L.call("pcs_dropout_bits_independent", 123, 0, 257, C, 0.0, L.ptr(e), s)
+    assert bool((e == 255).all())
+    # the model option routes the training forward's draw here (both dropouts, offsets 0 / 1)
+    m = PointNetSegmentation(2, compute_dtype="bf16", dropout_draw="independent").to(DEV).train()
+    B, N = 2, 1000
+    x = torch.randn(B, N, 4, device=DEV)
+    eng = m._engine()
+    sv = eng.forward(m._param_dict(), m._buffer_dict(), x, train=True, seed=77)
+    torch.cuda.synchronize()
+    for off, (K, got) in enumerate(((512, sv.masks[0]), (256, sv.masks[1]))):
+        ref = torch.empty(B * N, K // 8, dtype=torch.uint8, device=DEV)
+        L.call("pcs_dropout_bits_independent", 77, off, B * N, K, 0.3, L.ptr(ref), s)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+    with pytest.raises(ValueError):
+        PointNetSegmentation(2, dropout_draw="iid")
+
+
 def test_train_mode_random_dropout_runs_and_differs():
     sd = orc.init_params(2, 5)
     pts, _, _ = __import__("pcs_amd.data", fromlist=["x"]).synthetic_batch(3, [256, 256], 2)

@@ -104,13 +104,12 @@ def test_conv3d_argument_validation_without_gpu():
 
 
 def test_seg_backward_geometry_without_gpu():
-    """seg_conv2 / seg_conv3 backward (pcs_dgrad_wgrad_bn): the default four-wave kernel's
-    slices (fused_seg4.hip: 16-row steps, one 256-column workgroup per CU) and the 8-wave
-    kernel's under PCS_FLAG_SEG8 (fused_seg.hip: 32-row steps, 128-column workgroups)."""
+    """seg_conv2 / seg_conv3 backward (pcs_dgrad_wgrad_bn): the four-wave kernel's slices
+    (fused_seg4.hip: 16-row steps, one 256-column workgroup per CU)."""
     import pcs_amd._lib as L
     lib = L.load()
     for cout, cin in ((256, 512), (128, 256)):
-        for flags, nblk in ((0, cin // 256), (L.FLAG_SEG8, cin // 128)):
+        for flags, nblk in ((0, cin // 256),):
             a = L.GemmArgs(num_scenes=4, scene_rows=128 ** 3, K=cout, Ncols=cin, dtype=L.BF16,
                            prologue=L.PRO_BWD, epilogue=L.EPI_DGRAD, flags=flags)
             nbytes = lib.pcs_dgrad_wgrad_bn_workspace(ct.byref(a))
@@ -132,6 +131,13 @@ def test_sparse_pairs_argument_validation_without_gpu():
     ta = ct.addressof(good)
     assert lib.pcs_sparse_conv_wgrad_pairs_workspace(ta, 27, 100, 64, 64) > 0
     assert lib.pcs_sparse_conv_wgrad_pairs_workspace(ta, 27, 100, 32, 64) == -1000   # Cin % 64
+    # slices are divided over the 64 x 64 channel tiles: 27 taps x 2^20 pairs keep the workspace
+    # near 2048 tiles' partials at every width (a fixed 2048 slices took 544 MB at 256 -> 256)
+    V = 1 << 20
+    full = (ct.c_int64 * 28)(*[t * V for t in range(28)])
+    for ch, lim in ((64, 40 << 20), (128, 48 << 20), (256, 48 << 20)):
+        nb = lib.pcs_sparse_conv_wgrad_pairs_workspace(ct.addressof(full), 27, V, ch, ch)
+        assert 0 < nb <= lim, (ch, nb)
     bad = (ct.c_int64 * 28)(*([0] * 13 + [100] * 14 + [50]))   # decreasing
     assert lib.pcs_sparse_conv_wgrad_pairs_workspace(ct.addressof(bad), 27, 100, 64, 64) == -1000
     start = (ct.c_int64 * 28)(*([5] + [100] * 27))             # not starting at 0
