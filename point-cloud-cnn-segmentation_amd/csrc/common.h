@@ -140,6 +140,17 @@ PCS_DEV void chan_merge(float &n, float &mean, float &m2, float nb, float meanb,
 // diverged run would report a finite loss where the reference reports NaN
 PCS_DEV float relu(float x) { return __builtin_elementwise_maximum(x, 0.f); }
 
+// x where the mask m is all ones, +0 where it is 0 (m = a sign-extended keep bit, v_bfe_i32):
+// one v_and_b32.  In asm so that it stays a bitwise AND: hipcc rewrites x & sext(bit) into
+// v_cmp + v_cndmask, whose SGPR hand-off also costs wait states (s_nop) -- 3-4 issue slots per
+// element instead of 1 (r06: 128 v_cmp + 159 v_cndmask + 121 s_nop in the global_feat input
+// gradient's epilogue per tile and wave)
+PCS_DEV float and_mask(float x, uint32_t m) {
+  float r;
+  asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(m));
+  return r;
+}
+
 // Max-pool candidate order of torch.max / torch.min over a dim (P:114): a NaN beats every
 // number (torch propagates it), and among equal values -- or among NaNs -- the smaller row
 // wins (the first one in row order).  (v, vi) is the candidate, (cur, ci) the running pick.

@@ -297,18 +297,25 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   // row tid/2, 32 columns; bf16 x > 0 <=> sign clear and magnitude nonzero) in a per-tile-
   // parity LDS bitmap [256 rows][8 words] that the epilogue reads: the work is spread evenly
   // over all waves instead of stalling one wave column at the phase barriers.
-  // region: 0 = A-lo (phase 1), 1 = A-hi (phase 3); thread: region row tid/4, 16 columns
-  auto extract_mask = [&](int buf, int region, int kq, int par) {
+  // region: 0 = A-lo (phase 1), 1 = A-hi (phase 4); thread: region row tid/4, 16 columns.  (r06:
+  // reading A-hi with phase 3's fragment reads and forming the bits of each region one phase
+  // later made the input gradient 0.4 ms slower, profiles/ab_r06/; they stay in one phase.)
+  auto mask_load = [&](int buf, int region, u32x4 &v0, u32x4 &v1) {
+    const int q = tid >> 2, h = tid & 3;
+    const char *base = lds + buf * KBUF + region * REG + q * 128;
+    v0 = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2) * 16);
+    v1 = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + 1) * 16);
+  };
+  auto mask_bits = [&](int region, int kq, int par, const u32x4 &v0, const u32x4 &v1) {
     const int q = tid >> 2, h = tid & 3;
     const int t = a_row(region, q);
-    const char *base = lds + buf * KBUF + region * REG + q * 128;
     uint32_t w = 0;
     if constexpr (FP8) {   // 32 columns (bytes) per thread: x > 0 <=> sign clear, 7 low bits nonzero
       // word d (columns 4d .. 4d + 3) flags each byte in its bit 7; shifting word d right by
       // 7 - d and OR-ing the 8 words puts column 4d + k at bit 8k + d (the epilogue's order)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
+        const u32x4 &v = c ? v1 : v0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           const uint32_t x = v[d];
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // and the odd ones in bits 4-7 (the epilogue reads that order)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(base + swz(q, h * 2 + c) * 16);
+      const u32x4 &v = c ? v1 : v0;
       const uint32_t tb = pos01(v[0], 0x10001u) | (pos01(v[1], 0x10001u) << 1) | (pos01(v[2], 0x10001u) << 2) |
                          (pos01(v[3], 0x10001u) << 3);
       w |= ((tb | (tb >> 12)) & 0xffu) << (8 * c);
@@ -392,9 +399,14 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     const int kb = w2 ? 0 : ka + 1;
     const int pb = w2 ? pnext(pa) : pa;
     // phase 1: (rows lo, cols lo); restage A-hi of K-tile qs+1
+    const bool xmask = MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ;   // uniform
+    u32x4 mv0, mv1;
     read_a(buf, 0);
     read_b(buf, 2, 0);
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 0, kt - kq0, tcur & 1);
+    if (xmask) {
+      mask_load(buf, 0, mv0, mv1);
+      mask_bits(0, kt - kq0, tcur & 1, mv0, mv1);
+    }
     issue(qs + 1, pa, ka, 1);
     // every counted wait assumes the five regions issued after the one it retires are in
     // flight; on a chunk's last two K-tiles issue() skips loads, so the counts shrink to the
@@ -430,7 +442,10 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // phase 4: (hi, hi); restage B-hi of K-tile qs+2.  A-hi's mask bits are taken here, not
     // in phase 3: B-lo's fragments are dead by now, which keeps the extraction's registers
     // out of the accumulators' way (A-hi(qs) is restaged only in phase 1 of qs+1)
-    if (MODE == MODE_DGRAD && (unsigned)(kt - kq0) < NKQ) extract_mask(buf, 1, kt - kq0, tcur & 1);
+    if (xmask) {
+      mask_load(buf, 1, mv0, mv1);
+      mask_bits(1, kt - kq0, tcur & 1, mv0, mv1);
+    }
     issue(qs + 2, pb, kb, 3);
     // retires A-lo(qs+1), B-lo(qs+1): newer are B-hi(qs+1), A-hi(qs+1) and three of qs+2
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();
@@ -441,6 +456,12 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     barrier_raw();
 
     if (kt != nks - 1) continue;
+
+    // The halves meet for the epilogue (r06): staggered, half 1's epilogue would start only when
+    // half 0's was done and its next MFMA phase began, so the two ran one after the other with
+    // the SIMD's matrix pipe idle; aligned they run together and hide each other's latencies.
+    // The stagger comes back after it (half 1 takes the extra barrier).
+    if (wm == 0) barrier_raw();
 
     // ===================== epilogue of row tile tcur (rows of tile pcur) =====================
     const int64_t rb = row0 + (int64_t)pcur * BM;
@@ -646,7 +667,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, FP8 ? 8 * r : (r >> 1) + 4 * (r & 1), 1);
-            v[r] = __uint_as_float(__float_as_uint(acc[i][j][r]) & keep);
+            v[r] = and_mask(acc[i][j][r], keep);
             s1[j][r] += v[r];
           }
           pk[j][0] = pack2bf(v[0], v[1]);
@@ -682,6 +703,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     }
 
     bias_init(acc);
+    if (wm == 1) barrier_raw();   // the stagger again (see the epilogue's first barrier)
   }
 
   if (wm == 0) barrier_raw();   // re-align the halves (matching the stagger above)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # same-box step A/B of the in-tree build against abtest/<VAR>/libpcs.so (timing only; only builds
 # whose outputs stay valid indices -- a variant that skips the pool epilogue faults the step),
-# alternating processes, three rounds:  VAR=name [GREP=kernel-rows] bash tools/ab_lib_step.sh
+# alternating processes, three rounds:  VAR="name [name ...]" [GREP=kernel-rows] bash tools/ab_lib_step.sh
 set -e
 for i in 1 2 3; do
   for v in head $VAR; do
