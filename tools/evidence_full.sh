@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-5 evidence at one build (repo root, GPU box): GPU suite, smoke, the bf16 bench line with
+# Round evidence at one build (repo root, GPU box): GPU suite, smoke, the bf16 bench line with
 # its per-kernel table and rocprof/PMC passes, then the fp8 (with profile), fp32 and cfg3 lines.
-# Usage: tools/evidence_r05.sh <tag>
+# Usage: tools/evidence_full.sh <tag>
 set -e
 TAG=${1:-r05b}
 mkdir -p gpurun_out
