@@ -385,6 +385,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
   // fragment reads before arriving at a phase's first barrier, which keeps the restaging of
   // a region one phase after its last read safe across the stagger.
   if (wm == 1) barrier_raw();
+  // (No s_setprio around the MFMA sections: with the epilogues aligned, raising the MFMA
+  // sections' priority over the partner's preparation measured 0.1-0.2 ms slower per GEMM, and
+  // raising the preparation's instead no better; profiles/ab_r06/priority.txt)
 
   // (row tile, K-tile) of qs and of qs + 1; pcur / pa: their row tiles in visiting order
   int kt = 0, tcur = 0, ta = 0, ka = 0, pcur = 0, pa = 0;
@@ -415,9 +418,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     if (qs + 1 < total) wait_vm<10>(); else wait_vm<2>();
     wait_lgkm0();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
     mfma_quad(0, 0);
-    __builtin_amdgcn_s_setprio(0);
     barrier_raw();
     // phase 2: (lo, hi); restage A-lo of K-tile qs+2
     read_b(buf, 3, 2);
@@ -426,18 +427,14 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<8>(); else wait_vm<0>();
     wait_lgkm0();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
     mfma_quad(0, 2);
-    __builtin_amdgcn_s_setprio(0);
     barrier_raw();
     // phase 3: (hi, lo); restage B-lo of K-tile qs+2
     read_a(buf, 1);
     issue(qs + 2, pb, kb, 2);
     wait_lgkm0();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
     mfma_quad(4, 0);
-    __builtin_amdgcn_s_setprio(0);
     barrier_raw();
     // phase 4: (hi, hi); restage B-hi of K-tile qs+2.  A-hi's mask bits are taken here, not
     // in phase 3: B-lo's fragments are dead by now, which keeps the extraction's registers
@@ -450,9 +447,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
     // retires A-lo(qs+1), B-lo(qs+1): newer are B-hi(qs+1), A-hi(qs+1) and three of qs+2
     if (qs + 2 < total) wait_vm<10>(); else if (qs + 1 < total) wait_vm<4>(); else wait_vm<0>();
     barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
     mfma_quad(4, 2);
-    __builtin_amdgcn_s_setprio(0);
     barrier_raw();
 
     if (kt != nks - 1) continue;
