@@ -32,19 +32,22 @@ __device__ unsigned long long g_stamps[4096 * 8][16];"""),
 # per phase: prep | open barrier | mfma | close barrier
 for ph, quad in enumerate(("mfma_quad(0, 0);", "mfma_quad(0, 2);", "mfma_quad(4, 0);", "mfma_quad(4, 2);")):
     EDITS.append(("""    barrier_raw();
-    __builtin_amdgcn_s_setprio(1);
     """ + quad + """
-    __builtin_amdgcn_s_setprio(0);
     barrier_raw();""", "    " + st(ph) + """
     barrier_raw();
     """ + st(4 + ph) + """
-    __builtin_amdgcn_s_setprio(1);
     """ + quad + """
-    __builtin_amdgcn_s_setprio(0);
     """ + st(8) + """
     barrier_raw();
     """ + st(9)))
 EDITS += [
+    ("""    u32x4 mv0, mv1;
+    read_a(buf, 0);
+    read_b(buf, 2, 0);""", """    u32x4 mv0, mv1;
+    """ + st(14) + """
+    read_a(buf, 0);
+    """ + st(15) + """
+    read_b(buf, 2, 0);"""),
     ("""    if (xmask) {
       mask_load(buf, 0, mv0, mv1);
       mask_bits(0, kt - kq0, tcur & 1, mv0, mv1);
