@@ -201,3 +201,79 @@ def test_conv3_forward_gram_of_its_operand(B, N):
     serr = float((S - Sref).abs().max() / Sref.abs().max())
     print(f"B={B} N={N}: Gram rel err {err:.2e}, column sums {serr:.2e}")
     assert err < 1e-4 and serr < 1e-4
+
+
+@pytest.mark.parametrize("offset", [0.0, 2.0, 8.0])
+def test_bn_seg1_gram_stats_offset_operand(offset):
+    """bn_seg1's variance from the Gram route (uncentred: w (G - S S^T / N) w^T) on conv3's own
+    fp32 Gram records, with a2 = relu(s2 y2 + t2) pushed away from zero by `offset` so that the
+    channels of y1 = a2 W1^T have |mean| / std up to ~50: against fp64 statistics of the same
+    y1, and against the direct per-chunk (mean, M2) of seg_conv1's forward GEMM (shifted sums,
+    Chan merge).  The Gram route's variance error must stay within the direct route's error
+    plus 2e-4 relative (a quarter of a bf16 half-ulp in the BN scale), at every ratio."""
+    import pcs_amd._lib as L
+    lib = L.load()
+    B, N = 2, 2 ** 17
+    M = B * N
+    g = torch.Generator(device="cpu").manual_seed(11)
+    y2 = torch.randn(M, 64, generator=g).to(torch.bfloat16).to(DEV)
+    s2 = (torch.rand(64, generator=g) * 0.3 + 0.1).to(DEV)
+    t2 = (torch.randn(64, generator=g) * 0.1 + offset).to(DEV)
+    W3 = (torch.randn(64, 64, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    W1 = (torch.randn(512, 64, generator=g) * 0.05 + 0.03).to(torch.bfloat16).to(DEV)
+    sbias = (torch.randn(B, 512, generator=g) * 0.2).to(DEV)
+    # conv3's forward with the gram record, reduced as the engine does (engine._seg12)
+    a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=64, dtype=L.BF16, prologue=L.PRO_BNRELU,
+                   epilogue=L.EPI_FWD, chunks_per_scene=0, A=y2.data_ptr(), W=W3.data_ptr(),
+                   C=torch.empty(M, 64, dtype=torch.bfloat16, device=DEV).data_ptr(),
+                   pa=s2.data_ptr(), pb=t2.data_ptr(), a_keep_scale=1.0, c_keep_scale=1.0)
+    lib.pcs_gemm_geometry(ct.byref(a))
+    cps = a.chunks_per_scene
+    st3 = torch.empty(B * cps, 64, 2, device=DEV)
+    rec = 64 * 64 + 64
+    gr = torch.empty(B * cps, rec, device=DEV)
+    a.stats, a.gram = st3.data_ptr(), gr.data_ptr()
+    L.call("pcs_gemm", ct.byref(a), L.stream_ptr())
+    per_scene = torch.empty(B, rec, device=DEV)
+    L.call("pcs_reduce_partials_grouped", L.ptr(gr), B, cps, rec, 1.0, L.ptr(per_scene), L.stream_ptr())
+    tot = torch.empty(rec, device=DEV)
+    L.call("pcs_reduce_partials", L.ptr(per_scene), B, rec, 1.0, L.ptr(tot), 1, rec, L.stream_ptr())
+    Wf = W1.float().contiguous()
+    stg = torch.empty(B, 512, 2, device=DEV)
+    L.call("pcs_bn_stats_gram_sbias", L.ptr(tot[:4096]), L.ptr(per_scene[:, 4096:].contiguous()), B, N, L.ptr(Wf),
+           64, 64, 512, L.ptr(sbias), L.ptr(stg), L.stream_ptr())
+    # the direct route: seg_conv1's forward GEMM with per-chunk statistics of its fp32 outputs
+    y1 = torch.empty(M, 512, dtype=torch.bfloat16, device=DEV)
+    b = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=512, dtype=L.BF16, prologue=L.PRO_BNRELU,
+                   epilogue=L.EPI_FWD, chunks_per_scene=0, A=y2.data_ptr(), W=W1.data_ptr(), C=y1.data_ptr(),
+                   pa=s2.data_ptr(), pb=t2.data_ptr(), scene_bias=sbias.data_ptr(), a_keep_scale=1.0, c_keep_scale=1.0)
+    lib.pcs_gemm_geometry(ct.byref(b))
+    cpd = b.chunks_per_scene
+    std = torch.empty(B * cpd, 512, 2, device=DEV)
+    b.stats = std.data_ptr()
+    L.call("pcs_gemm", ct.byref(b), L.stream_ptr())
+    torch.cuda.synchronize()
+    a2 = torch.relu(y2.float() * s2 + t2).to(torch.bfloat16).double()
+    y = (a2 @ W1.double().T).view(B, N, 512) + sbias.double()[:, None, :]
+    mean_b = y.mean(1)
+    var = ((y - y.mean((0, 1))) ** 2).mean((0, 1))
+    ratio = float((y.mean((0, 1)).abs() / var.sqrt()).max())
+
+    def total_var(mb, m2b):   # per-scene (mean, M2) pairs -> the batch variance (Chan)
+        mu = mb.mean(0)
+        return (m2b.sum(0) + N * ((mb - mu) ** 2).sum(0)) / M
+
+    vg = total_var(stg[..., 0].double(), stg[..., 1].double())
+    sd = std.double().view(B, cpd, 512, 2)
+    rps = lib.pcs_gemm_geometry(ct.byref(b))
+    rows = torch.tensor([min(rps, N - c * rps) for c in range(cpd)], dtype=torch.float64, device=DEV)[None, :, None]
+    md = (sd[..., 0] * rows).sum(1) / N
+    m2d = sd[..., 1].sum(1) + (rows * (sd[..., 0] - md[:, None, :]) ** 2).sum(1)
+    vd = total_var(md, m2d)
+    eg = float(((vg - var).abs() / var).max())
+    ed = float(((vd - var).abs() / var).max())
+    emg = float(((stg[..., 0].double() - mean_b).abs() / var.sqrt()).max())
+    print(f"offset {offset}: max |mean|/std {ratio:.1f}; variance rel err Gram route {eg:.2e}, direct route "
+          f"{ed:.2e}; Gram-route mean err / std {emg:.2e}")
+    assert emg < 1e-4
+    assert eg <= ed + 2e-4
