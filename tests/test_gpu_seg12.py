@@ -207,10 +207,13 @@ def test_conv3_forward_gram_of_its_operand(B, N):
 def test_bn_seg1_gram_stats_offset_operand(offset):
     """bn_seg1's variance from the Gram route (uncentred: w (G - S S^T / N) w^T) on conv3's own
     fp32 Gram records, with a2 = relu(s2 y2 + t2) pushed away from zero by `offset` so that the
-    channels of y1 = a2 W1^T have |mean| / std up to ~50: against fp64 statistics of the same
+    channels of y1 = a2 W1^T have |mean| / std up to ~180: against fp64 statistics of the same
     y1, and against the direct per-chunk (mean, M2) of seg_conv1's forward GEMM (shifted sums,
-    Chan merge).  The Gram route's variance error must stay within the direct route's error
-    plus 2e-4 relative (a quarter of a bf16 half-ulp in the BN scale), at every ratio."""
+    Chan merge).  The Gram route's variance error must stay below 1e-3 and within the direct
+    route's error plus 2e-4 relative (a quarter of a bf16 half-ulp in the BN scale), at every
+    ratio.  Measured r06 (|mean|/std 9 / 47 / 184): Gram route 4.3e-7 / 3.8e-5 / 4.7e-4, direct
+    route 3.2e-4 / 7.2e-3 / 0.11 (it takes the statistics of the bf16-stored outputs, whose
+    rounding noise grows with |mean|)."""
     import pcs_amd._lib as L
     lib = L.load()
     B, N = 2, 2 ** 17
@@ -276,4 +279,4 @@ def test_bn_seg1_gram_stats_offset_operand(offset):
     print(f"offset {offset}: max |mean|/std {ratio:.1f}; variance rel err Gram route {eg:.2e}, direct route "
           f"{ed:.2e}; Gram-route mean err / std {emg:.2e}")
     assert emg < 1e-4
-    assert eg <= ed + 2e-4
+    assert eg < 1e-3 and eg <= ed + 2e-4
