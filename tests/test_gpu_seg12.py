@@ -226,9 +226,9 @@ def test_bn_seg1_gram_stats_offset_operand(offset):
     W1 = (torch.randn(512, 64, generator=g) * 0.05 + 0.03).to(torch.bfloat16).to(DEV)
     sbias = (torch.randn(B, 512, generator=g) * 0.2).to(DEV)
     # conv3's forward with the gram record, reduced as the engine does (engine._seg12)
+    y3 = torch.empty(M, 64, dtype=torch.bfloat16, device=DEV)   # (held: the kernel writes it)
     a = L.GemmArgs(num_scenes=B, scene_rows=N, K=64, Ncols=64, dtype=L.BF16, prologue=L.PRO_BNRELU,
-                   epilogue=L.EPI_FWD, chunks_per_scene=0, A=y2.data_ptr(), W=W3.data_ptr(),
-                   C=torch.empty(M, 64, dtype=torch.bfloat16, device=DEV).data_ptr(),
+                   epilogue=L.EPI_FWD, chunks_per_scene=0, A=y2.data_ptr(), W=W3.data_ptr(), C=y3.data_ptr(),
                    pa=s2.data_ptr(), pb=t2.data_ptr(), a_keep_scale=1.0, c_keep_scale=1.0)
     lib.pcs_gemm_geometry(ct.byref(a))
     cps = a.chunks_per_scene
