@@ -295,7 +295,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--draw-at-start", action="store_true",
-                    help="bf16: draw the dropout bits at the start of the forward (A/B)")
+                    help="draw the dropout bits at the start of the forward instead of beside the Gram of a5 (A/B)")
     ap.add_argument("--no-fused-seg12", action="store_true",
                     help="A/B: seg_conv1 and seg_conv2 forward as two passes instead of pcs_fwd_seg12")
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],

@@ -407,11 +407,11 @@ class Engine:
             m1.record_stream(side)
             m2.record_stream(side)
             sv.mask_bufs = (m1, m2)
-        # bf16 (stored-a5 Gram): draw beside the Gram of a5, MFMA-bound at 214 VGPRs x 2 waves per
+        # bf16 / fp8 (stored-a5 Gram): draw beside the Gram of a5, MFMA-bound at 214 / 216 VGPRs x 2 waves per
         # SIMD, with three 256-thread workgroups per CU (24 VGPRs a wave: they fit beside it and
         # use its idle VALU issue; 0.77 ms per call against 0.83 with two, the Gram and the step
         # unchanged, tools/draw_wg.py); otherwise at the start of the forward with a full grid
-        draw_beside_gram = (train and masks is None and self._raw_gram() and not self.fp8 and self.draw_beside_gram
+        draw_beside_gram = (train and masks is None and self._raw_gram() and self.draw_beside_gram
                             and self.dropout_draw != "independent")
         if train and masks is None and not draw_beside_gram:
             draw_masks()
