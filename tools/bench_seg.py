@@ -1,5 +1,5 @@
 """Micro-benchmark of the fused seg_conv2 / seg_conv3 input + weight gradient
-(pcs_dgrad_wgrad_bn on csrc/fused_seg.hip) at cfg2 (4 x 128^3 rows), with dropout bits.
+(pcs_dgrad_wgrad_bn: csrc/fused_seg4.hip; SEG_SMALL=1 the conv2-4 shapes of csrc/fused_bwd.hip, SEG_ADD=1 with an addend) at cfg2 (4 x 128^3 rows), with dropout bits.
     python tools/bench_seg.py [reps]"""
 import ctypes as ct
 import os
@@ -41,6 +41,9 @@ def fused(B, N, cout, cin, reps, mask=True):
     a.es, a.et, a.emean, a.erstd = (t.data_ptr() for t in keep[3:])
     if mask:
         a.c_mask = bits.data_ptr()
+    elif os.environ.get("SEG_ADD"):   # conv3's backward: + seg_conv1's input gradient dA2
+        add = torch.randn(M, cin, device=dev).to(torch.bfloat16)
+        a.addend = add.data_ptr()
     nbytes = L.load().pcs_dgrad_wgrad_bn_workspace(ct.byref(a))
     st = torch.empty(B * a.chunks_per_scene, cin, 2, device=dev)
     ws = torch.empty(nbytes // 4, device=dev)
