@@ -1,4 +1,4 @@
-# same-box A/B of fused_seg4.hip builds (abtest/<name>/libpcs.so, tools/build_variants.sh SRC=fused_seg4):
+# same-box A/B of fused_seg4.hip (or fused_bwd.hip) builds (abtest/<name>/libpcs.so, tools/build_variants.sh SRC=fused_seg4):
 # the fused-backward tests on each build, then alternating timing (tools/bench_seg.py)
 set -e
 mkdir -p gpurun_out
