@@ -29,8 +29,11 @@ constexpr int DY_ROWB = COUT * 2 + 32;             // dy [MS][COUT] (+32 B pad)
 constexpr int X_ROWB = CIN * 2 + 32;               // x  [MS][CIN]
 constexpr int OFF_DY = CIN * WT_ROWB;              // 64 KB
 constexpr int OFF_X = OFF_DY + MS * DY_ROWB;
-constexpr int OFF_OUT = OFF_X + MS * X_ROWB;       // dA2 tile [MS][CIN] bf16
-constexpr int OFF_COEF = OFF_OUT + MS * CIN * 2;  // alpha | beta | gamma [COUT], s | t [CIN]
+constexpr int OFF_OUT = OFF_X + MS * X_ROWB;       // dA2 tile [MS][CIN] bf16, rows OUT_ROWB apart
+// (+8 B: the epilogue's 8-B writes of 16 rows at one column hit 16 different banks -- 128-B rows
+// put them on two, 16-way (SQ_LDS_BANK_CONFLICT 0.38 of the LDS cycles, r06))
+constexpr int OUT_ROWB = CIN * 2 + 8;
+constexpr int OFF_COEF = OFF_OUT + MS * OUT_ROWB;  // alpha | beta | gamma [COUT], s | t [CIN]
 constexpr int LDS_BYTES = OFF_COEF + (3 * COUT + 2 * CIN) * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 // folded form: s | t | cvec [CIN] f32, then H [CIN][CIN] bf16 (XOR-swizzled 16-B slots)
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int c = (cb0 + j) * 16 + 4 * g;
-      *reinterpret_cast<uint2 *>(lds + OFF_OUT + (mb * 16 + l16) * CIN * 2 + c * 2) =
+      *reinterpret_cast<uint2 *>(lds + OFF_OUT + (mb * 16 + l16) * OUT_ROWB + c * 2) =
           make_uint2(pack2bf(accd[j][0], accd[j][1]), pack2bf(accd[j][2], accd[j][3]));
     }
     lds_barrier();   // step st consumed; its dA2 tile complete
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_s1_kernel(pcs_wgrad_args 
       const int r = tid >> 3, ch = tid & 7;   // 64 rows x 8 chunks of 16 B
       if (m0 + r < hi)
         st16(dX + (sbase + m0 + r) * CIN + ch * 8,
-             *reinterpret_cast<const u32x4 *>(lds + OFF_OUT + r * CIN * 2 + ch * 16));
+             *reinterpret_cast<const u32x4 *>(lds + OFF_OUT + r * OUT_ROWB + ch * 16));
     }
     if (st + 1 < nsteps) {
       store_step(m0 + MS);
@@ -477,14 +480,19 @@ template <int COUT, int CIN, int CB, int MS, bool MASK, bool ADD> struct FB {
   static constexpr int WT_ROWB = COUT * 2;
   static constexpr int DY_ROWB = COUT * 2 + 32;
   static constexpr int X_ROWB = CB * 2 + 32;
-  static constexpr int YP_ROWB = CB * 2;
+  // Yp / addend rows 16 B and the dz' tile's rows 8 B longer than their data: the epilogue reads
+  // (8 B) and writes (8 B) 16 rows at one column, which 128-B rows put on two banks (8-way
+  // reads, 16-way writes: SQ_LDS_BANK_CONFLICT 0.5-0.6 of the LDS cycles, r06); padded, the
+  // reads are conflict-free and the writes too (the store pass's 16-B reads 2-way)
+  static constexpr int YP_ROWB = CB * 2 + 16;
+  static constexpr int OUT_ROWB = CB * 2 + 8;
   static constexpr int OFF_DY = CB * WT_ROWB;
   static constexpr int OFF_X = OFF_DY + MS * DY_ROWB;
   static constexpr int OFF_YP = OFF_X + MS * X_ROWB;
   static constexpr int OFF_AD = OFF_YP + MS * YP_ROWB;
   static constexpr int OFF_MK = OFF_AD + (ADD ? MS * YP_ROWB : 0);
   static constexpr int OFF_OUT = OFF_MK + (MASK ? MS * CB / 8 : 0);
-  static constexpr int OFF_COEF = OFF_OUT + MS * CB * 2;   // alpha|beta|gamma [COUT], es|et [CB]
+  static constexpr int OFF_COEF = OFF_OUT + MS * OUT_ROWB;   // alpha|beta|gamma [COUT], es|et [CB]
   static constexpr int BYTES = OFF_COEF + (3 * COUT + 2 * CB) * 4;
   static constexpr bool FITS = BYTES <= 160 * 1024;   // LDS budget (checked in the kernel)
   static_assert(CIN % CB == 0, "column blocks");
@@ -501,8 +509,9 @@ template <int COUT, int CIN, int CB, int MS, bool MASK, bool ADD> struct FB {
 PCS_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 PCS_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
+// (the 64-wide layers run two workgroups per CU: at most 128 VGPRs)
 template <int COUT, int CIN, int CB, int MS, bool MASK, bool ADD>
-__global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a, float *__restrict__ wpart,
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(COUT == 64 ? 4 : 1, 8))) void dgrad_wgrad_bn_kernel(pcs_gemm_args a, float *__restrict__ wpart,
                                                                  int64_t rows_per_split) {
   typedef FB<COUT, CIN, CB, MS, MASK, ADD> F;
   static_assert(F::FITS, "LDS budget");
@@ -667,7 +676,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
         s1[u][r] += dz;
         s2[u][r] = fmaf(dz, y[r], s2[u][r]);
       }
-      *reinterpret_cast<uint2 *>(lds + F::OFF_OUT + ml * CB * 2 + c * 2) =
+      *reinterpret_cast<uint2 *>(lds + F::OFF_OUT + ml * F::OUT_ROWB + c * 2) =
           make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
     }
     lds_barrier();   // step st consumed; its dz' tile complete
@@ -676,7 +685,7 @@ __global__ __launch_bounds__(THREADS) void dgrad_wgrad_bn_kernel(pcs_gemm_args a
       const int q = tid + THREADS * i, rl = q / (CB / 8), cc = q % (CB / 8);
       if (m0 + rl < hi)
         st16(Cg + (sbase + m0 + rl) * CIN + n0 + cc * 8,
-             *reinterpret_cast<const u32x4 *>(lds + F::OFF_OUT + rl * CB * 2 + cc * 16));
+             *reinterpret_cast<const u32x4 *>(lds + F::OFF_OUT + rl * F::OUT_ROWB + cc * 16));
     }
     if (st + 1 < nsteps) {
       store_step(m0 + MS);
