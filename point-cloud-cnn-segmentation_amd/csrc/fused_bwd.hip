@@ -52,7 +52,9 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 PCS_DEV int prow(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
-PCS_DEV int wt_off(int c, int slot) { return c * WT_ROWB + ((slot ^ (c & 7)) << 4); }
+// (slot ^ (c & 15): the dgrad's 16-B fragment reads of 16 rows c at slots 4 kk + g fall in 16
+// different slots of a 64-slot row; with c & 7 the two lane groups g met in the same 8, 2-way)
+PCS_DEV int wt_off(int c, int slot) { return c * WT_ROWB + ((slot ^ (c & 15)) << 4); }
 
 PCS_DEV void lds_vec8(const float *p, float (&v)[8]) {
   const float4 a = *reinterpret_cast<const float4 *>(p);
@@ -478,6 +480,8 @@ namespace {
 template <int COUT, int CIN, int CB, int MS, bool MASK, bool ADD> struct FB {
   static constexpr int NBLK = CIN / CB;
   static constexpr int WT_ROWB = COUT * 2;
+  // W^T slot swizzle: c & 15 where a row holds 16 slots or more (as wt_off above), else c & 7
+  static constexpr int WSW = COUT >= 128 ? 15 : 7;
   static constexpr int DY_ROWB = COUT * 2 + 32;
   static constexpr int X_ROWB = CB * 2 + 32;
   // Yp / addend rows 16 B and the dz' tile's rows 8 B longer than their data: the epilogue reads
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(COUT ==
 
   for (int i = tid; i < CB * COUT / 8; i += THREADS) {   // W^T rows n0.. [CB][COUT] -> LDS
     const int c = i / (COUT / 8), slot = i % (COUT / 8);
-    *reinterpret_cast<u32x4 *>(lds + c * F::WT_ROWB + ((slot ^ (c & 7)) << 4)) =
+    *reinterpret_cast<u32x4 *>(lds + c * F::WT_ROWB + ((slot ^ (c & F::WSW)) << 4)) =
         *reinterpret_cast<const u32x4 *>(Wt + (int64_t)(n0 + c) * COUT + slot * 8);
   }
   float *cf = reinterpret_cast<float *>(lds + F::OFF_COEF);
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(COUT ==
 #pragma unroll
       for (int u = 0; u < F::TPW_D; ++u) {
         const int c = (cbd + u) * 16 + l16;
-        const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(lds + c * F::WT_ROWB + ((slot ^ (c & 7)) << 4));
+        const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(lds + c * F::WT_ROWB + ((slot ^ (c & F::WSW)) << 4));
         accd[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, yf, accd[u], 0, 0, 0);
       }
     }
