@@ -160,13 +160,16 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
   // ---- DMA of step s into stage sidx: dword pieces of 256 B.  y2: pieces p = w, w + 8 (rows 2p,
   // 2p + 1; lane -> row 2p + lane / 32, physical slot (lane % 32) / 4, dword lane % 4, holding
   // logical slot ps ^ f(row) of the source row); keep bits: piece w (rows 4 w .. 4 w + 3, 64 B
-  // each, unpermuted).  Rows past the slice clamp to its last row.
+  // each), dword d of row r holding logical dword d ^ (r & 15), so the 16 rows the epilogue reads
+  // at one logical byte fall in 16 banks instead of 2 (8-way).  Rows past the slice clamp to its
+  // last row.
   auto y_off = [&](int p, int lastr) -> uint32_t {
     const int r = 2 * p + (lane >> 5), ps = (lane & 31) >> 2;
     return (uint32_t)(min(r, lastr) * ROW1 + ((ps ^ f64s(r)) << 4) + 4 * (lane & 3));
   };
   auto m_off = [&](int lastr) -> uint32_t {
-    return (uint32_t)(min(4 * w + (lane >> 4), lastr) * MROW + 4 * (lane & 15));
+    const int r = 4 * w + (lane >> 4);
+    return (uint32_t)(min(r, lastr) * MROW + 4 * ((lane & 15) ^ (r & 15)));
   };
   const uint32_t lds_m0 = (uint32_t)(uintptr_t)(lds_void_t *)lds;
   auto dma_step = [&](int s, int sidx) {
@@ -206,6 +209,9 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
   const uint32_t o1 = (uint32_t)(l16 * (N1 * 2) + (64 * w + 16 * (g & 1) + 8 * (g >> 1)) * 2);
   const uint32_t o2 = (uint32_t)(l16 * (N2 * 2) + (32 * w + 16 * (g & 1) + 8 * (g >> 1)) * 2);
   const int fa = f64s(l16);   // (16 rt + l16) >> 1 & 7 and (64 w + 16 ct + l16) >> 1 & 7 alike
+  // keep byte 8 w + 2 ct + (g >> 1) of row 16 rt + l16 (permuted dwords, see the DMA): at
+  // 1024 rt + 2 (ct & 1) + (lkb ^ 4 (2 w + (ct >> 1))), one v_xor with a uniform per read
+  const int lkb = 68 * l16 + (g >> 1);
 
   // ---- stage 1 of a step, one 16-column tile ct at a time: Y1[row 16 rt + l16][64 w + 16 ct + 4 g + r]
   auto stage1 = [&](const char *st, int ct, f32x4 (&acc1)[2]) __attribute__((always_inline)) {
@@ -241,7 +247,8 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
       const float x3 = relu(fmaf(bf2f(pk[rt][1] >> 16), sc1[3], tc1[3]));
       uint2 xo = make_uint2(pack2bf(x0, x1), pack2bf(x2, x3));
       if constexpr (MASK) {   // columns c0 .. c0 + 3: keep byte c0 / 8 of row R, bits 4 (g % 2) ..
-        const uint32_t byte = *reinterpret_cast<const uint8_t *>(st + XB1 + R * MROW + 8 * w + 2 * ct + (g >> 1));
+        const uint32_t byte = *reinterpret_cast<const uint8_t *>(st + XB1 + 1024 * rt + 2 * (ct & 1) +
+                                                                 (lkb ^ (4 * (2 * w + (ct >> 1)))));
         const uint2 m = *reinterpret_cast<const uint2 *>(lds + OFF_LUT + byte * 16 + 8 * (g & 1));
         xo.x &= m.x;
         xo.y &= m.y;
