@@ -63,6 +63,7 @@ template <int COUT> struct S4 {
   static constexpr int VM_STEP = NPW + 1;            // + the dropout-bit piece
   static constexpr int TPASS = MS * CPR / THREADS;   // transform chunks per thread
   static_assert(TPASS == 1 || TPASS == 2, "transform passes");
+  static constexpr bool DACC_V = true;   // input gradient D in VGPRs (see the k-step loop)
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -139,6 +140,28 @@ PCS_DEV void lds_vec8(const char *p, int half_bytes, float (&v)[8]) {
 }
 PCS_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 PCS_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+// the coefficients of 8 channels as 4 packed pairs (channels 2 i, 2 i + 1)
+PCS_DEV void lds_pairs8(const char *p, int half_bytes, f32x2 (&v)[4]) {
+  const u32x4 x = *reinterpret_cast<const u32x4 *>(p);
+  const u32x4 y = *reinterpret_cast<const u32x4 *>(p + half_bytes);
+  v[0] = f32x2{__uint_as_float(x[0]), __uint_as_float(x[1])};
+  v[1] = f32x2{__uint_as_float(x[2]), __uint_as_float(x[3])};
+  v[2] = f32x2{__uint_as_float(y[0]), __uint_as_float(y[1])};
+  v[3] = f32x2{__uint_as_float(y[2]), __uint_as_float(y[3])};
+}
+// the bn backward of one 16-B chunk, dy = alpha dz + (gamma y + beta), in packed fp32 pairs
+// (v_pk_fma_f32: two channels per issue; the same roundings as two fmaf)
+PCS_DEV u32x4 bnb_chunk(const u32x4 &dz, const u32x4 &y, const f32x2 (&ca)[4], const f32x2 (&cb)[4],
+                        const f32x2 (&cg)[4]) {
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 d = {bf_lo(dz[i]), bf_hi(dz[i])}, yy = {bf_lo(y[i]), bf_hi(y[i])};
+    const f32x2 r = __builtin_elementwise_fma(ca[i], d, __builtin_elementwise_fma(cg[i], yy, cb[i]));
+    o[i] = pack2bf(r.x, r.y);
+  }
+  return mk_u32x4(o[0], o[1], o[2], o[3]);
+}
 template <int V> struct IC { static constexpr int value = V; };
 template <int N, int I = 0, typename Fn> PCS_DEV void sfor(Fn &&fn) {
   if constexpr (I < N) {
@@ -306,6 +329,12 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
   const int vrx0 = 8 * (p ^ g);
   // transform: logical chunk lc of rows trow + pass * (THREADS / CPR)
   const int lc = tid % F::CPR, trow = tid / F::CPR;
+  int o_tr[F::TPASS];
+#pragma unroll
+  for (int ps = 0; ps < F::TPASS; ++ps) {
+    const int r = trow + ps * (THREADS / F::CPR);
+    o_tr[ps] = r * ROWB + ((lc ^ fdz(r)) << 4);
+  }
   const char *cft = lds + F::OFF_CF + (lc * 16);   // split layout: elements 0-3 at + 16 lc, 4-7 at + COUT * 2 + 16 lc
 
   f32x16 acc[F::NO][2];
@@ -313,26 +342,23 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
   for (int o = 0; o < F::NO; ++o)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) acc[o][nb] = f32x16{};
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};   // the lane's column of tile ct
+  // the lane's column of tile ct: S1 / S2 as packed pairs (rows 4 g + 2 j, 4 g + 2 j + 1), summed at the end
+  f32x2 s1p[4] = {}, s2p[4] = {};
 
   // dy of step s (landed, barrier passed) in place over its dZ slab; rows past the slice -> 0
   auto transform = [&](int s, int sidx) __attribute__((always_inline)) {
     char *st = lds + sidx * F::STAGE;
     const int rem = min(rows - s * MS, MS);
-    float ca[8], cb[8], cg[8];
-    lds_vec8(cft, COUT * 2, ca);
-    lds_vec8(cft + COUT * 4, COUT * 2, cb);
-    lds_vec8(cft + 2 * COUT * 4, COUT * 2, cg);
+    f32x2 ca[4], cb[4], cg[4];
+    lds_pairs8(cft, COUT * 2, ca);
+    lds_pairs8(cft + COUT * 4, COUT * 2, cb);
+    lds_pairs8(cft + 2 * COUT * 4, COUT * 2, cg);
 #pragma unroll
     for (int ps = 0; ps < F::TPASS; ++ps) {
       const int r = trow + ps * (THREADS / F::CPR);
-      const int o = r * ROWB + ((lc ^ fdz(r)) << 4);
-      float v[8], y[8];
-      unpack_chunk(*reinterpret_cast<const u32x4 *>(st + o), v);
-      unpack_chunk(*reinterpret_cast<const u32x4 *>(st + F::DZB + o), y);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaf(ca[e], v[e], fmaf(cg[e], y[e], cb[e]));
-      const u32x4 out = pack_chunk(v);
+      const int o = o_tr[ps];
+      const u32x4 out = bnb_chunk(*reinterpret_cast<const u32x4 *>(st + o),
+                                  *reinterpret_cast<const u32x4 *>(st + F::DZB + o), ca, cb, cg);
       // (MASK: rows past the slice need no zeroing -- their keep bits read as 0 from the range-
       // checked DMA, so their x, v and dW terms are 0 whatever dy holds)
       const bool in = MASK || r < rem;
@@ -386,7 +412,8 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
     bf16x8 bq[2], wl[2][4];
     auto rd_k = [&](auto Kc) __attribute__((always_inline)) {
       constexpr int kk = decltype(Kc)::value;
-      bq[kk & 1] = *reinterpret_cast<const bf16x8 *>(st + o_dg + ((kk << 6) ^ dgx));
+      // ((kk << 6) ^ dgx) with dgx in bits 6-7: k-steps kk and kk + 4 differ by 256 B (an immediate)
+      bq[kk & 1] = *reinterpret_cast<const bf16x8 *>(st + o_dg + (((kk & 3) << 6) ^ dgx) + 256 * (kk >> 2));
       if constexpr (kk < F::WLK) {
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
@@ -398,12 +425,38 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       constexpr int kk = decltype(Kc)::value;
       if constexpr (kk + 1 < F::KSD) rd_k(IC<kk + 1>{});
       __builtin_amdgcn_sched_barrier(0);
+      bf16x8 w[4];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
-        bf16x8 w;
-        if constexpr (kk < F::WLK) w = wl[kk & 1][ct];
-        else w = wt[ct][kk - F::WLK];
-        dacc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[kk & 1], w, dacc[ct], 0, 0, 0);
+        if constexpr (kk < F::WLK) w[ct] = wl[kk & 1][ct];
+        else w[ct] = wt[ct][kk - F::WLK];
+      }
+      if constexpr (F::DACC_V) {
+        // (seg_conv2: dW's accumulators fill all 256 AGPRs; the builtin's AGPR-form D made hipcc
+        // park 16 of them in VGPRs around every step -- 32 moves.  Here D is in VGPRs: the
+        // operands get 2 wait states (VALU write -> MFMA read), the last group's D 12 before
+        // the epilogue reads it; an accumulate chain needs none)
+#define PCS_MF(d, b, c) "v_mfma_f32_16x16x32_bf16 " d ", %4, " b ", " c "\n\t"
+        if constexpr (kk == 0)
+          asm volatile("s_nop 1\n\t" PCS_MF("%0", "%5", "0") PCS_MF("%1", "%6", "0") PCS_MF("%2", "%7", "0")
+                           PCS_MF("%3", "%8", "0")
+                       : "=&v"(dacc[0]), "=&v"(dacc[1]), "=&v"(dacc[2]), "=&v"(dacc[3])
+                       : "v"(bq[kk & 1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+        else if constexpr (kk + 1 < F::KSD)
+          asm volatile("s_nop 1\n\t" PCS_MF("%0", "%5", "%0") PCS_MF("%1", "%6", "%1") PCS_MF("%2", "%7", "%2")
+                           PCS_MF("%3", "%8", "%3")
+                       : "+v"(dacc[0]), "+v"(dacc[1]), "+v"(dacc[2]), "+v"(dacc[3])
+                       : "v"(bq[kk & 1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+        else
+          asm volatile("s_nop 1\n\t" PCS_MF("%0", "%5", "%0") PCS_MF("%1", "%6", "%1") PCS_MF("%2", "%7", "%2")
+                           PCS_MF("%3", "%8", "%3") "s_nop 7\n\ts_nop 3"
+                       : "+v"(dacc[0]), "+v"(dacc[1]), "+v"(dacc[2]), "+v"(dacc[3])
+                       : "v"(bq[kk & 1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+#undef PCS_MF
+      } else {
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+          dacc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[kk & 1], w[ct], dacc[ct], 0, 0, 0);
       }
       if constexpr (kk <= F::NPW) dma_piece(IC<kk>{}, sdma, sd);
       __builtin_amdgcn_sched_barrier(0);
@@ -417,17 +470,23 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
     for (int ct = 0; ct < 4; ++ct) {
       float xv[4], v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float y = (r & 1) ? bf_hi(yv[ct][r >> 1]) : bf_lo(yv[ct][r >> 1]);
-        const uint32_t wb = ct < 2 ? bb[r].x : bb[r].y;
-        // MASK: the keep bits of rows past the slice are 0 (range-checked DMA), no row test
-        const int kb = __builtin_amdgcn_sbfe((int)wb, 16 * (ct & 1) + l16, 1);
-        const int keep = (MASK || 4 * g + r < rem) ? kb : 0;
-        const float z = fmaf(y, esk[ct], etk[ct]);
-        xv[r] = __int_as_float(__float_as_int(relu(z)) & keep);
-        v[r] = xv[r] > 0.f ? dacc[ct][r] * ks : 0.f;
-        s1[ct] += v[r];
-        s2[ct] = fmaf(v[r], y, s2[ct]);
+      for (int j = 0; j < 2; ++j) {   // rows 2 j, 2 j + 1 in packed fp32 (v_pk_fma / mul / add)
+        const f32x2 y2 = {bf_lo(yv[ct][j]), bf_hi(yv[ct][j])};
+        const f32x2 z2 = __builtin_elementwise_fma(y2, f32x2{esk[ct], esk[ct]}, f32x2{etk[ct], etk[ct]});
+        const f32x2 d2 = f32x2{dacc[ct][2 * j], dacc[ct][2 * j + 1]} * ks;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 2 * j + h;
+          const uint32_t wb = ct < 2 ? bb[r].x : bb[r].y;
+          // MASK: the keep bits of rows past the slice are 0 (range-checked DMA), no row test
+          const int kb = __builtin_amdgcn_sbfe((int)wb, 16 * (ct & 1) + l16, 1);
+          const int keep = (MASK || 4 * g + r < rem) ? kb : 0;
+          xv[r] = __int_as_float(__float_as_int(relu(z2[h])) & keep);
+          v[r] = xv[r] > 0.f ? d2[h] : 0.f;
+        }
+        const f32x2 v2 = {v[2 * j], v[2 * j + 1]};
+        s1p[ct] += v2;
+        s2p[ct] = __builtin_elementwise_fma(v2, y2, s2p[ct]);
       }
       *reinterpret_cast<uint2 *>(xw + o_tw + ((520 * ct) ^ twx)) = make_uint2(pack2bf(xv[0], xv[1]), pack2bf(xv[2], xv[3]));
       *reinterpret_cast<uint2 *>(xw + F::TILE + o_tw + ((520 * ct) ^ twx)) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
@@ -450,8 +509,9 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       const uint2 hi2 = *reinterpret_cast<const uint2 *>(xw + o_xb[nb][1]);
       xf[nb] = __builtin_bit_cast(bf16x8, mk_u32x4(lo2.x, lo2.y, hi2.x, hi2.y));
     }
-    auto rd_af = [&](int o) __attribute__((always_inline)) {
-      return tr_frag2(st + o_t0 + ((o << 6) ^ trx), st + o_t1 + ((o << 6) ^ trx));
+    auto rd_af = [&](int o) __attribute__((always_inline)) {   // ((o << 6) ^ trx), trx in bits 6-7
+      const int x = ((o & 3) << 6) ^ trx;
+      return tr_frag2(st + o_t0 + x + 256 * (o >> 2), st + o_t1 + x + 256 * (o >> 2));
     };
     bf16x8 afq[3];
     afq[0] = rd_af(0);
@@ -463,14 +523,14 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
 #pragma unroll
     for (int ps = 0; ps < F::TPASS; ++ps) {
       const int r = trow + ps * (THREADS / F::CPR);
-      const int o = r * ROWB + ((lc ^ fdz(r)) << 4);
+      const int o = o_tr[ps];
       tdz[ps] = *reinterpret_cast<const u32x4 *>(stn + o);
       tyy[ps] = *reinterpret_cast<const u32x4 *>(stn + F::DZB + o);
     }
-    float ca[8], cb[8], cg[8];
-    lds_vec8(cft, COUT * 2, ca);
-    lds_vec8(cft + COUT * 4, COUT * 2, cb);
-    lds_vec8(cft + 2 * COUT * 4, COUT * 2, cg);
+    f32x2 ca[4], cb[4], cg[4];
+    lds_pairs8(cft, COUT * 2, ca);
+    lds_pairs8(cft + COUT * 4, COUT * 2, cb);
+    lds_pairs8(cft + 2 * COUT * 4, COUT * 2, cg);
     __builtin_amdgcn_sched_barrier(0);
 
     // dz' stores: read s of v^T rows 16 s + 4 g + 0..3 (transposed: lane l16 gets row l16,
@@ -501,14 +561,11 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       if constexpr (o >= 1 && o - 1 < F::TPASS) {
         constexpr int ps = o - 1;
         const int r = trow + ps * (THREADS / F::CPR);
-        float vv[8], yy[8];
-        unpack_chunk(tdz[ps], vv);
-        unpack_chunk(tyy[ps], yy);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) vv[e] = fmaf(ca[e], vv[e], fmaf(cg[e], yy[e], cb[e]));
-        const u32x4 out = pack_chunk(vv);
-        const bool in = r < remn;   // (past the last step: a stage nobody reads)
-        *reinterpret_cast<u32x4 *>(stn + r * ROWB + ((lc ^ fdz(r)) << 4)) =
+        const u32x4 out = bnb_chunk(tdz[ps], tyy[ps], ca, cb, cg);
+        // (past the last step: a stage nobody reads; MASK: rows past the slice need no zeroing,
+        // as in transform() -- their keep bits are 0, so their x, v and dW terms are 0)
+        const bool in = MASK || r < remn;
+        *reinterpret_cast<u32x4 *>(stn + o_tr[ps]) =
             mk_u32x4(in ? out.x : 0u, in ? out.y : 0u, in ? out.z : 0u, in ? out.w : 0u);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -531,6 +588,12 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
         out[(int64_t)(32 * o + (e & 3) + 8 * (e >> 2) + 4 * H) * CIN + 32 * nb] = acc[o][nb][e];
 
   // ---- S1 / S2 over the four row groups g (lanes l16, l16 + 16, + 32, + 48)
+  float s1[4], s2[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    s1[ct] = s1p[ct].x + s1p[ct].y;
+    s2[ct] = s2p[ct].x + s2p[ct].y;
+  }
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll

@@ -1,0 +1,102 @@
+"""Register audit of the inline-asm MFMA chains in csrc/fused_seg4.hip (no GPU needed).
+
+The input gradient's v_mfma_f32_16x16x32_bf16 groups are inline asm with VGPR accumulators
+(fused_seg4.hip, the k-step loop): hipcc pads no hazard for them and sees their D registers as
+written at the end of each statement.  The wait states the statements carry are safe only if
+hipcc keeps the chain's accumulators where the asm left them -- the same four register ranges
+in every group of a chain and no compiler instruction touching them between the first group
+and the last (whose trailing s_nops cover the D -> VALU read).  Compiles the file to gfx950
+assembly and checks exactly that, plus no scratch / spills."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "point-cloud-cnn-segmentation_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC) and not shutil.which("hipcc"), reason="no hipcc")
+
+
+def vregs(text):
+    """The arch VGPR numbers an instruction names (vN and v[a:b])."""
+    out = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", text):
+        out.update(range(int(a), int(b) + 1))
+    for n in re.findall(r"(?<![\w\[])v(\d+)\b", text):
+        out.add(int(n))
+    return out
+
+
+@pytest.fixture(scope="module")
+def seg4_asm(tmp_path_factory):
+    out = tmp_path_factory.mktemp("asm") / "fused_seg4.s"
+    cmd = [HIPCC if os.path.exists(HIPCC) else "hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+           "--cuda-device-only", "-S", "-fno-slp-vectorize", "-o", str(out), "fused_seg4.hip"]
+    subprocess.run(cmd, cwd=CSRC, check=True, capture_output=True)
+    return out.read_text()
+
+
+def kernels(asm):
+    for m in re.finditer(r"^(_ZN\w*seg4_kernel\w*):", asm, flags=re.M):
+        end = asm.index(".Lfunc_end", m.end())
+        yield m.group(1), asm[m.end():end]
+
+
+def chains(body):
+    """Yield (groups, between): each group the list of D ranges of one asm MFMA statement, and
+    the compiler lines between the chain's first and last statements."""
+    lines = [ln.strip() for ln in body.splitlines()]
+    i, groups, between, in_chain = 0, [], [], False
+    while i < len(lines):
+        if lines[i] == ";;#ASMSTART":
+            j = lines.index(";;#ASMEND", i)
+            stmt = lines[i + 1:j]
+            mf = [s for s in stmt if s.startswith("v_mfma_f32_16x16x32_bf16")]
+            if mf:
+                ds = [s.split()[1].rstrip(",") for s in mf]
+                starts = all(s.rstrip().endswith(", 0") for s in mf)
+                if starts:
+                    assert not in_chain, "a chain restarted before its closing group"
+                    in_chain, groups, between = True, [], []
+                assert in_chain, "an accumulate group outside a chain"
+                groups.append(ds)
+                if any(s.startswith("s_nop 7") for s in stmt):
+                    yield groups, between
+                    in_chain = False
+            elif in_chain:
+                between.extend(stmt)
+            i = j + 1
+            continue
+        if in_chain and lines[i] and not lines[i].startswith(";") and not lines[i].startswith("."):
+            between.append(lines[i])
+        i += 1
+    assert not in_chain, "a chain without its closing group"
+
+
+def test_seg4_asm_chains_keep_their_accumulators(seg4_asm):
+    seen = 0
+    for name, body in kernels(seg4_asm):
+        n = 0
+        for groups, between in chains(body):
+            n += 1
+            assert all(g == groups[0] for g in groups), (name, groups)
+            d = set()
+            for r in groups[0]:
+                d |= vregs(r)
+            assert len(d) == 16, (name, groups[0])
+            touch = [ln for ln in between if vregs(ln) & d]
+            assert not touch, (name, touch[:5])
+        assert n >= 1, name
+        seen += 1
+    assert seen == 4   # <128, 256> and <256, 512>, dropout mask on / off
+
+
+def test_seg4_no_scratch(seg4_asm):
+    spills = re.findall(r"\.vgpr_spill_count:\s+(\d+)", seg4_asm)
+    scratch = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", seg4_asm)
+    assert spills and scratch
+    assert all(int(v) == 0 for v in spills + scratch)
