@@ -129,15 +129,6 @@ PCS_DEV bf16x8 tr_frag2(const char *p0, const char *p1) {
 }
 // split coefficient layout: elements 0-3 of every chunk first, then elements 4-7
 PCS_DEV int split_idx(int i, int n) { return ((i & 7) >> 2) * (n / 2) + (i >> 3) * 4 + (i & 3); }
-PCS_DEV void lds_vec8(const char *p, int half_bytes, float (&v)[8]) {
-  const u32x4 x = *reinterpret_cast<const u32x4 *>(p);
-  const u32x4 y = *reinterpret_cast<const u32x4 *>(p + half_bytes);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    v[e] = __uint_as_float(x[e]);
-    v[4 + e] = __uint_as_float(y[e]);
-  }
-}
 PCS_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 PCS_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 // the coefficients of 8 channels as 4 packed pairs (channels 2 i, 2 i + 1)
@@ -522,7 +513,6 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
     u32x4 tdz[F::TPASS], tyy[F::TPASS];
 #pragma unroll
     for (int ps = 0; ps < F::TPASS; ++ps) {
-      const int r = trow + ps * (THREADS / F::CPR);
       const int o = o_tr[ps];
       tdz[ps] = *reinterpret_cast<const u32x4 *>(stn + o);
       tyy[ps] = *reinterpret_cast<const u32x4 *>(stn + F::DZB + o);

@@ -633,11 +633,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       bf16_t *Cg = reinterpret_cast<bf16_t *>(a.C);
       const uint32_t *mrow = mbits + (tcur & 1) * 2048 + wn * 2;
       const bool full = valid == BM;   // uniform: only a scene's last tile is partial
-      float s1[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s1[j][r] = 0.f;
+      f32x2 s1[4][2] = {};   // columns (j, 2 h), (j, 2 h + 1) as a packed pair: v_pk_add_f32
       // Stores widened to 16 B (cdna_hip_programming.md T21 with v_permlane16_swap): a lane
       // holds 4 columns (8 B) of tile j; swapping tile j with tile j+1 between lane groups
       // 2h and 2h+1 leaves each lane 8 consecutive columns of tile j + (lg & 1), so every
@@ -663,8 +659,9 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
           for (int r = 0; r < 4; ++r) {
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe(word, FP8 ? 8 * r : (r >> 1) + 4 * (r & 1), 1);
             v[r] = and_mask(acc[i][j][r], keep);
-            s1[j][r] += v[r];
           }
+          s1[j][0] += f32x2{v[0], v[1]};
+          s1[j][1] += f32x2{v[2], v[3]};
           pk[j][0] = pack2bf(v[0], v[1]);
           pk[j][1] = pack2bf(v[2], v[3]);
         }
@@ -687,7 +684,7 @@ __global__ __launch_bounds__(THREADS) void gemm_glds_kernel(pcs_gemm_args a, int
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float t = row_sum(s1[j][r]);
+          const float t = row_sum(s1[j][r >> 1][r & 1]);
           if (lr == j * 4 + r) S1 = t;
         }
       if (do_stats) run[cme].x += S1;
