@@ -193,11 +193,11 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
     const f32x4 s2 = *reinterpret_cast<const f32x4 *>(lds + OFF_S2 + (8 * ls + 4 * hf) * 4);
     const f32x4 t2 = *reinterpret_cast<const f32x4 *>(lds + OFF_T2 + (8 * ls + 4 * hf) * 4);
     const uint2 u = *q;
-    const float v0 = relu(fmaf(bf2f(u.x & 0xffffu), s2[0], t2[0]));
-    const float v1 = relu(fmaf(bf2f(u.x >> 16), s2[1], t2[1]));
-    const float v2 = relu(fmaf(bf2f(u.y & 0xffffu), s2[2], t2[2]));
-    const float v3 = relu(fmaf(bf2f(u.y >> 16), s2[3], t2[3]));
-    *q = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+    const f32x2 v01 = __builtin_elementwise_fma(f32x2{bf2f(u.x & 0xffffu), bf2f(u.x >> 16)}, f32x2{s2[0], s2[1]},
+                                                f32x2{t2[0], t2[1]});
+    const f32x2 v23 = __builtin_elementwise_fma(f32x2{bf2f(u.y & 0xffffu), bf2f(u.y >> 16)}, f32x2{s2[2], s2[3]},
+                                                f32x2{t2[2], t2[3]});
+    *q = make_uint2(pack2bf(relu(v01.x), relu(v01.y)), pack2bf(relu(v23.x), relu(v23.y)));
   };
 
   // ---- outputs through buffer descriptors over the slice's rows (stores past them are dropped)
@@ -239,13 +239,16 @@ __global__ __launch_bounds__(THREADS) void fwd_s12_kernel(pcs_seg12_args a, int6
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       const int R = 16 * rt + l16;
-      pk[rt][0] = pack2bf(acc1[rt][0] + sb[0], acc1[rt][1] + sb[1]);
-      pk[rt][1] = pack2bf(acc1[rt][2] + sb[2], acc1[rt][3] + sb[3]);
-      const float x0 = relu(fmaf(bf2f(pk[rt][0] & 0xffffu), sc1[0], tc1[0]));
-      const float x1 = relu(fmaf(bf2f(pk[rt][0] >> 16), sc1[1], tc1[1]));
-      const float x2 = relu(fmaf(bf2f(pk[rt][1] & 0xffffu), sc1[2], tc1[2]));
-      const float x3 = relu(fmaf(bf2f(pk[rt][1] >> 16), sc1[3], tc1[3]));
-      uint2 xo = make_uint2(pack2bf(x0, x1), pack2bf(x2, x3));
+      // (column pairs in packed fp32: v_pk_add_f32 / v_pk_fma_f32, the same roundings)
+      const f32x2 y01 = f32x2{acc1[rt][0], acc1[rt][1]} + f32x2{sb[0], sb[1]};
+      const f32x2 y23 = f32x2{acc1[rt][2], acc1[rt][3]} + f32x2{sb[2], sb[3]};
+      pk[rt][0] = pack2bf(y01.x, y01.y);
+      pk[rt][1] = pack2bf(y23.x, y23.y);
+      const f32x2 z01 = __builtin_elementwise_fma(f32x2{bf2f(pk[rt][0] & 0xffffu), bf2f(pk[rt][0] >> 16)},
+                                                  f32x2{sc1[0], sc1[1]}, f32x2{tc1[0], tc1[1]});
+      const f32x2 z23 = __builtin_elementwise_fma(f32x2{bf2f(pk[rt][1] & 0xffffu), bf2f(pk[rt][1] >> 16)},
+                                                  f32x2{sc1[2], sc1[3]}, f32x2{tc1[2], tc1[3]});
+      uint2 xo = make_uint2(pack2bf(relu(z01.x), relu(z01.y)), pack2bf(relu(z23.x), relu(z23.y)));
       if constexpr (MASK) {   // columns c0 .. c0 + 3: keep byte c0 / 8 of row R, bits 4 (g % 2) ..
         const uint32_t byte = *reinterpret_cast<const uint8_t *>(st + XB1 + 1024 * rt + 2 * (ct & 1) +
                                                                  (lkb ^ (4 * (2 * w + (ct >> 1)))));
