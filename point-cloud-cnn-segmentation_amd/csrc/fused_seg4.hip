@@ -424,22 +424,23 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       }
       if constexpr (F::DACC_V) {
         // (seg_conv2: dW's accumulators fill all 256 AGPRs; the builtin's AGPR-form D made hipcc
-        // park 16 of them in VGPRs around every step -- 32 moves.  Here D is in VGPRs: the
-        // operands get 2 wait states (VALU write -> MFMA read), the last group's D 12 before
-        // the epilogue reads it; an accumulate chain needs none)
+        // park 16 of them in VGPRs around every step -- 32 moves.  Here D is in VGPRs; the last
+        // group's D gets 12 wait states before the epilogue reads it, an accumulate chain needs
+        // none, and the A / B operands come from ds_reads (hipcc's s_waitcnt), never from a VALU
+        // write in the 2 instructions before -- tests/test_asm_audit.py checks the compiled code)
 #define PCS_MF(d, b, c) "v_mfma_f32_16x16x32_bf16 " d ", %4, " b ", " c "\n\t"
         if constexpr (kk == 0)
-          asm volatile("s_nop 1\n\t" PCS_MF("%0", "%5", "0") PCS_MF("%1", "%6", "0") PCS_MF("%2", "%7", "0")
+          asm volatile(PCS_MF("%0", "%5", "0") PCS_MF("%1", "%6", "0") PCS_MF("%2", "%7", "0")
                            PCS_MF("%3", "%8", "0")
                        : "=&v"(dacc[0]), "=&v"(dacc[1]), "=&v"(dacc[2]), "=&v"(dacc[3])
                        : "v"(bq[kk & 1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
         else if constexpr (kk + 1 < F::KSD)
-          asm volatile("s_nop 1\n\t" PCS_MF("%0", "%5", "%0") PCS_MF("%1", "%6", "%1") PCS_MF("%2", "%7", "%2")
+          asm volatile(PCS_MF("%0", "%5", "%0") PCS_MF("%1", "%6", "%1") PCS_MF("%2", "%7", "%2")
                            PCS_MF("%3", "%8", "%3")
                        : "+v"(dacc[0]), "+v"(dacc[1]), "+v"(dacc[2]), "+v"(dacc[3])
                        : "v"(bq[kk & 1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
         else
-          asm volatile("s_nop 1\n\t" PCS_MF("%0", "%5", "%0") PCS_MF("%1", "%6", "%1") PCS_MF("%2", "%7", "%2")
+          asm volatile(PCS_MF("%0", "%5", "%0") PCS_MF("%1", "%6", "%1") PCS_MF("%2", "%7", "%2")
                            PCS_MF("%3", "%8", "%3") "s_nop 7\n\ts_nop 3"
                        : "+v"(dacc[0]), "+v"(dacc[1]), "+v"(dacc[2]), "+v"(dacc[3])
                        : "v"(bq[kk & 1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));

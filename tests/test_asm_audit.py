@@ -5,8 +5,10 @@ The input gradient's v_mfma_f32_16x16x32_bf16 groups are inline asm with VGPR ac
 written at the end of each statement.  The wait states the statements carry are safe only if
 hipcc keeps the chain's accumulators where the asm left them -- the same four register ranges
 in every group of a chain and no compiler instruction touching them between the first group
-and the last (whose trailing s_nops cover the D -> VALU read).  Compiles the file to gfx950
-assembly and checks exactly that, plus no scratch / spills."""
+and the last (whose trailing s_nops cover the D -> VALU read).  The statements carry no pad for
+a VALU write of an A / B operand (2 wait states): the check is that no VALU instruction among
+the 2 before a statement writes one (they come from ds_reads, waited by hipcc's s_waitcnt).
+Compiles the file to gfx950 assembly and checks exactly that, plus no scratch / spills."""
 import os
 import re
 import shutil
@@ -93,6 +95,45 @@ def test_seg4_asm_chains_keep_their_accumulators(seg4_asm):
         assert n >= 1, name
         seen += 1
     assert seen == 4   # <128, 256> and <256, 512>, dropout mask on / off
+
+
+def operand_hazards(body):
+    """(statement, instruction) pairs where one of the 2 instructions before an asm MFMA
+    statement is a VALU write of one of its A / B operands."""
+    lines = [ln.strip() for ln in body.splitlines()]
+    bad = []
+    for i, ln in enumerate(lines):
+        if ln != ";;#ASMSTART":
+            continue
+        j = lines.index(";;#ASMEND", i)
+        mf = [s for s in lines[i + 1:j] if s.startswith("v_mfma_f32_16x16x32_bf16")]
+        if not mf:
+            continue
+        ins = set()
+        for s in mf:
+            ops = [o.strip() for o in s.split(None, 1)[1].split(",")]
+            ins |= vregs(ops[1]) | vregs(ops[2])
+        seen, k = 0, i - 1
+        while seen < 2 and k >= 0:
+            prev = lines[k]
+            k -= 1
+            if not prev or prev.startswith(";") or prev.startswith("."):
+                continue
+            if prev.endswith(":"):
+                bad.append((mf[0], "a label: control may arrive without the wait states"))
+                break
+            seen += 1
+            if prev.startswith("v_") and not prev.startswith("v_mfma"):
+                dst = prev.split(None, 1)[1].split(",")[0] if " " in prev else ""
+                if vregs(dst) & ins:
+                    bad.append((mf[0], prev))
+    return bad
+
+
+def test_seg4_asm_operands_not_fresh_from_valu(seg4_asm):
+    for name, body in kernels(seg4_asm):
+        bad = operand_hazards(body)
+        assert not bad, (name, bad[:3])
 
 
 def test_seg4_no_scratch(seg4_asm):
