@@ -76,7 +76,9 @@ PCS_DEV int xcd_remap(int bid, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 // LDS-DMA through a buffer descriptor (su32x4 in SGPRs): rows past the descriptor's range
-// read as zeros (and are never used), so no row clamping and no per-step branches
+// read as zeros (and are never used), so no row clamping and no per-step branches.  M0 is
+// set per piece and not restored: hipcc never reads M0 in this file's kernels
+// (tests/test_asm_audit.py checks the compiled code)
 typedef unsigned int su32x4 __attribute__((ext_vector_type(4)));
 template <int OFF> PCS_DEV void blds16o(const su32x4 &rs, uint32_t voff, uint32_t soff, uint32_t m0base) {
   asm volatile("s_add_u32 m0, %3, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
@@ -95,12 +97,6 @@ PCS_DEV su32x4 rsrc_of(const void *base, uint32_t bytes) {
   r.w = 0x00020000u;
   return r;
 }
-PCS_DEV uint32_t m0_save() {
-  uint32_t k;
-  asm volatile("s_mov_b32 %0, m0" : "=s"(k));
-  return k;
-}
-PCS_DEV void m0_restore(uint32_t k) { asm volatile("s_mov_b32 m0, %0" ::"s"(k)); }
 template <int N> PCS_DEV void wait_vm() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -217,7 +213,6 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
   auto dma_piece = [&](auto Ic, int s, int sidx) __attribute__((always_inline)) {
     constexpr int i = decltype(Ic)::value;
     const uint32_t mb = lds_m0 + sidx * F::STAGE + wid * 1024;
-    const uint32_t keep = m0_save();
     if constexpr (i == F::NPW)
       blds4o<2 * F::DZB + F::YPB>(rs_mk, voff[i], (uint32_t)(s * MS * MKROW), lds_m0 + sidx * F::STAGE + (wid & 1) * 256);
     else if constexpr (4 * i < F::NPD)   // (NPD % 4 == 0: a round is one kind for every wave)
@@ -226,7 +221,6 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       blds16o<4096 * i>(rs_y, voff[i], (uint32_t)(s * MS * ROWB), mb);
     else
       blds16o<4096 * i>(rs_yp, voff[i], (uint32_t)(s * MS * CIN * 2), mb);
-    m0_restore(keep);
   };
 
   // ---- coefficients in LDS: dy-transform alpha / beta / gamma (split); the first WLK k-steps

@@ -64,10 +64,9 @@ PCS_DEV void sbar() { __builtin_amdgcn_sched_barrier(0); }
 // before unrelated LDS reads nor spills their 64-bit addresses: the kernel counts them itself.
 PCS_DEV void glds16(const char *sbase, uint32_t voff, char *lds_dst) {
   const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t *)lds_dst;
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(m0v)
+  // (M0 not restored: hipcc never reads M0 in this file's kernels -- tests/test_asm_audit.py)
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0v)
                : "memory");
 }
 PCS_DEV void barrier_raw() {

@@ -33,13 +33,39 @@ def vregs(text):
     return out
 
 
-@pytest.fixture(scope="module")
-def seg4_asm(tmp_path_factory):
-    out = tmp_path_factory.mktemp("asm") / "fused_seg4.s"
+def compile_asm(tmp_path_factory, src, extra):
+    """gfx950 assembly of csrc/<src> with csrc/Makefile's flags for it."""
+    out = tmp_path_factory.mktemp("asm") / (src + ".s")
     cmd = [HIPCC if os.path.exists(HIPCC) else "hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
-           "--cuda-device-only", "-S", "-fno-slp-vectorize", "-o", str(out), "fused_seg4.hip"]
+           "--cuda-device-only", "-S", *extra, "-o", str(out), src]
     subprocess.run(cmd, cwd=CSRC, check=True, capture_output=True)
     return out.read_text()
+
+
+@pytest.fixture(scope="module")
+def seg4_asm(tmp_path_factory):
+    return compile_asm(tmp_path_factory, "fused_seg4.hip", ["-fno-slp-vectorize"])
+
+
+# kernels whose LDS-DMA statements set M0 without restoring it (the file's comment at the DMA
+# helper): hipcc's own code must never read or write M0 there
+M0_FILES = {"fused_seg4.hip": ["-fno-slp-vectorize"], "gemm_glds.hip": ["-mllvm", "-disable-machine-sink"],
+            "gram_glds.hip": ["-mllvm", "-disable-machine-sink"]}
+
+
+@pytest.mark.parametrize("src", sorted(M0_FILES))
+def test_compiler_code_leaves_m0_alone(tmp_path_factory, src):
+    asm = compile_asm(tmp_path_factory, src, M0_FILES[src])
+    inasm, uses = False, []
+    for ln in asm.splitlines():
+        t = ln.strip()
+        if t == ";;#ASMSTART":
+            inasm = True
+        elif t == ";;#ASMEND":
+            inasm = False
+        elif not inasm and not t.startswith(";") and re.search(r"\bm0\b", t.split(";")[0]):
+            uses.append(t)
+    assert not uses, uses[:5]
 
 
 def kernels(asm):
