@@ -84,6 +84,14 @@ template <int OFF> PCS_DEV void blds16o(const su32x4 &rs, uint32_t voff, uint32_
   asm volatile("s_add_u32 m0, %3, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                :: "v"(voff), "s"(rs), "s"(soff), "s"(m0base), "n"(OFF) : "memory", "scc");
 }
+// the same loads with M0 already set (by set_m0, at least one instruction earlier)
+template <int OFF> PCS_DEV void set_m0(uint32_t base) { asm volatile("s_add_u32 m0, %0, %1" ::"s"(base), "n"(OFF) : "scc"); }
+PCS_DEV void blds16_m0(const su32x4 &rs, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rs), "s"(soff) : "memory");
+}
+PCS_DEV void blds4_m0(const su32x4 &rs, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dword %0, %1, %2 offen lds" ::"v"(voff), "s"(rs), "s"(soff) : "memory");
+}
 template <int OFF> PCS_DEV void blds4o(const su32x4 &rs, uint32_t voff, uint32_t soff, uint32_t m0base) {
   asm volatile("s_add_u32 m0, %3, %4\n\ts_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
                :: "v"(voff), "s"(rs), "s"(soff), "s"(m0base), "n"(OFF) : "memory", "scc");
@@ -221,6 +229,20 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       blds16o<4096 * i>(rs_y, voff[i], (uint32_t)(s * MS * ROWB), mb);
     else
       blds16o<4096 * i>(rs_yp, voff[i], (uint32_t)(s * MS * CIN * 2), mb);
+  };
+  // the same piece in two parts: M0 (ahead of an MFMA group, whose instructions are the
+  // SALU M0 write -> LDS-DMA wait state) and the load (after the group)
+  auto dma_m0 = [&](auto Ic, int sidx) __attribute__((always_inline)) {
+    constexpr int i = decltype(Ic)::value;
+    if constexpr (i == F::NPW) set_m0<2 * F::DZB + F::YPB>(lds_m0 + sidx * F::STAGE + (wid & 1) * 256);
+    else set_m0<4096 * i>(lds_m0 + sidx * F::STAGE + wid * 1024);
+  };
+  auto dma_load = [&](auto Ic, int s) __attribute__((always_inline)) {
+    constexpr int i = decltype(Ic)::value;
+    if constexpr (i == F::NPW) blds4_m0(rs_mk, voff[i], (uint32_t)(s * MS * MKROW));
+    else if constexpr (4 * i < F::NPD) blds16_m0(rs_dz, voff[i], (uint32_t)(s * MS * ROWB));
+    else if constexpr (4 * i < 2 * F::NPD) blds16_m0(rs_y, voff[i], (uint32_t)(s * MS * ROWB));
+    else blds16_m0(rs_yp, voff[i], (uint32_t)(s * MS * CIN * 2));
   };
 
   // ---- coefficients in LDS: dy-transform alpha / beta / gamma (split); the first WLK k-steps
@@ -410,6 +432,7 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       constexpr int kk = decltype(Kc)::value;
       if constexpr (kk + 1 < F::KSD) rd_k(IC<kk + 1>{});
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (kk <= F::NPW) dma_m0(IC<kk>{}, sd);
       bf16x8 w[4];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
@@ -444,7 +467,7 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
         for (int ct = 0; ct < 4; ++ct)
           dacc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[kk & 1], w[ct], dacc[ct], 0, 0, 0);
       }
-      if constexpr (kk <= F::NPW) dma_piece(IC<kk>{}, sdma, sd);
+      if constexpr (kk <= F::NPW) dma_load(IC<kk>{}, sdma);
       __builtin_amdgcn_sched_barrier(0);
     });
     sfor<F::VM_STEP - (F::KSD < F::VM_STEP ? F::KSD : F::VM_STEP)>([&](auto Ic) __attribute__((always_inline)) {
