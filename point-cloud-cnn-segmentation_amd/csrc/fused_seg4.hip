@@ -353,13 +353,10 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
   f32x2 s1p[4] = {}, s2p[4] = {};
 
   // dy of step s (landed, barrier passed) in place over its dZ slab; rows past the slice -> 0
+  f32x2 ca[4], cb[4], cg[4];   // the thread's transform coefficients (loop-invariant), read once below
   auto transform = [&](int s, int sidx) __attribute__((always_inline)) {
     char *st = lds + sidx * F::STAGE;
     const int rem = min(rows - s * MS, MS);
-    f32x2 ca[4], cb[4], cg[4];
-    lds_pairs8(cft, COUT * 2, ca);
-    lds_pairs8(cft + COUT * 4, COUT * 2, cb);
-    lds_pairs8(cft + 2 * COUT * 4, COUT * 2, cg);
 #pragma unroll
     for (int ps = 0; ps < F::TPASS; ++ps) {
       const int r = trow + ps * (THREADS / F::CPR);
@@ -384,6 +381,9 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
   }
   wait_vm<2 + (NST - 2) * (F::VM_STEP + 2)>();
   barrier_lds();
+  lds_pairs8(cft, COUT * 2, ca);
+  lds_pairs8(cft + COUT * 4, COUT * 2, cb);
+  lds_pairs8(cft + 2 * COUT * 4, COUT * 2, cg);
   transform(0, 0);
 
   int sc = 0, sn = 1, sd = NST - 1;   // stages of steps t, t+1 and t+NST-1 (= t-1's)
@@ -535,10 +535,6 @@ void seg4_kernel(pcs_gemm_args a, float *__restrict__ wpart, int64_t rows_per_sp
       tdz[ps] = *reinterpret_cast<const u32x4 *>(stn + o);
       tyy[ps] = *reinterpret_cast<const u32x4 *>(stn + F::DZB + o);
     }
-    f32x2 ca[4], cb[4], cg[4];
-    lds_pairs8(cft, COUT * 2, ca);
-    lds_pairs8(cft + COUT * 4, COUT * 2, cb);
-    lds_pairs8(cft + 2 * COUT * 4, COUT * 2, cg);
     __builtin_amdgcn_sched_barrier(0);
 
     // dz' stores: read s of v^T rows 16 s + 4 g + 0..3 (transposed: lane l16 gets row l16,
