@@ -167,3 +167,38 @@ def test_seg4_no_scratch(seg4_asm):
     scratch = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", seg4_asm)
     assert spills and scratch
     assert all(int(v) == 0 for v in spills + scratch)
+
+
+def test_audit_catches_the_patterns_it_guards():
+    """The parsers above flag what they are meant to flag (synthetic assembly, no compiler)."""
+    moved = """
+;;#ASMSTART
+v_mfma_f32_16x16x32_bf16 v[0:3], v[8:11], v[12:15], 0
+;;#ASMEND
+v_mov_b32_e32 v20, v2
+;;#ASMSTART
+v_mfma_f32_16x16x32_bf16 v[0:3], v[8:11], v[12:15], v[0:3]
+s_nop 7
+s_nop 3
+;;#ASMEND
+"""
+    (groups, between), = list(chains(moved))
+    assert [ln for ln in between if vregs(ln) & vregs(groups[0][0])] == ["v_mov_b32_e32 v20, v2"]
+    fresh = """
+v_add_u32_e32 v9, v1, v2
+;;#ASMSTART
+v_mfma_f32_16x16x32_bf16 v[0:3], v[8:11], v[12:15], 0
+;;#ASMEND
+"""
+    assert operand_hazards(fresh) == [("v_mfma_f32_16x16x32_bf16 v[0:3], v[8:11], v[12:15], 0",
+                                       "v_add_u32_e32 v9, v1, v2")]
+    padded = """
+v_add_u32_e32 v9, v1, v2
+s_waitcnt lgkmcnt(0)
+s_mov_b32 s1, s2
+;;#ASMSTART
+v_mfma_f32_16x16x32_bf16 v[0:3], v[8:11], v[12:15], 0
+;;#ASMEND
+"""
+    assert operand_hazards(padded) == []
+    assert vregs("v_pk_fma_f32 v[70:71], v[198:199], v3, v[190:191]") == {70, 71, 198, 199, 3, 190, 191}
